@@ -1,0 +1,180 @@
+"""Per-rank execution engine: state buffers, integrator stages, halo phases.
+
+One ``Engine`` per rank (one process per GPU, or one virtual rank in-process).
+A time step is the integrator's stage list; each stage is
+
+    transport.start(Q)      pack boundary cells, post P2P messages
+    compute(interior)       HIP: blocks that read no remote ghost
+    recv = transport.finish()
+    compute(boundary)       the remaining blocks (gather from recv)
+
+With ``backend='torch'`` compute is the PyTorch reference (CPU or GPU); with
+``backend='hip'`` it is the fused gfx950 stage kernel (``ops/csrc``), and the
+``NativeRuntime`` can take over the whole step loop (C++ + hipGraph + RCCL).
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .models.base import Physics, RankGeometry, extend
+from .models.geometry import CubedSphereGrid
+from .models.integrators import Integrator, Stage, get_integrator
+from .parallel.comm import NullTransport, Transport
+from .parallel.layout import TileLayout
+
+
+class TorchCompute:
+    """Reference stage computation in PyTorch."""
+
+    def __init__(self, engine: "Engine"):
+        self.e = engine
+
+    def stage(self, st: Stage, dt: float, recv: Optional[torch.Tensor], part: str = "all") -> None:
+        if part == "interior":
+            return  # torch path computes everything in the "boundary" call
+        e = self.e
+        phys = e.physics
+        Q = e.pool[st.Q]
+        X = e.pool[st.X]
+        g = phys.halo
+        qe = extend(Q, recv, e.gmap, e.plan.T, e.plan.n, g)
+        dq = phys.rhs(qe, Q, e.tens, e.plan.n, g).reshape(phys.F, -1)
+        if st.acc_out >= 0:
+            acc = st.c1 * X + (st.c2 * dt) * dq
+            if st.acc_in >= 0 and st.c0 != 0.0:
+                acc = acc + st.c0 * e.pool[st.acc_in]
+            acc = phys.finalize(acc, e.tens)
+        out = st.a2 * dt * dq
+        if st.a1 != 0.0:
+            out = out + st.a1 * Q
+        if st.a0 != 0.0:
+            out = out + st.a0 * X
+        out = phys.finalize(out, e.tens)
+        if st.acc_out >= 0:
+            e.pool[st.acc_out].copy_(acc)
+        e.pool[st.out].copy_(out)
+
+
+class Engine:
+    def __init__(self, physics: Physics, layout: TileLayout, rank: int = 0, grid: Optional[CubedSphereGrid] = None,
+                 dtype=torch.float64, device="cpu", transport: Optional[Transport] = None, backend: str = "torch",
+                 integrator: str = "ssprk3", dt: Optional[float] = None, cfl: float = 0.8, block=(16, 16)):
+        if physics.halo > layout.ng:
+            raise ValueError(f"{physics.name} needs halo {physics.halo} > layout ng {layout.ng}")
+        self.physics = physics
+        self.layout = layout
+        self.rank = rank
+        self.grid = grid or CubedSphereGrid(layout.N)
+        self.dtype = dtype
+        self.device = torch.device(device)
+        self.plan = layout.plan(rank)
+        self.geo = RankGeometry(self.grid, layout, rank)
+        self.tens: Dict[str, torch.Tensor] = physics.setup(self.geo, dtype, self.device)
+        self.gmap = torch.as_tensor(self.plan.ghost_map, device=self.device)
+        self.integ: Integrator = get_integrator(integrator)
+        F, S = physics.F, self.plan.S
+        self.pool: List[torch.Tensor] = [torch.zeros((F, S), dtype=dtype, device=self.device) for _ in range(self.integ.nbuf)]
+        q0 = physics.initial_state(self.geo).reshape(F, S)
+        self.pool[0].copy_(torch.as_tensor(q0, dtype=dtype))
+        self.transport = transport or NullTransport(self.plan, F, dtype, self.device)
+        self.dt = float(dt) if dt is not None else physics.max_dt(self.grid, cfl)
+        self.time = 0.0
+        self.step_count = 0
+        self.backend = backend
+        self.block = tuple(block)
+        if backend == "torch":
+            self.compute = TorchCompute(self)
+        elif backend == "hip":
+            from .ops.hip_compute import HipCompute
+            self.compute = HipCompute(self)
+        else:
+            raise ValueError(f"unknown backend {backend!r}")
+
+    # ---- state ------------------------------------------------------------
+    @property
+    def state(self) -> torch.Tensor:
+        return self.pool[0]
+
+    def set_state(self, q: torch.Tensor) -> None:
+        self.pool[0].copy_(q.reshape(self.pool[0].shape))
+
+    def tiles_view(self, q: Optional[torch.Tensor] = None) -> torch.Tensor:
+        q = self.state if q is None else q
+        return q.view(self.physics.F, self.plan.T, self.plan.n, self.plan.n)
+
+    # ---- stepping -----------------------------------------------------------
+    def stage_begin(self, st: Stage) -> None:
+        self.transport.start(self.pool[st.Q])
+        self.compute.stage(st, self.dt, None, part="interior")
+
+    def stage_end(self, st: Stage) -> None:
+        recv = self.transport.finish()
+        self.compute.stage(st, self.dt, recv, part="boundary")
+
+    def end_step(self) -> None:
+        rot = self.integ.rotation
+        self.pool = [self.pool[r] for r in rot]
+        self.time += self.dt
+        self.step_count += 1
+
+    def step(self, nsteps: int = 1) -> None:
+        for _ in range(nsteps):
+            for st in self.integ.stages:
+                self.stage_begin(st)
+                self.stage_end(st)
+            self.end_step()
+
+    def diagnostics(self) -> Dict[str, float]:
+        d = self.physics.diagnostics(self.state, self.tens)
+        return {k: float(v) for k, v in d.items()}
+
+    def global_field(self, f: int = 0) -> np.ndarray:
+        """Single-rank only: [6, N, N] float64 of field f."""
+        assert self.layout.num_ranks == 1
+        return assemble_global(self.layout, {0: self.tiles_view()[f].detach().cpu().numpy()})
+
+
+def assemble_global(layout: TileLayout, tiles_by_rank: Dict[int, np.ndarray]) -> np.ndarray:
+    """{rank: [T, n, n]} -> [6, N, N]."""
+    N, n = layout.N, layout.n
+    out = np.zeros((6, N, N))
+    for r, arr in tiles_by_rank.items():
+        for li, tid in enumerate(layout.rank_tiles[r]):
+            f, I0, J0 = layout.tile_origin(tid)
+            out[f, J0:J0 + n, I0:I0 + n] = arr[li]
+    return out
+
+
+class VirtualCluster:
+    """All ranks of a layout in one process, stepped in lockstep (the analogue
+    of the reference's CPU virtual devices, PY:64-68)."""
+
+    def __init__(self, physics_factory, layout: TileLayout, **engine_kw):
+        from .parallel.comm import VirtualHub
+        self.layout = layout
+        self.hub = VirtualHub()
+        self.engines: List[Engine] = []
+        for r in range(layout.num_ranks):
+            phys = physics_factory()
+            plan = layout.plan(r)
+            dtype = engine_kw.get("dtype", torch.float64)
+            dev = engine_kw.get("device", "cpu")
+            tr = self.hub.transport(plan, phys.F, dtype, torch.device(dev))
+            self.engines.append(Engine(phys, layout, r, transport=tr, **engine_kw))
+
+    def step(self, nsteps: int = 1) -> None:
+        for _ in range(nsteps):
+            for st in self.engines[0].integ.stages:
+                for e in self.engines:
+                    e.stage_begin(st)
+                for e in self.engines:
+                    e.stage_end(st)
+            for e in self.engines:
+                e.end_step()
+
+    def global_field(self, f: int = 0) -> np.ndarray:
+        return assemble_global(self.layout, {e.rank: e.tiles_view()[f].detach().cpu().numpy() for e in self.engines})

@@ -1,0 +1,216 @@
+"""Physics base class, per-rank geometry, and the PyTorch reference path.
+
+The PyTorch implementation here is the numerical oracle of the framework and
+the ``device_type: cpu`` execution path (the analogue of the reference's CPU
+virtual devices, PY:64-68).  The HIP kernels in ``ops/csrc`` implement the same
+formulas; the GPU tests compare the two.
+
+Finite-volume update (PDF s.4 "Finite Volume (PLR) Method"):
+
+    dq/dt = -(1/A) [F_{i+1/2} - F_{i-1/2} + G_{j+1/2} - G_{j-1/2}] + S(q)
+
+with piecewise-linear (PLR) reconstruction in index space along each grid
+direction, a slope limiter, and physics-specific edge fluxes.  Ghost cells
+come from the per-rank ghost map (``parallel/layout.py``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..parallel.layout import RankPlan, TileLayout
+from .geometry import CubedSphereGrid, arc_angle, tangent_project
+
+LIMITERS = {"none": 0, "central": 0, "minmod": 1, "mc": 2, "vanleer": 3}
+
+
+def limiter_code(name) -> int:
+    if isinstance(name, int):
+        return name
+    try:
+        return LIMITERS[name.lower()]
+    except KeyError:
+        raise ValueError(f"unknown limiter {name!r}; choose from {sorted(LIMITERS)}")
+
+
+class RankGeometry:
+    """Float64 host geometry for the tiles of one rank (numpy)."""
+
+    def __init__(self, grid: CubedSphereGrid, layout: TileLayout, rank: int):
+        self.grid = grid
+        self.layout = layout
+        self.rank = rank
+        self.plan: RankPlan = layout.plan(rank)
+        n, N = layout.n, layout.N
+        tiles = self.plan.tiles
+        self.T = len(tiles)
+        self.n = n
+        A = grid.areas()
+        C = grid.centers()
+        LX = grid.x_edge_lengths()
+        LY = grid.y_edge_lengths()
+        MX = grid.x_edge_normals()
+        MY = grid.y_edge_normals()
+        XM = grid.x_edge_midpoints()
+        YM = grid.y_edge_midpoints()
+        self.area = np.empty((self.T, n, n))
+        self.center = np.empty((self.T, n, n, 3))
+        self.lx = np.empty((self.T, n, n + 1))
+        self.ly = np.empty((self.T, n + 1, n))
+        self.mx = np.empty((self.T, n + 1, 3))
+        self.my = np.empty((self.T, n + 1, 3))
+        self.xmid = np.empty((self.T, n, n + 1, 3))
+        self.ymid = np.empty((self.T, n + 1, n, 3))
+        self.ext1 = np.empty((self.T, n + 2, n + 2), dtype=np.int64)
+        self.face = np.empty(self.T, dtype=np.int64)
+        for li, tid in enumerate(tiles):
+            f, I0, J0 = layout.tile_origin(tid)
+            self.face[li] = f
+            sj, si = slice(J0, J0 + n), slice(I0, I0 + n)
+            self.area[li] = A[f, sj, si]
+            self.center[li] = C[f, sj, si]
+            self.lx[li] = LX[f, sj, I0:I0 + n + 1]
+            self.ly[li] = LY[f, J0:J0 + n + 1, si]
+            self.mx[li] = MX[f, I0:I0 + n + 1]
+            self.my[li] = MY[f, J0:J0 + n + 1]
+            self.xmid[li] = XM[f, sj, I0:I0 + n + 1]
+            self.ymid[li] = YM[f, J0:J0 + n + 1, si]
+            self.ext1[li] = layout.tile_extended_index(tid, 1)
+
+    def gather_global(self, arr_global: np.ndarray) -> np.ndarray:
+        """[6, N, N, ...] global array -> [T, n, n, ...] local tiles."""
+        n = self.n
+        out = np.empty((self.T, n, n) + arr_global.shape[3:], dtype=arr_global.dtype)
+        for li, tid in enumerate(self.plan.tiles):
+            f, I0, J0 = self.layout.tile_origin(tid)
+            out[li] = arr_global[f, J0:J0 + n, I0:I0 + n]
+        return out
+
+    def neighbor_values(self, arr_global: np.ndarray) -> np.ndarray:
+        """[T, n+2, n+2, ...] one-ring extended values from a global array."""
+        flat = arr_global.reshape((-1,) + arr_global.shape[3:])
+        idx = np.where(self.ext1 >= 0, self.ext1, 0)
+        return flat[idx]
+
+    def center_distances(self):
+        """Great-circle distances between the true cell centres on both sides
+        of every x-edge [T,n,n+1] and y-edge [T,n+1,n] (across panels too)."""
+        ce = self.neighbor_values(self.grid.centers())
+        n = self.n
+        dx = arc_angle(ce[:, 1:n + 1, 0:n + 1], ce[:, 1:n + 1, 1:n + 2]) * self.grid.radius
+        dy = arc_angle(ce[:, 0:n + 1, 1:n + 1], ce[:, 1:n + 2, 1:n + 1]) * self.grid.radius
+        return dx, dy
+
+    def fv_gradient(self, arr_global: np.ndarray) -> np.ndarray:
+        """Tangent FV gradient [T,n,n,3] of a global scalar: Gauss sum of
+        (edge average - cell value) m L / A (balanced: constant -> 0)."""
+        ve = self.neighbor_values(arr_global)
+        n = self.n
+        c = ve[:, 1:n + 1, 1:n + 1]
+        bx = 0.5 * (ve[:, 1:n + 1, 0:n + 1] + ve[:, 1:n + 1, 1:n + 2])   # [T,n,n+1]
+        by = 0.5 * (ve[:, 0:n + 1, 1:n + 1] + ve[:, 1:n + 2, 1:n + 1])   # [T,n+1,n]
+        fx = (bx[..., None] * self.lx[..., None]) * self.mx[:, None, :, :]
+        fy = (by[..., None] * self.ly[..., None]) * self.my[:, :, None, :]
+        s = (fx[:, :, 1:] - fx[:, :, :-1]) + (fy[:, 1:] - fy[:, :-1])
+        mlx = self.lx[..., None] * self.mx[:, None, :, :]
+        mly = self.ly[..., None] * self.my[:, :, None, :]
+        S = (mlx[:, :, 1:] - mlx[:, :, :-1]) + (mly[:, 1:] - mly[:, :-1])
+        grad = (s - c[..., None] * S) / self.area[..., None]
+        return tangent_project(grad, self.center)
+
+
+# ----------------------------------------------------------------------------
+# Torch reference helpers
+# ----------------------------------------------------------------------------
+
+def extend(q: torch.Tensor, recv: Optional[torch.Tensor], gmap: torch.Tensor, T: int, n: int, g: int,
+           ng_map: Optional[int] = None) -> torch.Tensor:
+    """q [F, T*n*n] + recv [R, F] -> extended [F, T, n+2g, n+2g]; cube-corner
+    (and tile-corner) ghost blocks are zero (never read by the stencils).
+    ``gmap`` is the [T, 4, ng_map, n] ghost map; only its first g layers are used."""
+    F = q.shape[0]
+    qe = q.new_zeros((F, T, n + 2 * g, n + 2 * g))
+    qe[:, :, g:g + n, g:g + n] = q.view(F, T, n, n)
+    gm = gmap[:, :, :g, :].long()
+    loc = gm >= 0
+    vals = q[:, gm.clamp(min=0)]                               # [F,T,4,g,n]
+    if recv is not None and recv.numel() > 0:
+        rv = recv[(-1 - gm).clamp(min=0)].permute(4, 0, 1, 2, 3)  # [F,T,4,g,n]
+        vals = torch.where(loc.unsqueeze(0), vals, rv)
+    for k in range(g):
+        qe[:, :, g:g + n, g - 1 - k] = vals[:, :, 0, k, :]
+        qe[:, :, g:g + n, g + n + k] = vals[:, :, 1, k, :]
+        qe[:, :, g - 1 - k, g:g + n] = vals[:, :, 2, k, :]
+        qe[:, :, g + n + k, g:g + n] = vals[:, :, 3, k, :]
+    return qe
+
+
+def limited_slope(dl: torch.Tensor, dr: torch.Tensor, lim: int) -> torch.Tensor:
+    if lim == 0:
+        return 0.5 * (dl + dr)
+    same = dl * dr > 0
+    if lim == 1:
+        return torch.where(same, torch.sign(dl) * torch.minimum(dl.abs(), dr.abs()), torch.zeros_like(dl))
+    if lim == 2:
+        c = 0.5 * (dl + dr)
+        m = torch.minimum(torch.minimum(2 * dl.abs(), 2 * dr.abs()), c.abs())
+        return torch.where(same, torch.sign(c) * m, torch.zeros_like(dl))
+    if lim == 3:
+        return torch.where(same, 2 * dl * dr / torch.where(same, dl + dr, torch.ones_like(dl)), torch.zeros_like(dl))
+    raise ValueError(lim)
+
+
+def plr_x(qe: torch.Tensor, g: int, n: int, lim: int):
+    """Left/right PLR states at the n+1 x-edges of the interior rows:
+    returns (qL, qR) each [..., n, n+1]."""
+    rows = qe[..., g:g + n, :]
+    d = rows[..., 1:] - rows[..., :-1]
+    s = limited_slope(d[..., g - 2:g + n], d[..., g - 1:g + n + 1], lim)
+    c = rows[..., g - 1:g + n + 1]
+    return (c + 0.5 * s)[..., :-1], (c - 0.5 * s)[..., 1:]
+
+
+def plr_y(qe: torch.Tensor, g: int, n: int, lim: int):
+    """(qL, qR) each [..., n+1, n] at the y-edges of the interior columns."""
+    qL, qR = plr_x(qe.transpose(-1, -2), g, n, lim)
+    return qL.transpose(-1, -2), qR.transpose(-1, -2)
+
+
+class Physics:
+    """Base class.  Subclasses define fields, halo need and the reference RHS."""
+
+    name = "base"
+    kernel_id = -1
+    fields: List[str] = []
+    halo = 2
+
+    @property
+    def F(self) -> int:
+        return len(self.fields)
+
+    def setup(self, geo: RankGeometry, dtype: torch.dtype, device) -> Dict[str, torch.Tensor]:
+        raise NotImplementedError
+
+    def initial_state(self, geo: RankGeometry) -> np.ndarray:
+        """[F, T, n, n] float64."""
+        raise NotImplementedError
+
+    def rhs(self, qe: torch.Tensor, q: torch.Tensor, tens: Dict[str, torch.Tensor], n: int, g: int) -> torch.Tensor:
+        raise NotImplementedError
+
+    def finalize(self, out: torch.Tensor, tens: Dict[str, torch.Tensor]) -> torch.Tensor:
+        return out
+
+    def kernel_params(self) -> Dict[str, float]:
+        return {}
+
+    def max_dt(self, grid: CubedSphereGrid, cfl: float = 0.8) -> float:
+        raise NotImplementedError
+
+    def diagnostics(self, q: torch.Tensor, tens: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """Per-rank partial sums (to be all-reduced)."""
+        area = tens["area"].reshape(-1)
+        return {"mass": (q[0] * area).sum()}

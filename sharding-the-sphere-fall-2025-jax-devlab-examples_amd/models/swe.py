@@ -1,0 +1,149 @@
+"""Shallow-water equations on the cubed sphere (PY:2 "FV Cubed-Sphere Shallow
+Water Solver").
+
+Formulation (chosen here; the reference does not show one):
+
+* state per cell: depth h and **Cartesian momentum** M = h v (3 components),
+  panel-invariant, so halos need no basis rotation (PDF s.18, "Cartesian
+  Velocity Exchange");
+* flux form  d(h, M)/dt + div(h v, M v + g h^2/2 I) = S,  FV with PLR on the
+  primitive variables (h, v) and a Rusanov (local Lax-Friedrichs) edge flux
+  along the exact great-circle edge normals;
+* sources: Coriolis  -f r x M  (f = 2 Omega z/R), topography  -g h grad b, and
+  the curvature balance  +g h_c^2 / 2 * (sum m L) / A, which makes a constant
+  depth exactly force-free on the curved cell;
+* after each stage M is projected onto the tangent plane at the cell centre
+  (removes the radial "constraint force" of motion on the sphere).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict
+
+import numpy as np
+import torch
+
+from .base import Physics, RankGeometry, limited_slope, plr_x, plr_y
+from .geometry import GRAVITY, OMEGA, CubedSphereGrid
+from . import initial_conditions as ic
+
+
+class ShallowWater(Physics):
+    name = "swe"
+    kernel_id = 2
+    fields = ["h", "mx", "my", "mz"]
+    halo = 2
+
+    def __init__(self, case: str = "tc5", limiter: int = 2, g: float = GRAVITY, omega: float = OMEGA,
+                 alpha: float = 0.0):
+        self.case = case
+        self.limiter = limiter
+        self.g = g
+        self.omega = omega
+        self.alpha = alpha
+        self._b_global = None
+
+    # ---- initial conditions --------------------------------------------
+    def global_fields(self, grid: CubedSphereGrid):
+        p = grid.centers()
+        if self.case == "tc2":
+            h, wind, b = ic.williamson_tc2(p, alpha=self.alpha, radius=grid.radius, omega=self.omega, g=self.g)
+        elif self.case == "tc5":
+            h, wind, b = ic.williamson_tc5(p, radius=grid.radius, omega=self.omega, g=self.g)
+        elif self.case == "tc6":
+            h, wind, b = ic.williamson_tc6(p, radius=grid.radius, omega=self.omega, g=self.g)
+        elif self.case == "rest":
+            h = np.full(p.shape[:-1], 1000.0)
+            wind = np.zeros(p.shape)
+            b = np.zeros(p.shape[:-1])
+        else:
+            raise ValueError(f"unknown SWE case {self.case!r}")
+        return h, wind, b
+
+    def initial_state(self, geo: RankGeometry) -> np.ndarray:
+        h, wind, b = self.global_fields(geo.grid)
+        hl = geo.gather_global(h)
+        wl = geo.gather_global(wind)
+        q = np.empty((4,) + hl.shape)
+        q[0] = hl
+        q[1:] = np.moveaxis(hl[..., None] * wl, -1, 0)
+        return q
+
+    # ---- geometry ---------------------------------------------------------
+    def setup(self, geo: RankGeometry, dtype, device) -> Dict[str, torch.Tensor]:
+        _, _, b = self.global_fields(geo.grid)
+        gb = geo.fv_gradient(b)
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=device)
+        return {
+            "area": t(geo.area),
+            "invA": t(1.0 / geo.area),
+            "ex": t(geo.lx),
+            "ey": t(geo.ly),
+            "mx": t(np.moveaxis(geo.mx, -1, 1)),           # [T,3,n+1]
+            "my": t(np.moveaxis(geo.my, -1, 1)),
+            "ctr": t(np.moveaxis(geo.center, -1, 0)),      # [3,T,n,n]
+            "gradb": t(np.moveaxis(gb, -1, 0)),            # [3,T,n,n]
+            "b": t(geo.gather_global(b)),
+        }
+
+    def kernel_params(self):
+        return {"g": self.g, "omega2": 2.0 * self.omega, "limiter": self.limiter}
+
+    # ---- reference RHS ------------------------------------------------------
+    def _flux(self, wL, wR, m, L):
+        g = self.g
+        hL, hR = wL[0], wR[0]
+        vL, vR = wL[1:], wR[1:]
+        vnL = (vL * m).sum(0)
+        vnR = (vR * m).sum(0)
+        c = torch.maximum(vnL.abs() + torch.sqrt(g * hL), vnR.abs() + torch.sqrt(g * hR))
+        Fh = 0.5 * (hL * vnL + hR * vnR) - 0.5 * c * (hR - hL)
+        Fm = 0.5 * (hL * vL * vnL + hR * vR * vnR + 0.5 * g * (hL * hL + hR * hR) * m) - 0.5 * c * (hR * vR - hL * vL)
+        return torch.cat([Fh[None], Fm], 0) * L
+
+    def rhs(self, qe, q, tens, n, g):
+        F, T = qe.shape[0], qe.shape[1]
+        h = qe[0]
+        safe = torch.where(h != 0, h, torch.ones_like(h))
+        w = torch.stack([h, qe[1] / safe, qe[2] / safe, qe[3] / safe])
+        lim = self.limiter
+        wL, wR = plr_x(w, g, n, lim)                                  # [4,T,n,n+1]
+        mx = tens["mx"].permute(1, 0, 2)[:, :, None, :]              # [3,T,1,n+1]
+        Fx = self._flux(wL, wR, mx, tens["ex"])
+        wL, wR = plr_y(w, g, n, lim)                                  # [4,T,n+1,n]
+        my = tens["my"].permute(1, 0, 2)[:, :, :, None]              # [3,T,n+1,1]
+        Gy = self._flux(wL, wR, my, tens["ey"])
+        invA = tens["invA"]
+        dq = -((Fx[..., 1:] - Fx[..., :-1]) + (Gy[..., 1:, :] - Gy[..., :-1, :])) * invA
+        hc = q[0].view(T, n, n)
+        M = q[1:4].view(3, T, n, n)
+        r = tens["ctr"]
+        f = self.omega * 2.0 * r[2]
+        cor = torch.stack([r[1] * M[2] - r[2] * M[1], r[2] * M[0] - r[0] * M[2], r[0] * M[1] - r[1] * M[0]])
+        lx, ly = tens["ex"], tens["ey"]
+        S = (lx[None, :, :, 1:] * mx[..., 1:] - lx[None, :, :, :-1] * mx[..., :-1]
+             + ly[None, :, 1:, :] * my[:, :, 1:, :] - ly[None, :, :-1, :] * my[:, :, :-1, :])
+        dq[1:] += -f * cor + (0.5 * self.g * hc * hc * invA) * S - self.g * hc * tens["gradb"]
+        return dq
+
+    def finalize(self, out, tens):
+        F = out.shape[0]
+        r = tens["ctr"].reshape(3, -1)
+        M = out[1:4]
+        d = (M * r).sum(0)
+        out[1:4] = M - d * r
+        return out
+
+    def max_dt(self, grid: CubedSphereGrid, cfl: float = 0.8) -> float:
+        h, wind, b = self.global_fields(grid)
+        speed = np.linalg.norm(wind, axis=-1) + np.sqrt(self.g * np.maximum(h, 0))
+        return cfl * grid.min_spacing() / float(speed.max())
+
+    def diagnostics(self, q, tens):
+        A = tens["area"].reshape(-1)
+        h = q[0]
+        M = q[1:4]
+        b = tens["b"].reshape(-1)
+        ke = 0.5 * (M * M).sum(0) / h
+        pe = 0.5 * self.g * h * h + self.g * h * b
+        return {"mass": (h * A).sum(), "energy": ((ke + pe) * A).sum()}

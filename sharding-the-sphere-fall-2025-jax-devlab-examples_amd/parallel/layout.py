@@ -1,0 +1,242 @@
+"""Tile layout and per-rank halo plans (the "Communication Scheduler" box of
+PDF s.7, generalised beyond the reference's fixed 6-face table).
+
+Storage model: every rank holds, per field, its tiles packed
+tile-major **without ghost padding**: ``q[field, tile_local * n*n + j*n + i]``.
+Ghost values are never stored in the state; kernels gather them on the fly
+through a per-rank ghost map:
+
+    ghost_map[tile_local, side, layer, pos] =  k >= 0   -> q[f, k]           (same rank)
+                                               -1 - s   -> recv[s, f]         (remote slot s)
+
+with side 0 = W (x < 0), 1 = E (x >= n), 2 = S (y < 0), 3 = N (y >= n), layer
+0 nearest the tile edge, pos the index along the edge.  Cross-panel
+orientation (the reference's "T"/"R"/"TR" ops, PY:143-163) is folded into the
+map, for any halo width ng.
+
+Remote ghost values arrive in ``recv`` (slot-major, fields interleaved:
+``recv[slot * F + f]``), one contiguous segment per peer, filled by one RCCL /
+gloo message per peer per exchange (bundle per peer).  The
+sender packs ``send[k * F + f] = q[f, send_idx[k]]`` in the order the receiver
+expects; both sides derive that order from the same deterministic enumeration,
+so no index lists are exchanged at run time.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from functools import cached_property
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .partition import partition_tiles, tile_coords, tile_id, tiles_of, validate_device_count
+from .topology import neighbor_cells
+
+SIDES = ("W", "E", "S", "N")
+
+
+def ghost_xy(side: int, layer: int, pos: np.ndarray, n: int):
+    """Tile-extended coordinates of ghost cells."""
+    if side == 0:
+        return np.full_like(pos, -1 - layer), pos
+    if side == 1:
+        return np.full_like(pos, n + layer), pos
+    if side == 2:
+        return pos, np.full_like(pos, -1 - layer)
+    return pos, np.full_like(pos, n + layer)
+
+
+class TileLayout:
+    """Global tiling of a C<N> cubed sphere into 6 t^2 tiles over `num_ranks`."""
+
+    def __init__(self, N: int, tiles_per_edge: int = 1, num_ranks: int = 1, ng: int = 2,
+                 partition: str = "auto", owner: Optional[Sequence[int]] = None):
+        if N % tiles_per_edge:
+            raise ValueError(f"N = {N} is not divisible by tiles_per_edge = {tiles_per_edge}")
+        validate_device_count(num_ranks, tiles_per_edge)
+        self.N = N
+        self.t = tiles_per_edge
+        self.n = N // tiles_per_edge
+        self.ng = ng
+        if ng > self.n:
+            raise ValueError(f"halo width ng = {ng} exceeds tile size n = {self.n}")
+        self.num_ranks = num_ranks
+        self.partition = partition
+        self.owner = list(owner) if owner is not None else partition_tiles(tiles_per_edge, num_ranks, partition)
+        self.num_tiles = 6 * tiles_per_edge ** 2
+        self.rank_tiles: List[List[int]] = [tiles_of(self.owner, r) for r in range(num_ranks)]
+        self.local_index: Dict[int, Tuple[int, int]] = {}
+        for r, tl in enumerate(self.rank_tiles):
+            for li, tid in enumerate(tl):
+                self.local_index[tid] = (r, li)
+        self._plans: Dict[int, "RankPlan"] = {}
+        self._cache: Dict = {}
+        self._owner_arr = np.asarray(self.owner, dtype=np.int64)
+        self._local_arr = np.zeros(self.num_tiles, dtype=np.int64)
+        for tid, (_, li) in self.local_index.items():
+            self._local_arr[tid] = li
+
+    # ---- global cell addressing ------------------------------------------
+    def tile_origin(self, tid: int) -> Tuple[int, int, int]:
+        f, ti, tj = tile_coords(tid, self.t)
+        return f, ti * self.n, tj * self.n
+
+    def global_flat(self, face, I, J):
+        return (face * self.N + J) * self.N + I
+
+    def tile_extended_index(self, tid: int, ng: Optional[int] = None) -> np.ndarray:
+        """[n+2g, n+2g] global flat cell index of every cell in the tile's
+        extended (ghosted) window; -1 where undefined (cube-corner ghosts).
+        Corner ghosts inside a face (4 tiles meeting) are defined."""
+        g = self.ng if ng is None else ng
+        n = self.n
+        f, I0, J0 = self.tile_origin(tid)
+        yy, xx = np.mgrid[-g:n + g, -g:n + g]
+        F, I2, J2 = neighbor_cells(self.N, f, I0 + xx, J0 + yy)
+        return np.where(F >= 0, self.global_flat(F, I2, J2), -1)
+
+    def locate(self, gflat: np.ndarray):
+        """global flat -> (tile_id, i, j)."""
+        N, n, t = self.N, self.n, self.t
+        face, rem = np.divmod(gflat, N * N)
+        J, I = np.divmod(rem, N)
+        tid = face * t * t + (J // n) * t + (I // n)
+        return tid, I % n, J % n
+
+    # ---- per-rank plans ---------------------------------------------------
+    def plan(self, rank: int) -> "RankPlan":
+        if rank not in self._plans:
+            self._plans[rank] = RankPlan(self, rank)
+        return self._plans[rank]
+
+    def ghost_sources(self, rank: int) -> np.ndarray:
+        """[T, 4, ng, n] global flat index of the source cell of every ghost."""
+        key = ("gs", rank)
+        if key in self._cache:
+            return self._cache[key]
+        tiles = self.rank_tiles[rank]
+        n, g = self.n, self.ng
+        out = np.empty((len(tiles), 4, g, n), dtype=np.int64)
+        pos = np.arange(n)
+        for li, tid in enumerate(tiles):
+            f, I0, J0 = self.tile_origin(tid)
+            for s in range(4):
+                for k in range(g):
+                    x, y = ghost_xy(s, k, pos, n)
+                    F, I2, J2 = neighbor_cells(self.N, f, I0 + x, J0 + y)
+                    out[li, s, k] = self.global_flat(F, I2, J2)
+        assert (out >= 0).all()
+        self._cache[key] = out
+        return out
+
+    def needs(self, rank: int, peer: int) -> np.ndarray:
+        """Ordered unique global cells owned by `peer` that `rank` reads as
+        ghosts (first-occurrence order of rank's ghost enumeration)."""
+        src = self.ghost_sources(rank).reshape(-1)
+        tid, _, _ = self.locate(src)
+        own = np.asarray(self.owner)[tid]
+        sel = src[own == peer]
+        _, first = np.unique(sel, return_index=True)
+        return sel[np.sort(first)]
+
+    def local_flat(self, gflat: np.ndarray) -> np.ndarray:
+        tid, i, j = self.locate(gflat)
+        li = self._local_arr[tid]
+        return (li * self.n + j) * self.n + i
+
+
+@dataclass
+class RankPlan:
+    layout: TileLayout
+    rank: int
+
+    def __post_init__(self):
+        L = self.layout
+        self.tiles = list(L.rank_tiles[self.rank])
+        self.T = len(self.tiles)
+        self.n = L.n
+        self.ng = L.ng
+        self.S = self.T * self.n * self.n
+        src = L.ghost_sources(self.rank)
+        tid, _, _ = L.locate(src)
+        own = np.asarray(L.owner)[tid]
+        gmap = np.empty(src.shape, dtype=np.int64)
+        local = own == self.rank
+        if local.any():
+            gmap[local] = L.local_flat(src[local])
+        # remote: recv slots, peers in ascending order
+        self.recv_peers: List[int] = sorted(int(p) for p in np.unique(own[~local]))
+        self.recv_counts: List[int] = []
+        self.recv_offsets: List[int] = []
+        off = 0
+        for p in self.recv_peers:
+            need = L.needs(self.rank, p)
+            m = own == p
+            sorter = np.argsort(need)
+            k = sorter[np.searchsorted(need[sorter], src[m])]
+            gmap[m] = -1 - (off + k)
+            self.recv_offsets.append(off)
+            self.recv_counts.append(len(need))
+            off += len(need)
+        self.num_recv = off
+        self.ghost_map = gmap.astype(np.int32)
+        # send lists: what each peer needs from us, in the peer's order
+        self.send_peers: List[int] = []
+        self.send_counts: List[int] = []
+        self.send_offsets: List[int] = []
+        idx = []
+        off = 0
+        for p in range(L.num_ranks):
+            if p == self.rank:
+                continue
+            need = L.needs(p, self.rank)
+            if len(need) == 0:
+                continue
+            self.send_peers.append(p)
+            self.send_counts.append(len(need))
+            self.send_offsets.append(off)
+            idx.append(L.local_flat(need))
+            off += len(need)
+        self.num_send = off
+        self.send_idx = (np.concatenate(idx) if idx else np.zeros(0, dtype=np.int64)).astype(np.int32)
+
+    @property
+    def peers(self) -> List[int]:
+        return sorted(set(self.recv_peers) | set(self.send_peers))
+
+    def tile_has_remote(self) -> np.ndarray:
+        """[T, 4] True where a tile side reads any remote ghost."""
+        return (self.ghost_map < 0).any(axis=(2, 3))
+
+    def block_classes(self, bx: int, by: int) -> Tuple[np.ndarray, np.ndarray]:
+        """Split the (tile, block_y, block_x) work items of a bx x by block
+        decomposition into (interior, boundary): boundary blocks read at least
+        one remote ghost cell (within `ng` of the block) and must wait for the
+        exchange; interior blocks can run while messages are in flight.
+        Returns two int32 arrays of linear block ids t*(nby*nbx) + yb*nbx + xb."""
+        n, g = self.n, self.ng
+        nbx = (n + bx - 1) // bx
+        nby = (n + by - 1) // by
+        rem = self.ghost_map < 0  # [T,4,g,n]
+        interior, boundary = [], []
+        for t in range(self.T):
+            for yb in range(nby):
+                y0, y1 = yb * by, min(n, (yb + 1) * by)
+                for xb in range(nbx):
+                    x0, x1 = xb * bx, min(n, (xb + 1) * bx)
+                    r = False
+                    if x0 < g and rem[t, 0, : g - x0, y0:y1].any():
+                        r = True
+                    if x1 > n - g and rem[t, 1, : x1 - (n - g), y0:y1].any():
+                        r = True
+                    if y0 < g and rem[t, 2, : g - y0, x0:x1].any():
+                        r = True
+                    if y1 > n - g and rem[t, 3, : y1 - (n - g), x0:x1].any():
+                        r = True
+                    bid = (t * nby + yb) * nbx + xb
+                    (boundary if r else interior).append(bid)
+        return np.asarray(interior, dtype=np.int32), np.asarray(boundary, dtype=np.int32)
+
+    def summary(self) -> str:
+        return (f"rank {self.rank}: tiles {self.tiles}, recv {dict(zip(self.recv_peers, self.recv_counts))}, "
+                f"send {dict(zip(self.send_peers, self.send_counts))}")
