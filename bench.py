@@ -1,0 +1,156 @@
+#!/usr/bin/env python
+"""Headline benchmark: cell-updates/s (whole node) of the cubed-sphere
+shallow-water solver at C96 (BASELINE.json metric), plus simulated-days/day.
+
+Flagship step: Williamson TC5 (zonal flow over a mountain; synthetic initial
+condition, nothing downloaded), C96 = 6 x 96^2 cells, float64, SSP-RK3 (3 fused
+gfx950 stage kernels per step), 24 tiles of 48^2 (tiles_per_edge = 2) so the
+same decomposition runs on 1, 2, 4 and 8 GPUs (corner partition: a rank owns
+the 3 face-quadrants around each cube vertex it holds).  Strong scaling: the
+C96 problem is fixed as N grows.
+
+    python bench.py                         # 1 GPU
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Rank 0 prints one JSON line.  The timed region is exactly K full time steps
+(every RK stage, every halo exchange) bracketed by barrier + synchronize; the
+time is the max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+BASELINE_CUPS = 2.6e8   # derived FV-PLR roofline cell-updates/s (900 GB/s device)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--N", type=int, default=96)
+    ap.add_argument("--tiles-per-edge", type=int, default=2)
+    ap.add_argument("--case", default="tc5")
+    ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
+    ap.add_argument("--integrator", default="ssprk3")
+    ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--runtime", default="auto", choices=["auto", "native", "graph", "eager"])
+    ap.add_argument("--steps-per-graph", type=int, default=30)
+    ap.add_argument("--partition", default="auto")
+    ap.add_argument("--dt", type=float, default=None)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    from stsphere.engine import Engine, GraphStepper
+    from stsphere.models.geometry import CubedSphereGrid, DAY
+    from stsphere.models.swe import ShallowWater
+    from stsphere.parallel.comm import TorchDistTransport
+    from stsphere.parallel.layout import TileLayout
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus > 1 needs a torch.distributed launch (one process per GPU)")
+    cuda = torch.cuda.is_available() and a.backend == "hip" or (torch.cuda.is_available() and a.backend == "torch")
+    device = torch.device(f"cuda:{local}") if torch.cuda.is_available() else torch.device("cpu")
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl" if device.type == "cuda" else "gloo", device_id=device if device.type == "cuda" else None)
+    dtype = torch.float64 if a.dtype == "fp64" else torch.float32
+    layout = TileLayout(a.N, a.tiles_per_edge, world, ng=2, partition=a.partition)
+    grid = CubedSphereGrid(a.N)
+    phys = ShallowWater(a.case)
+    transport = None
+    if world > 1:
+        transport = TorchDistTransport(layout.plan(rank), phys.F, dtype, device)
+    backend = a.backend if device.type == "cuda" else "torch"
+    eng = Engine(phys, layout, rank, grid=grid, dtype=dtype, device=device, transport=transport,
+                 backend=backend, integrator=a.integrator, dt=a.dt)
+
+    runtime = a.runtime
+    if runtime == "auto":
+        runtime = "graph" if (device.type == "cuda" and world == 1) else "eager"
+    runner = None
+    if runtime == "graph":
+        runner = GraphStepper(eng, a.steps_per_graph)
+        step = runner.run
+    else:
+        step = eng.step
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+
+    step(a.warmup)
+    sync()
+    t0 = time.perf_counter()
+    step(a.steps)
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    diag = eng.diagnostics()
+    finite = bool(torch.isfinite(eng.state).all().item())
+    cells = 6 * a.N * a.N
+    cups = cells * a.steps / elapsed
+    sdpd = (a.steps * eng.dt / DAY) / (elapsed / DAY)
+    if rank == 0:
+        out = {
+            "metric": "cell-updates/sec (whole node) at C96",
+            "value": cups,
+            "unit": "cell-updates/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": 1e3 * elapsed / a.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": cups / BASELINE_CUPS,
+            "dtype": "fp64" if dtype == torch.float64 else "fp32",
+            "data": "synthetic (Williamson TC5 initial condition, random-free analytic fields)",
+            "config": {
+                "model": f"cubed-sphere shallow water, Williamson {a.case.upper()}, C{a.N}, SSP-RK3 FV-PLR (MC limiter, Rusanov)",
+                "global_batch": 1,
+                "seq_len": cells,
+                "parallelism": f"tiles{layout.num_tiles}-dev{world} ({layout.partition} partition)",
+                "N": a.N,
+                "tiles_per_edge": a.tiles_per_edge,
+                "integrator": a.integrator,
+                "dt_s": eng.dt,
+                "backend": backend,
+                "runtime": runtime,
+            },
+            "simulated_days_per_day": sdpd,
+            "finite": finite,
+            "mass": diag.get("mass"),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

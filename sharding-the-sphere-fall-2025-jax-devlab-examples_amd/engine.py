@@ -20,7 +20,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from .models.base import Physics, RankGeometry, extend
+from .models.base import Physics, RankGeometry, extend, interior
 from .models.geometry import CubedSphereGrid
 from .models.integrators import Integrator, Stage, get_integrator
 from .parallel.comm import NullTransport, Transport
@@ -39,30 +39,31 @@ class TorchCompute:
         e = self.e
         phys = e.physics
         Q = e.pool[st.Q]
-        X = e.pool[st.X]
         g = phys.halo
         qe = extend(Q, recv, e.gmap, e.plan.T, e.plan.n, g)
-        dq = phys.rhs(qe, Q, e.tens, e.plan.n, g).reshape(phys.F, -1)
+        Qi = e.interior(Q)
+        Xi = e.interior(e.pool[st.X])
+        dq = phys.rhs(qe, Qi, e.tens, e.plan.n, g)
         if st.acc_out >= 0:
-            acc = st.c1 * X + (st.c2 * dt) * dq
+            acc = st.c1 * Xi + (st.c2 * dt) * dq
             if st.acc_in >= 0 and st.c0 != 0.0:
-                acc = acc + st.c0 * e.pool[st.acc_in]
+                acc = acc + st.c0 * e.interior(e.pool[st.acc_in])
             acc = phys.finalize(acc, e.tens)
         out = st.a2 * dt * dq
         if st.a1 != 0.0:
-            out = out + st.a1 * Q
+            out = out + st.a1 * Qi
         if st.a0 != 0.0:
-            out = out + st.a0 * X
+            out = out + st.a0 * Xi
         out = phys.finalize(out, e.tens)
         if st.acc_out >= 0:
-            e.pool[st.acc_out].copy_(acc)
-        e.pool[st.out].copy_(out)
+            e.interior(e.pool[st.acc_out]).copy_(acc)
+        e.interior(e.pool[st.out]).copy_(out)
 
 
 class Engine:
     def __init__(self, physics: Physics, layout: TileLayout, rank: int = 0, grid: Optional[CubedSphereGrid] = None,
                  dtype=torch.float64, device="cpu", transport: Optional[Transport] = None, backend: str = "torch",
-                 integrator: str = "ssprk3", dt: Optional[float] = None, cfl: float = 0.8, block=(16, 16)):
+                 integrator: str = "ssprk3", dt: Optional[float] = None, cfl: Optional[float] = None, block=(16, 16)):
         if physics.halo > layout.ng:
             raise ValueError(f"{physics.name} needs halo {physics.halo} > layout ng {layout.ng}")
         self.physics = physics
@@ -77,11 +78,13 @@ class Engine:
         self.gmap = torch.as_tensor(self.plan.ghost_map, device=self.device)
         self.integ: Integrator = get_integrator(integrator)
         F, S = physics.F, self.plan.S
+        # padded storage, zero-initialised (corner ghost blocks stay 0 forever)
         self.pool: List[torch.Tensor] = [torch.zeros((F, S), dtype=dtype, device=self.device) for _ in range(self.integ.nbuf)]
-        q0 = physics.initial_state(self.geo).reshape(F, S)
-        self.pool[0].copy_(torch.as_tensor(q0, dtype=dtype))
+        self.halo_src = torch.as_tensor(self.plan.halo_src, dtype=torch.long, device=self.device)
+        self.halo_dst = torch.as_tensor(self.plan.halo_dst, dtype=torch.long, device=self.device)
         self.transport = transport or NullTransport(self.plan, F, dtype, self.device)
-        self.dt = float(dt) if dt is not None else physics.max_dt(self.grid, cfl)
+        self.set_state(torch.as_tensor(physics.initial_state(self.geo), dtype=dtype))
+        self.dt = float(dt) if dt is not None else (physics.max_dt(self.grid) if cfl is None else physics.max_dt(self.grid, cfl))
         self.time = 0.0
         self.step_count = 0
         self.backend = backend
@@ -99,12 +102,24 @@ class Engine:
     def state(self) -> torch.Tensor:
         return self.pool[0]
 
+    def interior(self, q: torch.Tensor) -> torch.Tensor:
+        """[F, S] padded buffer -> [F, T, n, n] interior view."""
+        return interior(q, self.plan.T, self.plan.n, self.plan.ng)
+
     def set_state(self, q: torch.Tensor) -> None:
-        self.pool[0].copy_(q.reshape(self.pool[0].shape))
+        """q: [F, T, n, n] interior values (any device); refreshes the halos."""
+        self.interior(self.pool[0]).copy_(q.reshape(self.physics.F, self.plan.T, self.plan.n, self.plan.n))
+        self.refresh_halos(self.pool[0])
+
+    def refresh_halos(self, q: torch.Tensor) -> None:
+        """Fill the same-rank ghost slots of a padded buffer from their source
+        cells (the HIP stages keep them current by pushing; needed after any
+        external write of the state)."""
+        if self.halo_src.numel():
+            q[:, self.halo_dst] = q[:, self.halo_src]
 
     def tiles_view(self, q: Optional[torch.Tensor] = None) -> torch.Tensor:
-        q = self.state if q is None else q
-        return q.view(self.physics.F, self.plan.T, self.plan.n, self.plan.n)
+        return self.interior(self.state if q is None else q)
 
     # ---- stepping -----------------------------------------------------------
     def stage_begin(self, st: Stage) -> None:
@@ -129,13 +144,52 @@ class Engine:
             self.end_step()
 
     def diagnostics(self) -> Dict[str, float]:
-        d = self.physics.diagnostics(self.state, self.tens)
+        d = self.physics.diagnostics(self.tiles_view(), self.tens)
         return {k: float(v) for k, v in d.items()}
 
     def global_field(self, f: int = 0) -> np.ndarray:
         """Single-rank only: [6, N, N] float64 of field f."""
         assert self.layout.num_ranks == 1
         return assemble_global(self.layout, {0: self.tiles_view()[f].detach().cpu().numpy()})
+
+
+class GraphStepper:
+    """Capture `k` whole time steps (a multiple of the integrator's buffer
+    period) of a GPU engine into one HIP graph and replay it: removes the host
+    launch overhead that dominates small grids."""
+
+    def __init__(self, engine: Engine, steps_per_graph: int = 10, warmup: bool = True):
+        self.e = engine
+        p = engine.integ.period
+        self.k = max(p, ((steps_per_graph + p - 1) // p) * p)
+        self.stream = torch.cuda.Stream(device=engine.device)
+        t0, c0, pool0 = engine.time, engine.step_count, list(engine.pool)
+        saved = [b.clone() for b in engine.pool]
+        self.stream.wait_stream(torch.cuda.current_stream(engine.device))
+        if warmup:
+            with torch.cuda.stream(self.stream):
+                engine.step(p)
+        torch.cuda.current_stream(engine.device).wait_stream(self.stream)
+        torch.cuda.synchronize(engine.device)
+        engine.pool = pool0
+        for b, s in zip(engine.pool, saved):
+            b.copy_(s)
+        torch.cuda.synchronize(engine.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=self.stream):
+            engine.step(self.k)
+        engine.pool = pool0
+        engine.time, engine.step_count = t0, c0
+
+    def run(self, nsteps: int) -> None:
+        e = self.e
+        full, rem = divmod(nsteps, self.k)
+        for _ in range(full):
+            self.graph.replay()
+        e.time += full * self.k * e.dt
+        e.step_count += full * self.k
+        if rem:
+            e.step(rem)
 
 
 def assemble_global(layout: TileLayout, tiles_by_rank: Dict[int, np.ndarray]) -> np.ndarray:

@@ -64,7 +64,7 @@ class Advection(Physics):
     def kernel_params(self):
         return {"limiter": self.limiter}
 
-    def rhs(self, qe, q, tens, n, g):
+    def rhs(self, qe, qi, tens, n, g):
         qL, qR = plr_x(qe, g, n, self.limiter)
         U = tens["ex"]
         Fx = U * torch.where(U > 0, qL, qR)
@@ -73,5 +73,6 @@ class Advection(Physics):
         Gy = V * torch.where(V > 0, qL, qR)
         return -((Fx[..., 1:] - Fx[..., :-1]) + (Gy[..., 1:, :] - Gy[..., :-1, :])) * tens["invA"]
 
-    def max_dt(self, grid: CubedSphereGrid, cfl: float = 0.8) -> float:
-        return cfl * grid.min_spacing() / self._u0(grid)
+    def max_dt(self, grid: CubedSphereGrid, cfl: float = 0.9) -> float:
+        """2-D unsplit bound dt * |v| * (1/dx + 1/dy) <= cfl."""
+        return cfl * grid.min_spacing() / (2.0 * self._u0(grid))

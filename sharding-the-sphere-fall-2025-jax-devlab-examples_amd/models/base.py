@@ -127,13 +127,17 @@ class RankGeometry:
 # ----------------------------------------------------------------------------
 
 def extend(q: torch.Tensor, recv: Optional[torch.Tensor], gmap: torch.Tensor, T: int, n: int, g: int,
-           ng_map: Optional[int] = None) -> torch.Tensor:
-    """q [F, T*n*n] + recv [R, F] -> extended [F, T, n+2g, n+2g]; cube-corner
-    (and tile-corner) ghost blocks are zero (never read by the stencils).
-    ``gmap`` is the [T, 4, ng_map, n] ghost map; only its first g layers are used."""
+           ng: Optional[int] = None) -> torch.Tensor:
+    """Padded state q [F, T*P*P] (P = n + 2 ng) + recv [R, F] -> extended
+    window [F, T, n+2g, n+2g] with every ghost strip gathered through the ghost
+    map (pull).  Corner blocks are whatever the storage holds (never read by the
+    dimension-split stencils).  ``gmap`` is [T, 4, ng, n]; its first g layers
+    are used."""
     F = q.shape[0]
-    qe = q.new_zeros((F, T, n + 2 * g, n + 2 * g))
-    qe[:, :, g:g + n, g:g + n] = q.view(F, T, n, n)
+    ng = gmap.shape[2] if ng is None else ng
+    P = n + 2 * ng
+    o = ng - g
+    qe = q.view(F, T, P, P)[:, :, o:o + n + 2 * g, o:o + n + 2 * g].clone()
     gm = gmap[:, :, :g, :].long()
     loc = gm >= 0
     vals = q[:, gm.clamp(min=0)]                               # [F,T,4,g,n]
@@ -146,6 +150,23 @@ def extend(q: torch.Tensor, recv: Optional[torch.Tensor], gmap: torch.Tensor, T:
         qe[:, :, g - 1 - k, g:g + n] = vals[:, :, 2, k, :]
         qe[:, :, g + n + k, g:g + n] = vals[:, :, 3, k, :]
     return qe
+
+
+def interior(q: torch.Tensor, T: int, n: int, ng: int) -> torch.Tensor:
+    """[F, T*P*P] padded -> [F, T, n, n] view of the interior cells."""
+    P = n + 2 * ng
+    return q.view(q.shape[0], T, P, P)[:, :, ng:ng + n, ng:ng + n]
+
+
+def cells_x(qe: torch.Tensor, g: int, n: int):
+    """Unreconstructed cell values left/right of the n+1 x-edges of the interior rows."""
+    rows = qe[..., g:g + n, :]
+    return rows[..., g - 1:g + n], rows[..., g:g + n + 1]
+
+
+def cells_y(qe: torch.Tensor, g: int, n: int):
+    cols = qe[..., :, g:g + n]
+    return cols[..., g - 1:g + n, :], cols[..., g:g + n + 1, :]
 
 
 def limited_slope(dl: torch.Tensor, dr: torch.Tensor, lim: int) -> torch.Tensor:
@@ -198,10 +219,13 @@ class Physics:
         """[F, T, n, n] float64."""
         raise NotImplementedError
 
-    def rhs(self, qe: torch.Tensor, q: torch.Tensor, tens: Dict[str, torch.Tensor], n: int, g: int) -> torch.Tensor:
+    def rhs(self, qe: torch.Tensor, qi: torch.Tensor, tens: Dict[str, torch.Tensor], n: int, g: int) -> torch.Tensor:
+        """qe: extended window [F,T,n+2g,n+2g]; qi: interior [F,T,n,n].
+        Returns dq/dt [F,T,n,n]."""
         raise NotImplementedError
 
     def finalize(self, out: torch.Tensor, tens: Dict[str, torch.Tensor]) -> torch.Tensor:
+        """Post-stage fix-up on an interior tensor [F,T,n,n] (in place)."""
         return out
 
     def kernel_params(self) -> Dict[str, float]:
@@ -210,7 +234,6 @@ class Physics:
     def max_dt(self, grid: CubedSphereGrid, cfl: float = 0.8) -> float:
         raise NotImplementedError
 
-    def diagnostics(self, q: torch.Tensor, tens: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
-        """Per-rank partial sums (to be all-reduced)."""
-        area = tens["area"].reshape(-1)
-        return {"mass": (q[0] * area).sum()}
+    def diagnostics(self, qi: torch.Tensor, tens: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """Per-rank partial sums over the interior qi [F,T,n,n] (to be all-reduced)."""
+        return {"mass": (qi[0] * tens["area"]).sum()}

@@ -48,7 +48,7 @@ class Diffusion(Physics):
         return {"area": t(geo.area), "invA": t(1.0 / geo.area),
                 "ex": t(self.kappa * geo.lx / dx), "ey": t(self.kappa * geo.ly / dy)}
 
-    def rhs(self, qe, q, tens, n, g):
+    def rhs(self, qe, qi, tens, n, g):
         c = qe[..., g:g + n, g - 1:g + n + 1]
         Fx = -tens["ex"] * (c[..., 1:] - c[..., :-1])
         c = qe[..., g - 1:g + n + 1, g:g + n]

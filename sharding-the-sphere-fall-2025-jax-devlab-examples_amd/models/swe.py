@@ -8,7 +8,8 @@ Formulation (chosen here; the reference does not show one):
   Velocity Exchange");
 * flux form  d(h, M)/dt + div(h v, M v + g h^2/2 I) = S,  FV with PLR on the
   primitive variables (h, v) and a Rusanov (local Lax-Friedrichs) edge flux
-  along the exact great-circle edge normals;
+  along the exact great-circle edge normals; the Rusanov speed is
+  max(|v.m| + sqrt(g h)) over the two adjacent cell averages;
 * sources: Coriolis  -f r x M  (f = 2 Omega z/R), topography  -g h grad b, and
   the curvature balance  +g h_c^2 / 2 * (sum m L) / A, which makes a constant
   depth exactly force-free on the curved cell;
@@ -23,7 +24,7 @@ from typing import Dict
 import numpy as np
 import torch
 
-from .base import Physics, RankGeometry, limited_slope, plr_x, plr_y
+from .base import Physics, RankGeometry, cells_x, cells_y, plr_x, plr_y
 from .geometry import GRAVITY, OMEGA, CubedSphereGrid
 from . import initial_conditions as ic
 
@@ -73,6 +74,11 @@ class ShallowWater(Physics):
     def setup(self, geo: RankGeometry, dtype, device) -> Dict[str, torch.Tensor]:
         _, _, b = self.global_fields(geo.grid)
         gb = geo.fv_gradient(b)
+        # curvature balance  g/2 * sum_e(+-L_e m_e) / A  per cell (metric term)
+        mlx = geo.lx[..., None] * geo.mx[:, None, :, :]
+        mly = geo.ly[..., None] * geo.my[:, :, None, :]
+        S = (mlx[:, :, 1:] - mlx[:, :, :-1]) + (mly[:, 1:] - mly[:, :-1])
+        sbal = 0.5 * self.g * S / geo.area[..., None]
         t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=device)
         return {
             "area": t(geo.area),
@@ -83,6 +89,10 @@ class ShallowWater(Physics):
             "my": t(np.moveaxis(geo.my, -1, 1)),
             "ctr": t(np.moveaxis(geo.center, -1, 0)),      # [3,T,n,n]
             "gradb": t(np.moveaxis(gb, -1, 0)),            # [3,T,n,n]
+            "sbal": t(np.moveaxis(sbal, -1, 0)),           # [3,T,n,n]
+            # HIP kernel: one 16-byte-aligned record per cell (1/A, centre, grad b, 0)
+            "cgeo": t(np.concatenate([(1.0 / geo.area)[..., None], geo.center, gb,
+                                      np.zeros(geo.area.shape + (1,))], axis=-1)),   # [T,n,n,8]
             "b": t(geo.gather_global(b)),
         }
 
@@ -90,60 +100,60 @@ class ShallowWater(Physics):
         return {"g": self.g, "omega2": 2.0 * self.omega, "limiter": self.limiter}
 
     # ---- reference RHS ------------------------------------------------------
-    def _flux(self, wL, wR, m, L):
+    def _flux(self, wL, wR, cL, cR, m, L):
         g = self.g
         hL, hR = wL[0], wR[0]
         vL, vR = wL[1:], wR[1:]
         vnL = (vL * m).sum(0)
         vnR = (vR * m).sum(0)
-        c = torch.maximum(vnL.abs() + torch.sqrt(g * hL), vnR.abs() + torch.sqrt(g * hR))
+        sL = ((cL[1:] * m).sum(0)).abs() + torch.sqrt(g * cL[0])
+        sR = ((cR[1:] * m).sum(0)).abs() + torch.sqrt(g * cR[0])
+        c = torch.maximum(sL, sR)
         Fh = 0.5 * (hL * vnL + hR * vnR) - 0.5 * c * (hR - hL)
         Fm = 0.5 * (hL * vL * vnL + hR * vR * vnR + 0.5 * g * (hL * hL + hR * hR) * m) - 0.5 * c * (hR * vR - hL * vL)
         return torch.cat([Fh[None], Fm], 0) * L
 
-    def rhs(self, qe, q, tens, n, g):
-        F, T = qe.shape[0], qe.shape[1]
+    def rhs(self, qe, qi, tens, n, g):
         h = qe[0]
         safe = torch.where(h != 0, h, torch.ones_like(h))
         w = torch.stack([h, qe[1] / safe, qe[2] / safe, qe[3] / safe])
         lim = self.limiter
         wL, wR = plr_x(w, g, n, lim)                                  # [4,T,n,n+1]
+        cL, cR = cells_x(w, g, n)
         mx = tens["mx"].permute(1, 0, 2)[:, :, None, :]              # [3,T,1,n+1]
-        Fx = self._flux(wL, wR, mx, tens["ex"])
+        Fx = self._flux(wL, wR, cL, cR, mx, tens["ex"])
         wL, wR = plr_y(w, g, n, lim)                                  # [4,T,n+1,n]
+        cL, cR = cells_y(w, g, n)
         my = tens["my"].permute(1, 0, 2)[:, :, :, None]              # [3,T,n+1,1]
-        Gy = self._flux(wL, wR, my, tens["ey"])
+        Gy = self._flux(wL, wR, cL, cR, my, tens["ey"])
         invA = tens["invA"]
         dq = -((Fx[..., 1:] - Fx[..., :-1]) + (Gy[..., 1:, :] - Gy[..., :-1, :])) * invA
-        hc = q[0].view(T, n, n)
-        M = q[1:4].view(3, T, n, n)
+        hc = qi[0]
+        M = qi[1:4]
         r = tens["ctr"]
         f = self.omega * 2.0 * r[2]
         cor = torch.stack([r[1] * M[2] - r[2] * M[1], r[2] * M[0] - r[0] * M[2], r[0] * M[1] - r[1] * M[0]])
-        lx, ly = tens["ex"], tens["ey"]
-        S = (lx[None, :, :, 1:] * mx[..., 1:] - lx[None, :, :, :-1] * mx[..., :-1]
-             + ly[None, :, 1:, :] * my[:, :, 1:, :] - ly[None, :, :-1, :] * my[:, :, :-1, :])
-        dq[1:] += -f * cor + (0.5 * self.g * hc * hc * invA) * S - self.g * hc * tens["gradb"]
+        dq[1:] += -f * cor + (hc * hc) * tens["sbal"] - self.g * hc * tens["gradb"]
         return dq
 
     def finalize(self, out, tens):
-        F = out.shape[0]
-        r = tens["ctr"].reshape(3, -1)
+        r = tens["ctr"]
         M = out[1:4]
         d = (M * r).sum(0)
         out[1:4] = M - d * r
         return out
 
-    def max_dt(self, grid: CubedSphereGrid, cfl: float = 0.8) -> float:
+    def max_dt(self, grid: CubedSphereGrid, cfl: float = 0.9) -> float:
+        """2-D unsplit bound: dt * speed * (1/dx + 1/dy) <= cfl."""
         h, wind, b = self.global_fields(grid)
         speed = np.linalg.norm(wind, axis=-1) + np.sqrt(self.g * np.maximum(h, 0))
-        return cfl * grid.min_spacing() / float(speed.max())
+        return cfl * grid.min_spacing() / (2.0 * float(speed.max()))
 
-    def diagnostics(self, q, tens):
-        A = tens["area"].reshape(-1)
-        h = q[0]
-        M = q[1:4]
-        b = tens["b"].reshape(-1)
+    def diagnostics(self, qi, tens):
+        A = tens["area"]
+        h = qi[0]
+        M = qi[1:4]
+        b = tens["b"]
         ke = 0.5 * (M * M).sum(0) / h
         pe = 0.5 * self.g * h * h + self.g * h * b
         return {"mass": (h * A).sum(), "energy": ((ke + pe) * A).sum()}

@@ -1,0 +1,80 @@
+"""Build the in-tree gfx950 shared library (hipcc, no JIT cache).
+
+    python -m stsphere.ops.build            # build if sources are newer
+    python -m stsphere.ops.build --force
+
+Produces ``ops/libstsp.so`` next to the sources, so it travels with the repo
+snapshot to the GPU box.  Links RCCL (``librccl.so.1``; at run time the process
+shares the copy that PyTorch already loaded, same SONAME) and roctx.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libstsp.so")
+SOURCES = ["stage_kernel.hip", "runtime.cpp"]
+HEADERS = ["stsp_kernels.h", "runtime.h"]
+ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
+# library variants: "" = production; "diag" = in-kernel phase stamps (-DSTSP_STAMPS)
+VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"]}
+
+
+def lib_for(variant: str = "") -> str:
+    return LIB if not variant else os.path.join(HERE, f"libstsp_{variant}.so")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.exists(c) or c == "hipcc"):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def needs_build(variant: str = "") -> bool:
+    lib = lib_for(variant)
+    if not os.path.exists(lib):
+        return True
+    t = os.path.getmtime(lib)
+    for f in SOURCES + HEADERS:
+        p = os.path.join(CSRC, f)
+        if os.path.exists(p) and os.path.getmtime(p) > t:
+            return True
+    return False
+
+
+def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
+    lib = lib_for(variant)
+    if not force and not needs_build(variant):
+        return lib
+    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
+           "-Wno-unused-result", "-I", CSRC, "-I", "/opt/rocm/include", *VARIANT_FLAGS[variant],
+           *srcs, "-o", lib + ".tmp", "-L/opt/rocm/lib", "-l:librccl.so.1", "-lroctx64"]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"hipcc failed ({r.returncode})")
+    os.replace(lib + ".tmp", lib)
+    return lib
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--variant", default="", choices=sorted(VARIANT_FLAGS))
+    ap.add_argument("--all", action="store_true", help="build every variant")
+    a = ap.parse_args()
+    for v in (sorted(VARIANT_FLAGS) if a.all else [a.variant]):
+        print(build(a.force, a.verbose, v))
+
+
+if __name__ == "__main__":
+    main()

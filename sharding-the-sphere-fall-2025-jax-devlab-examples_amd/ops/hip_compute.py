@@ -1,0 +1,133 @@
+"""HIP stage computation for ``Engine(backend='hip')``: one fused gfx950 kernel
+launch per RK stage (two when the rank has remote neighbours: interior blocks
+while the halo messages fly, boundary blocks after).
+
+All shape contracts the kernel relies on are checked here, on the host, once,
+before anything is launched (a bad index in a hand-written kernel can reset a
+whole node).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import native
+from ..models.integrators import Stage
+
+BLOCK_SHAPES = ((16, 16), (32, 8), (16, 8), (8, 16), (8, 8))
+
+
+def choose_block(n: int):
+    """Pick the block shape with the least padding waste (ties -> 16x16)."""
+    best, waste = (16, 16), None
+    for bx, by in BLOCK_SHAPES:
+        if bx * by != 256:
+            continue
+        nbx, nby = -(-n // bx), -(-n // by)
+        w = nbx * nby * bx * by - n * n
+        if waste is None or w < waste:
+            best, waste = (bx, by), w
+    return best
+
+
+class HipCompute:
+    def __init__(self, engine):
+        e = engine
+        self.e = e
+        self.lib = native.require_native()
+        if e.device.type != "cuda":
+            raise RuntimeError("backend='hip' needs a GPU tensor device")
+        plan = e.plan
+        phys = e.physics
+        self.phys_id = phys.kernel_id
+        self.dcode = native.dtype_code(e.dtype)
+        n, T = plan.n, plan.T
+        bx, by = e.block if e.block != (16, 16) else choose_block(n)
+        if (bx, by) not in BLOCK_SHAPES:
+            raise ValueError(f"unsupported block shape {(bx, by)}")
+        self.bx, self.by = bx, by
+        self.nbx, self.nby = -(-n // bx), -(-n // by)
+        self.nblocks = T * self.nbx * self.nby
+        t = e.tens
+        F, S = phys.F, plan.S
+        # ---- host-side shape contract checks ----------------------------
+        for b in e.pool:
+            assert b.shape == (F, S) and b.is_contiguous() and b.dtype == e.dtype
+        assert e.gmap.dtype == torch.int32 and e.gmap.shape == (T, 4, plan.ng, n)
+        assert phys.halo <= plan.ng
+        assert t["invA"].shape == (T, n, n)
+        assert t["ex"].shape == (T, n, n + 1) and t["ey"].shape == (T, n + 1, n)
+        if self.phys_id == 2:
+            assert t["mx"].shape == (T, 3, n + 1) and t["my"].shape == (T, 3, n + 1)
+            assert t["cgeo"].shape == (T, n, n, 8)
+        assert S == T * (n + 2 * plan.ng) ** 2
+        pm = plan.push_map
+        assert pm.shape == (T, 4, plan.ng, n) and pm.max(initial=-1) < S
+        self.push = torch.as_tensor(pm, dtype=torch.int32, device=e.device)
+        recv = e.transport.recv
+        assert recv.shape == (plan.num_recv, F)
+        gm = plan.ghost_map
+        if gm.size:
+            assert gm.max() < S and (-1 - gm[gm < 0]).max(initial=-1) < plan.num_recv
+        for k in t:
+            t[k] = t[k].contiguous()
+        self.remote = plan.num_recv > 0
+        if self.remote:
+            inter, bnd = plan.block_classes(bx, by)
+            self.blk_interior = torch.as_tensor(inter, dtype=torch.int32, device=e.device)
+            self.blk_boundary = torch.as_tensor(bnd, dtype=torch.int32, device=e.device)
+            assert (inter.size == 0 or inter.max() < self.nblocks) and (bnd.size == 0 or bnd.max() < self.nblocks)
+        self._g = phys.kernel_params().get("g", 0.0)
+        self._omega2 = phys.kernel_params().get("omega2", 0.0)
+        self._lim = int(phys.kernel_params().get("limiter", 0))
+
+    def desc(self, st: Stage, dt: float, blocks: Optional[torch.Tensor], nblocks: int,
+             remote: bool = False) -> native.StageDesc:
+        e = self.e
+        t = e.tens
+        p = native.ptr
+        d = native.StageDesc()
+        d.X = p(e.pool[st.X])
+        d.Q = p(e.pool[st.Q])
+        d.acc_in = p(e.pool[st.acc_in]) if st.acc_in >= 0 else 0
+        d.out = p(e.pool[st.out])
+        d.acc_out = p(e.pool[st.acc_out]) if st.acc_out >= 0 else 0
+        d.recv = p(e.transport.recv) if e.transport.recv.numel() else 0
+        d.gmap = p(e.gmap)
+        d.push = p(self.push)
+        d.blocks = p(blocks) if blocks is not None else 0
+        d.invA = p(t["invA"])
+        d.ex = p(t["ex"])
+        d.ey = p(t["ey"])
+        if self.phys_id == 2:
+            d.mx, d.my, d.cgeo = p(t["mx"]), p(t["my"]), p(t["cgeo"])
+        d.ntile = e.plan.T
+        d.n = e.plan.n
+        d.S = e.plan.S
+        d.mg = e.plan.ng
+        d.pw = e.plan.P
+        d.nblocks = nblocks
+        d.limiter = self._lim
+        d.remote = 1 if remote else 0
+        d.a0, d.a1, d.a2 = st.a0, st.a1, st.a2
+        d.c0, d.c1, d.c2 = st.c0, st.c1, st.c2
+        d.dt = dt
+        d.g = self._g
+        d.omega2 = self._omega2
+        return d
+
+    def launch(self, d: native.StageDesc, stream: Optional[int] = None) -> None:
+        rc = self.lib.stsp_stage_launch(self.phys_id, self.dcode, self.bx, self.by, d,
+                                        native.current_stream_handle() if stream is None else stream)
+        native.check(rc, "stage kernel")
+
+    def stage(self, st: Stage, dt: float, recv, part: str = "all") -> None:
+        if not self.remote:
+            if part in ("all", "interior"):
+                self.launch(self.desc(st, dt, None, self.nblocks))
+            return
+        if part in ("all", "interior") and self.blk_interior.numel():
+            self.launch(self.desc(st, dt, self.blk_interior, self.blk_interior.numel()))
+        if part in ("all", "boundary") and self.blk_boundary.numel():
+            self.launch(self.desc(st, dt, self.blk_boundary, self.blk_boundary.numel(), remote=True))

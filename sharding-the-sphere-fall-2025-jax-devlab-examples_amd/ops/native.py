@@ -1,0 +1,149 @@
+"""ctypes binding of the in-tree gfx950 library ``ops/libstsp.so``.
+
+``import torch`` happens first so that the library's ``libamdhip64.so.7`` /
+``librccl.so.1`` dependencies resolve to the copies PyTorch already loaded
+(same SONAME): one HIP runtime, one device context, torch streams usable.
+
+On a machine with a GPU, a missing or stale library is an error (no silent
+fallback); ``require_native()`` raises with the build command.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the library load)
+
+from . import build as _build
+
+_LIB = None
+_LOCK = threading.Lock()
+
+
+class StageDesc(ctypes.Structure):
+    _fields_ = [
+        ("X", ctypes.c_void_p), ("Q", ctypes.c_void_p), ("acc_in", ctypes.c_void_p),
+        ("out", ctypes.c_void_p), ("acc_out", ctypes.c_void_p), ("recv", ctypes.c_void_p),
+        ("gmap", ctypes.c_void_p), ("push", ctypes.c_void_p), ("blocks", ctypes.c_void_p),
+        ("invA", ctypes.c_void_p), ("ex", ctypes.c_void_p), ("ey", ctypes.c_void_p),
+        ("mx", ctypes.c_void_p), ("my", ctypes.c_void_p), ("cgeo", ctypes.c_void_p),
+        ("ntile", ctypes.c_int), ("n", ctypes.c_int), ("S", ctypes.c_int), ("mg", ctypes.c_int), ("pw", ctypes.c_int),
+        ("nblocks", ctypes.c_int), ("limiter", ctypes.c_int), ("remote", ctypes.c_int),
+        ("a0", ctypes.c_double), ("a1", ctypes.c_double), ("a2", ctypes.c_double),
+        ("c0", ctypes.c_double), ("c1", ctypes.c_double), ("c2", ctypes.c_double), ("dt", ctypes.c_double),
+        ("g", ctypes.c_double), ("omega2", ctypes.c_double),
+        ("stamps", ctypes.c_void_p),
+    ]
+
+
+def lib_path() -> str:
+    return _build.lib_for(os.environ.get("STSP_VARIANT", ""))
+
+
+def load(build_if_missing: bool = True):
+    """Load (building first if the sources are newer and hipcc exists)."""
+    global _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        variant = os.environ.get("STSP_VARIANT", "")
+        path = _build.lib_for(variant)
+        if build_if_missing and _build.needs_build(variant):
+            try:
+                _build.build(variant=variant)
+            except Exception:
+                if not os.path.exists(path):
+                    raise
+        L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        vp, ci, cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
+        L.stsp_stage_launch.argtypes = [ci, ci, ci, ci, ctypes.POINTER(StageDesc), vp]
+        L.stsp_stage_launch.restype = ci
+        L.stsp_pack_launch.argtypes = [ci, vp, ci, ci, vp, ci, vp, vp]
+        L.stsp_pack_launch.restype = ci
+        L.stsp_copy_index_launch.argtypes = [ci, vp, vp, vp, vp, ci, ci, cl, cl, vp]
+        L.stsp_copy_index_launch.restype = ci
+        _declare_runtime(L)
+        _LIB = L
+        return L
+
+
+def _declare_runtime(L):
+    vp, ci, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    if not hasattr(L, "stsp_rt_create"):
+        return
+    L.stsp_rt_create.argtypes = [vp]
+    L.stsp_rt_create.restype = vp
+    L.stsp_rt_destroy.argtypes = [vp]
+    L.stsp_rt_destroy.restype = None
+    L.stsp_rt_run.argtypes = [vp, ci]
+    L.stsp_rt_run.restype = ci
+    L.stsp_rt_set_dt.argtypes = [vp, cd]
+    L.stsp_rt_set_dt.restype = ci
+    L.stsp_rt_last_error.argtypes = [vp]
+    L.stsp_rt_last_error.restype = ctypes.c_char_p
+    L.stsp_nccl_unique_id.argtypes = [vp]
+    L.stsp_nccl_unique_id.restype = ci
+    L.stsp_nccl_id_bytes.argtypes = []
+    L.stsp_nccl_id_bytes.restype = ci
+    L.stsp_roctx_push.argtypes = [ctypes.c_char_p]
+    L.stsp_roctx_push.restype = ci
+    L.stsp_roctx_pop.argtypes = []
+    L.stsp_roctx_pop.restype = ci
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except Exception:
+        return False
+
+
+def require_native():
+    try:
+        return load()
+    except Exception as e:
+        raise RuntimeError(
+            f"native gfx950 library unavailable ({e}); build it with "
+            f"`python -m stsphere.ops.build` (hipcc --offload-arch=gfx950)") from e
+
+
+def dtype_code(dtype: torch.dtype) -> int:
+    if dtype == torch.float64:
+        return 1
+    if dtype == torch.float32:
+        return 0
+    raise TypeError(f"unsupported dtype {dtype}")
+
+
+def ptr(t) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+def current_stream_handle() -> int:
+    return int(torch.cuda.current_stream().cuda_stream)
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with code {rc}")
+
+
+def pack(q: torch.Tensor, idx: torch.Tensor, send: torch.Tensor, stream: int = None) -> None:
+    L = require_native()
+    F, S = q.shape
+    assert idx.dtype == torch.int32 and send.numel() >= idx.numel() * F
+    rc = L.stsp_pack_launch(dtype_code(q.dtype), ptr(q), S, F, ptr(idx), idx.numel(), ptr(send),
+                            current_stream_handle() if stream is None else stream)
+    check(rc, "pack")
+
+
+def copy_index(src: torch.Tensor, sidx: torch.Tensor, dst: torch.Tensor, didx: torch.Tensor, batch: int,
+               src_stride: int, dst_stride: int) -> None:
+    L = require_native()
+    assert sidx.numel() == didx.numel()
+    assert sidx.dtype == torch.int32 and didx.dtype == torch.int32
+    rc = L.stsp_copy_index_launch(dtype_code(src.dtype), ptr(src), ptr(sidx), ptr(dst), ptr(didx), sidx.numel(),
+                                  batch, src_stride, dst_stride, current_stream_handle())
+    check(rc, "copy_index")

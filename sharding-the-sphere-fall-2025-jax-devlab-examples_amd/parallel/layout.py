@@ -1,13 +1,24 @@
 """Tile layout and per-rank halo plans (the "Communication Scheduler" box of
 PDF s.7, generalised beyond the reference's fixed 6-face table).
 
-Storage model: every rank holds, per field, its tiles packed
-tile-major **without ghost padding**: ``q[field, tile_local * n*n + j*n + i]``.
-Ghost values are never stored in the state; kernels gather them on the fly
-through a per-rank ghost map:
+Storage model: every rank holds, per field, its tiles
+tile-major with an ng-cell ghost ring, P = n + 2 ng:
 
-    ghost_map[tile_local, side, layer, pos] =  k >= 0   -> q[f, k]           (same rank)
-                                               -1 - s   -> recv[s, f]         (remote slot s)
+    q[field, (tile_local * P + j + ng) * P + i + ng]        interior (i, j) in [0, n)^2
+
+Two maps describe the halo:
+
+    ghost_map[tile_local, side, layer, pos] =  k >= 0   -> q[f, k] (padded offset of the
+                                                          same-rank source cell)
+                                               -1 - s   -> recv[s, f]  (remote slot s)
+    push_map[tile_local, side, layer, pos]  =  padded offset of the ghost slot (in a
+                                               same-rank tile) that the interior strip
+                                               cell (side, layer, pos) feeds, or -1
+
+The HIP stage kernel *pushes*: when it writes a cell near a tile edge it also
+writes the value into the neighbour tile's ghost slot, so the next stage loads
+its whole window with plain, regular loads (one memory round trip, no index
+indirection).  Remote ghost slots are read from ``recv`` through ghost_map.
 
 with side 0 = W (x < 0), 1 = E (x >= n), 2 = S (y < 0), 3 = N (y >= n), layer
 0 nearest the tile edge, pos the index along the edge.  Cross-panel
@@ -140,9 +151,27 @@ class TileLayout:
         return sel[np.sort(first)]
 
     def local_flat(self, gflat: np.ndarray) -> np.ndarray:
+        """global flat -> padded offset in the owning rank's storage."""
         tid, i, j = self.locate(gflat)
         li = self._local_arr[tid]
-        return (li * self.n + j) * self.n + i
+        P, g = self.n + 2 * self.ng, self.ng
+        return (li * P + j + g) * P + i + g
+
+    def tile_neighbors(self) -> np.ndarray:
+        """[num_tiles, 4] tile across side W, E, S, N."""
+        key = "tnbr"
+        if key not in self._cache:
+            n = self.n
+            out = np.empty((self.num_tiles, 4), dtype=np.int64)
+            for tid in range(self.num_tiles):
+                f, I0, J0 = self.tile_origin(tid)
+                mid = n // 2
+                pts = [(I0 - 1, J0 + mid), (I0 + n, J0 + mid), (I0 + mid, J0 - 1), (I0 + mid, J0 + n)]
+                for s, (I, J) in enumerate(pts):
+                    F_, I2, J2 = neighbor_cells(self.N, f, np.array([I]), np.array([J]))
+                    out[tid, s] = self.locate(self.global_flat(F_, I2, J2))[0][0]
+            self._cache[key] = out
+        return self._cache[key]
 
 
 @dataclass
@@ -156,7 +185,8 @@ class RankPlan:
         self.T = len(self.tiles)
         self.n = L.n
         self.ng = L.ng
-        self.S = self.T * self.n * self.n
+        self.P = self.n + 2 * self.ng
+        self.S = self.T * self.P * self.P
         src = L.ghost_sources(self.rank)
         tid, _, _ = L.locate(src)
         own = np.asarray(L.owner)[tid]
@@ -199,6 +229,44 @@ class RankPlan:
             off += len(need)
         self.num_send = off
         self.send_idx = (np.concatenate(idx) if idx else np.zeros(0, dtype=np.int64)).astype(np.int32)
+        self._build_push_map(src, own)
+
+    def _build_push_map(self, src: np.ndarray, own: np.ndarray) -> None:
+        """push_map and the halo-refresh index lists (see module docstring)."""
+        L = self.layout
+        n, g, P, T = self.n, self.ng, self.P, self.T
+        tnbr = L.tile_neighbors()
+        push = np.full((T, 4, g, n), -1, dtype=np.int64)
+        hsrc, hdst = [], []
+        pos = np.arange(n)
+        for t in range(T):
+            for s in range(4):
+                for k in range(g):
+                    x, y = ghost_xy(s, k, pos, n)
+                    dst = (t * P + y + g) * P + x + g
+                    loc = own[t, s, k] == self.rank
+                    if not loc.any():
+                        continue
+                    c = src[t, s, k][loc]
+                    tid2, i2, j2 = L.locate(c)
+                    hsrc.append(L.local_flat(c))
+                    hdst.append(dst[loc])
+                    recv_tile = self.tiles[t]
+                    for q, (tt, ii, jj, d) in enumerate(zip(tid2, i2, j2, dst[loc])):
+                        sides = np.nonzero(tnbr[tt] == recv_tile)[0]
+                        ok = False
+                        for s2 in sides:
+                            kk, pp = ((ii, jj), (n - 1 - ii, jj), (jj, ii), (n - 1 - jj, ii))[s2]
+                            if kk < g:
+                                li = L._local_arr[tt]
+                                assert push[li, s2, kk, pp] in (-1, d), "push collision"
+                                push[li, s2, kk, pp] = d
+                                ok = True
+                                break
+                        assert ok, "no strip feeds this ghost slot"
+        self.push_map = push.astype(np.int32)
+        self.halo_src = (np.concatenate(hsrc) if hsrc else np.zeros(0, np.int64)).astype(np.int32)
+        self.halo_dst = (np.concatenate(hdst) if hdst else np.zeros(0, np.int64)).astype(np.int32)
 
     @property
     def peers(self) -> List[int]:
