@@ -1,0 +1,357 @@
+"""Solver driver: the "JAXStream" pipeline of PDF s.6 (Geometry -> Initial
+Conditions -> Solver -> {History, Restarts, Analysis}) on MI355X.
+
+The reference shows only a method ``setup_sharding(self)`` of an unnamed class
+holding ``self.config``, ``self.mesh`` and ``self.sharding`` (PY:19-85).
+``Solver`` is that class:
+
+    solver = Solver("config.yaml")      # or a dict / Config
+    solver.setup_sharding()             # validation + banner, sets .mesh/.sharding
+    solver.initialize()                 # grid, physics, per-rank engines, restore
+    summary = solver.run(days=5)        # time loop, history, checkpoints, metrics
+
+Execution modes (chosen from the config and the launch environment):
+
+* ``single``  one device (GPU: fused HIP stage kernels + HIP-graph replay;
+              CPU: PyTorch reference);
+* ``virtual`` several ranks in one process, stepped in lockstep (the analogue
+              of the reference's CPU virtual devices, PY:64-68; also works on
+              one GPU);
+* ``spmd``    one process per device under ``torchrun`` (WORLD_SIZE > 1):
+              RCCL (backend "nccl") on GPUs, gloo on CPUs, bundled P2P halos.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .engine import Engine, GraphStepper, VirtualCluster, assemble_global
+from .models.advection import Advection
+from .models.base import limiter_code
+from .models.diffusion import Diffusion
+from .models.geometry import DAY, EARTH_RADIUS, CubedSphereGrid
+from .models.swe import ShallowWater
+from .parallel.comm import TorchDistTransport
+from .parallel.layout import TileLayout
+from .parallel.mesh import setup_sharding
+from .utils import checkpoint as ckpt
+from .utils.config import Config, default_case, load_config
+from .utils.history import HistoryWriter, MetricsLogger
+
+
+def make_physics(pc) -> Any:
+    model = pc.model.lower()
+    case = pc.case or default_case(model)
+    lim = limiter_code(pc.limiter)
+    if model == "swe":
+        return ShallowWater(case, limiter=lim, alpha=pc.alpha)
+    if model == "advection":
+        return Advection(case, alpha=pc.alpha, limiter=lim)
+    if model == "diffusion":
+        return Diffusion(kappa=pc.kappa, case=case)
+    raise ValueError(f"unknown physics model {pc.model!r}")
+
+
+class Solver:
+    def __init__(self, config=None, verbose: bool = True):
+        self.cfg: Config = load_config(config)
+        self.config: Dict[str, Any] = self.cfg.to_dict()
+        self.verbose = verbose
+        self.mesh = None
+        self.sharding = None
+        self.engines: List[Engine] = []
+        self.cluster: Optional[VirtualCluster] = None
+        self.runner: Optional[GraphStepper] = None
+        self.mode = None
+        self.world, self.rank = 1, 0
+
+    # ---- setup ------------------------------------------------------------
+    def setup_sharding(self) -> None:
+        self.mesh, self.sharding = setup_sharding(self.config, verbose=self.verbose and self._is_root())
+
+    def _is_root(self) -> bool:
+        return int(os.environ.get("RANK", "0")) == 0
+
+    def _log(self, *a) -> None:
+        if self.verbose and self.rank == 0:
+            print(*a, flush=True)
+
+    def initialize(self) -> None:
+        if self.sharding is None:
+            self.setup_sharding()
+        c = self.cfg
+        nd = c.parallelization.num_devices
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        gpu = c.parallelization.device_type == "gpu"
+        if gpu and not torch.cuda.is_available():
+            raise RuntimeError("device_type 'gpu' requested but no GPU is visible (use device_type: cpu)")
+        if self.world > 1:
+            if self.world != nd:
+                raise ValueError(f"launched with {self.world} processes but num_devices = {nd}")
+            self.mode = "spmd"
+            import torch.distributed as dist
+            device = torch.device(f"cuda:{local}") if gpu else torch.device("cpu")
+            if gpu:
+                torch.cuda.set_device(device)
+            if not dist.is_initialized():
+                dist.init_process_group("nccl" if gpu else "gloo",
+                                        device_id=device if gpu else None)
+        else:
+            self.mode = "single" if nd == 1 else "virtual"
+            device = torch.device("cuda:0") if gpu else torch.device("cpu")
+        self.device = device
+        backend = c.runtime.backend
+        if backend == "auto":
+            backend = "hip" if device.type == "cuda" else "torch"
+        self.backend = backend
+        dtype = {"float64": torch.float64, "fp64": torch.float64, "float32": torch.float32,
+                 "fp32": torch.float32}[c.grid.dtype]
+        self.dtype = dtype
+        N, t = c.grid.N, c.parallelization.tiles_per_edge
+        self.layout = TileLayout(N, t, nd, ng=c.grid.halo, owner=self.sharding.owner)
+        self.grid = CubedSphereGrid(N, c.grid.radius or EARTH_RADIUS)
+        phys0 = make_physics(c.physics)
+        dt = c.time.dt or (phys0.max_dt(self.grid, c.time.cfl) if c.time.cfl else phys0.max_dt(self.grid))
+        kw = dict(grid=self.grid, dtype=dtype, device=device, backend=backend, integrator=c.time.integrator, dt=dt)
+        if c.runtime.block:
+            kw["block"] = tuple(c.runtime.block)
+        if self.mode == "virtual":
+            self.cluster = VirtualCluster(lambda: make_physics(c.physics), self.layout, **kw)
+            self.engines = list(self.cluster.engines)
+        elif self.mode == "spmd":
+            tr = TorchDistTransport(self.layout.plan(self.rank), phys0.F, dtype, device,
+                                    staged=(c.runtime.comm == "staged"))
+            self.engines = [Engine(phys0, self.layout, self.rank, transport=tr, **kw)]
+        else:
+            self.engines = [Engine(phys0, self.layout, 0, **kw)]
+        for e in self.engines:
+            e.canary = c.runtime.canary
+        self.dt = dt
+        self.physics = phys0
+        self.fields = list(phys0.fields)
+        self._log(f"Initialized {phys0.name} ({getattr(phys0, 'case', '')}) C{N}, {self.mode} mode, "
+                  f"backend={backend}, dtype={c.grid.dtype}, dt={dt:.3f} s, integrator={c.time.integrator}")
+        if c.io.restore:
+            path = c.io.restore
+            if path == "latest":
+                path = ckpt.latest_checkpoint(self.checkpoint_root())
+            if path:
+                self.restore_checkpoint(path)
+
+    # ---- state access ---------------------------------------------------------
+    @property
+    def time(self) -> float:
+        return self.engines[0].time
+
+    @property
+    def step_count(self) -> int:
+        return self.engines[0].step_count
+
+    def local_values(self) -> Dict[int, np.ndarray]:
+        """{rank: [F, T_local, n, n]} for the engines of this process."""
+        return {e.rank: e.tiles_view().detach().cpu().double().numpy() for e in self.engines}
+
+    def gather_global(self) -> Optional[np.ndarray]:
+        """[F, 6, N, N] on rank 0 (None elsewhere)."""
+        F = len(self.fields)
+        vals = self.local_values()
+        if self.mode == "spmd":
+            import torch.distributed as dist
+            objs = [None] * self.world
+            dist.all_gather_object(objs, vals)
+            vals = {}
+            for o in objs:
+                vals.update(o)
+            if self.rank != 0:
+                return None
+        return np.stack([assemble_global(self.layout, {r: v[f] for r, v in vals.items()}) for f in range(F)])
+
+    def global_field(self, name_or_index=0) -> Optional[np.ndarray]:
+        f = self.fields.index(name_or_index) if isinstance(name_or_index, str) else name_or_index
+        g = self.gather_global()
+        return None if g is None else g[f]
+
+    def _allreduce(self, vals: Dict[str, float], op: str = "sum") -> Dict[str, float]:
+        if self.mode != "spmd":
+            return vals
+        import torch.distributed as dist
+        keys = sorted(vals)
+        t = torch.tensor([vals[k] for k in keys], dtype=torch.float64,
+                         device=self.device if self.device.type == "cuda" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MIN)
+        return dict(zip(keys, t.tolist()))
+
+    def diagnostics(self) -> Dict[str, float]:
+        tot: Dict[str, float] = {}
+        for e in self.engines:
+            for k, v in e.diagnostics().items():
+                tot[k] = tot.get(k, 0.0) + v
+        return self._allreduce(tot)
+
+    def all_finite(self) -> bool:
+        ok = float(all(bool(torch.isfinite(e.tiles_view()).all()) for e in self.engines))
+        return self._allreduce({"ok": ok}, op="min")["ok"] > 0.5
+
+    # ---- stepping ---------------------------------------------------------------
+    def _use_graph(self) -> bool:
+        c = self.cfg.runtime
+        return (self.mode == "single" and self.backend == "hip" and c.graph and not c.canary)
+
+    def step(self, nsteps: int = 1) -> None:
+        if nsteps <= 0:
+            return
+        if self.mode == "virtual":
+            self.cluster.step(nsteps)
+        elif self._use_graph():
+            if self.runner is None:
+                self.runner = GraphStepper(self.engines[0], self.cfg.runtime.steps_per_graph)
+            self.runner.run(nsteps)
+        else:
+            self.engines[0].step(nsteps)
+
+    def _sync(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def run(self, nsteps: Optional[int] = None, days: Optional[float] = None) -> Dict[str, Any]:
+        if not self.engines:
+            self.initialize()
+        c = self.cfg
+        if nsteps is None:
+            days = days if days is not None else c.time.days
+            if days is not None:
+                nsteps = int(math.ceil(days * DAY / self.dt - 1e-9))
+            else:
+                nsteps = c.time.nsteps or 1
+        io = c.io
+        out = io.output_dir
+        hist = None
+        if io.history_interval > 0:
+            n_out = nsteps // io.history_interval + 1
+            hpath = os.path.join(out, "history.zarr")
+            if self.rank == 0:
+                os.makedirs(out, exist_ok=True)
+                HistoryWriter(hpath, self.fields, self.layout.N, self.layout.n, n_out,
+                              attrs={"config": self.config})
+            self._barrier()
+            hist = HistoryWriter(hpath, self.fields, self.layout.N, self.layout.n, n_out, create=False)
+        metrics = MetricsLogger(os.path.join(out, "metrics.jsonl") if io.metrics_interval > 0 else None,
+                                enabled=self.rank == 0)
+        intervals = [x for x in (io.history_interval, io.checkpoint_interval, io.metrics_interval,
+                                 c.runtime.watchdog_interval) if x > 0]
+        done = 0
+        k_hist = 0
+        if hist is not None:
+            self._write_history(hist, k_hist)
+            k_hist += 1
+        wall0 = time.perf_counter()
+        self._sync()
+        recoveries = 0
+        while done < nsteps:
+            chunk = nsteps - done
+            for iv in intervals:
+                chunk = min(chunk, iv - (self.step_count % iv) if self.step_count % iv else iv)
+            chunk = max(1, min(chunk, nsteps - done))
+            self.step(chunk)
+            done += chunk
+            sc = self.step_count
+            if c.runtime.watchdog_interval and sc % c.runtime.watchdog_interval == 0:
+                if not self.all_finite():
+                    saved = ckpt.list_checkpoints(self.checkpoint_root())
+                    if recoveries < 3 and saved:
+                        recoveries += 1
+                        # go back further on each repeated failure (recent checkpoints may
+                        # already hold a growing instability)
+                        last = ckpt.step_dir(self.checkpoint_root(), saved[-min(recoveries, len(saved))])
+                        self._log(f"watchdog: non-finite state at step {sc}; restarting from {last} with dt/2")
+                        self.restore_checkpoint(last)
+                        self.set_dt(self.dt * 0.5)
+                        done = max(0, done - (sc - self.step_count))
+                        continue
+                    raise FloatingPointError(f"non-finite state detected at step {sc}")
+            if hist is not None and sc % io.history_interval == 0:
+                self._write_history(hist, k_hist)
+                k_hist += 1
+            if io.checkpoint_interval and sc % io.checkpoint_interval == 0:
+                self.save_checkpoint()
+            if io.metrics_interval and sc % io.metrics_interval == 0:
+                self._sync()
+                d = self.diagnostics()
+                wall = time.perf_counter() - wall0
+                metrics.log(step=sc, time_s=self.time, sim_days=self.time / DAY, dt=self.dt,
+                            cell_updates_per_s=6 * self.layout.N ** 2 * done / max(wall, 1e-12), **d)
+        self._sync()
+        wall = time.perf_counter() - wall0
+        summary = {"steps": nsteps, "wall_s": wall, "sim_days": self.time / DAY,
+                   "cell_updates_per_s": 6 * self.layout.N ** 2 * nsteps / max(wall, 1e-12),
+                   "sim_days_per_day": (nsteps * self.dt / DAY) / max(wall / DAY, 1e-30)}
+        summary.update(self.diagnostics())
+        self._log(f"Run complete: {nsteps} steps, {summary['sim_days']:.3f} days, "
+                  f"{summary['cell_updates_per_s']:.3e} cell-updates/s")
+        return summary
+
+    def set_dt(self, dt: float) -> None:
+        self.dt = dt
+        for e in self.engines:
+            e.dt = dt
+        self.runner = None   # graphs bake dt in; recapture lazily
+
+    def _barrier(self) -> None:
+        if self.mode == "spmd":
+            import torch.distributed as dist
+            dist.barrier()
+
+    def _write_history(self, hist: HistoryWriter, k: int) -> None:
+        for e in self.engines:
+            hist.write_tiles(k, e.plan.tiles, self.layout.tile_origin, e.tiles_view().detach().cpu().double().numpy())
+        if self.rank == 0:
+            hist.write_time(k, self.time, self.step_count)
+
+    # ---- checkpoint / restart ------------------------------------------------------
+    def checkpoint_root(self) -> str:
+        return self.cfg.io.checkpoint_dir or os.path.join(self.cfg.io.output_dir, "checkpoints")
+
+    def save_checkpoint(self, root: Optional[str] = None) -> str:
+        root = root or self.checkpoint_root()
+        self._sync()
+        step = self.step_count
+        d = ckpt.step_dir(root, step)
+        if self.rank == 0:
+            meta = {"step": step, "time": self.time, "dt": self.dt, "N": self.layout.N,
+                    "tiles_per_edge": self.layout.t, "num_ranks": self.layout.num_ranks,
+                    "owner": self.layout.owner, "fields": self.fields, "dtype": self.cfg.grid.dtype,
+                    "integrator": self.cfg.time.integrator, "physics": self.physics.name,
+                    "config": self.config, "format": "stsphere-ckpt-v1"}
+            ckpt.begin(root, step, meta, self.fields, self.layout.N, self.layout.n, np.float64)
+        self._barrier()
+        for e in self.engines:
+            ckpt.write_tiles(d, self.fields, e.plan.tiles, self.layout.tile_origin,
+                             e.tiles_view().detach().cpu().double().numpy(), self.layout.n)
+        self._barrier()
+        if self.rank == 0:
+            ckpt.commit(d)
+            ckpt.prune(root, self.cfg.io.keep_checkpoints)
+        self._barrier()
+        return d
+
+    def restore_checkpoint(self, path: str) -> None:
+        meta = ckpt.read_meta(path)
+        arrs = ckpt.read_fields(path, self.fields)
+        if meta["N"] != self.layout.N:
+            raise ValueError(f"checkpoint grid C{meta['N']} != configured C{self.layout.N}")
+        glob = np.stack([arrs[f] for f in self.fields])           # [F,6,N,N]
+        for e in self.engines:
+            loc = np.stack([e.geo.gather_global(glob[k]) for k in range(len(self.fields))])
+            e.set_state(torch.as_tensor(loc, dtype=self.dtype))
+            e.time = float(meta["time"])
+            e.step_count = int(meta["step"])
+        self.set_dt(float(meta["dt"]))
+        self._log(f"Restored {path} (step {meta['step']}, t = {meta['time'] / DAY:.4f} days, "
+                  f"written by {meta['num_ranks']} rank(s), tiles_per_edge {meta['tiles_per_edge']})")

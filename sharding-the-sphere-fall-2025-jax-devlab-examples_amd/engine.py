@@ -122,13 +122,28 @@ class Engine:
         return self.interior(self.state if q is None else q)
 
     # ---- stepping -----------------------------------------------------------
+    canary = False   # debug race screen, HIP backend, eager only
+
     def stage_begin(self, st: Stage) -> None:
+        if self.canary and self.backend == "hip":
+            # every same-rank ghost slot of the output must be re-pushed this stage
+            self.pool[st.out][:, self.halo_dst] = float("nan")
+            if self.transport.recv.numel():
+                self.transport.recv.fill_(float("nan"))
         self.transport.start(self.pool[st.Q])
         self.compute.stage(st, self.dt, None, part="interior")
 
     def stage_end(self, st: Stage) -> None:
         recv = self.transport.finish()
+        if self.canary and self.backend == "hip" and recv is not None and recv.numel():
+            if not bool(torch.isfinite(recv).all()):
+                raise RuntimeError("canary: a remote ghost slot was not delivered by the exchange")
         self.compute.stage(st, self.dt, recv, part="boundary")
+        if self.canary and self.backend == "hip":
+            out = self.pool[st.out]
+            bad = ~torch.isfinite(out[:, self.halo_dst])
+            if bool(bad.any()):
+                raise RuntimeError(f"canary: {int(bad.sum())} ghost slots not written by the stage kernel")
 
     def end_step(self) -> None:
         rot = self.integ.rotation

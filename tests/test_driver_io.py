@@ -1,0 +1,90 @@
+"""Driver, config, checkpoint/restart, history, metrics, zarr."""
+import os
+
+import numpy as np
+import pytest
+import yaml
+
+import stsphere as S
+from stsphere.utils import checkpoint as ckpt, zarr_lite
+from stsphere.utils.history import read_history, read_metrics
+
+
+def _cfg(tmp, nd=1, t=1, **io):
+    return {"parallelization": {"tiles_per_edge": t, "num_devices": nd, "device_type": "cpu"},
+            "grid": {"N": 8}, "physics": {"model": "swe", "case": "tc2"}, "time": {"nsteps": 4},
+            "io": dict({"output_dir": str(tmp)}, **io)}
+
+
+def test_config_roundtrip_and_errors(tmp_path):
+    c = S.load_config(_cfg(tmp_path))
+    p = tmp_path / "c.yaml"
+    S.save_config(c, str(p))
+    assert S.load_config(str(p)).to_dict() == c.to_dict()
+    with pytest.raises(ValueError):
+        S.load_config({"parallelization": {"bogus": 1}})
+    assert S.load_config("parallelization:\n  num_devices: 2\n").parallelization.num_devices == 2
+
+
+def test_shipped_configs_parse():
+    here = os.path.join(S.__path__[0], "configs")
+    files = [f for f in os.listdir(here) if f.endswith(".yaml")]
+    assert files
+    for f in files:
+        S.load_config(os.path.join(here, f))
+
+
+def test_checkpoint_partition_independent(tmp_path):
+    s = S.Solver(_cfg(tmp_path, nd=8, t=2, checkpoint_interval=2), verbose=False)
+    s.run()
+    assert ckpt.list_checkpoints(os.path.join(str(tmp_path), "checkpoints")) == [2, 4]
+    ref = s.gather_global()
+    s2 = S.Solver(_cfg(tmp_path, nd=3, t=1, restore="latest"), verbose=False)
+    s2.initialize()
+    assert s2.step_count == 4 and np.array_equal(s2.gather_global(), ref)
+    # continuing from the restart equals continuing the original
+    s.step(2)
+    s2.step(2)
+    assert np.array_equal(s2.gather_global(), s.gather_global())
+
+
+def test_incomplete_checkpoint_ignored(tmp_path):
+    s = S.Solver(_cfg(tmp_path, checkpoint_interval=2), verbose=False)
+    s.run()
+    d = ckpt.latest_checkpoint(str(tmp_path / "checkpoints"))
+    os.remove(os.path.join(d, ckpt.COMMIT))
+    assert ckpt.latest_checkpoint(str(tmp_path / "checkpoints")).endswith("00000002")
+
+
+def test_history_and_metrics(tmp_path):
+    s = S.Solver(_cfg(tmp_path, nd=2, history_interval=2, metrics_interval=1), verbose=False)
+    s.run()
+    h = read_history(str(tmp_path / "history.zarr"), "h")
+    assert h.shape == (3, 6, 8, 8) and np.allclose(h[-1], s.global_field("h"))
+    t = zarr_lite.read_array(str(tmp_path / "history.zarr"), "time")
+    assert np.allclose(t, [0, 2 * s.dt, 4 * s.dt])
+    m = read_metrics(str(tmp_path / "metrics.jsonl"))
+    assert len(m) == 4 and "mass" in m[-1] and m[-1]["step"] == 4
+
+
+def test_watchdog_raises_on_nan(tmp_path):
+    c = _cfg(tmp_path)
+    c["runtime"] = {"watchdog_interval": 1}
+    c["time"]["dt"] = 1e6          # violently unstable
+    c["time"]["nsteps"] = 50
+    s = S.Solver(c, verbose=False)
+    with pytest.raises(FloatingPointError):
+        s.run()
+
+
+def test_watchdog_recovers_from_checkpoint(tmp_path):
+    c = _cfg(tmp_path, checkpoint_interval=2)
+    c["runtime"] = {"watchdog_interval": 1}
+    s = S.Solver(c, verbose=False)
+    s.initialize()
+    dt0 = s.dt
+    s.run(nsteps=2)                # good checkpoint at step 2
+    s.cfg.io.checkpoint_interval = 0
+    s.set_dt(dt0 * 8)              # unstable from here on
+    s.run(nsteps=40)               # watchdog: restore step 2, halve dt, until stable
+    assert s.all_finite() and s.dt <= dt0
