@@ -54,7 +54,7 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
            "-Wno-unused-result", "-I", CSRC, "-I", "/opt/rocm/include", *VARIANT_FLAGS[variant],
-           *srcs, "-o", lib + ".tmp", "-L/opt/rocm/lib", "-l:librccl.so.1", "-lroctx64"]
+           *srcs, "-o", lib + ".tmp", "-L/opt/rocm/lib", "-l:librccl.so.1", "-lrocprofiler-sdk-roctx"]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)

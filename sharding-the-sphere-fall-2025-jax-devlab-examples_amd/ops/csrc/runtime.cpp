@@ -1,0 +1,298 @@
+// Native step runtime for the cubed-sphere solver (see runtime.h).
+//
+// One rank's time step is a fixed op list (built once in Python from the
+// integrator and the halo plan):
+//
+//   per RK stage, same-rank only :  STAGE(all blocks)
+//   per RK stage, with remote peers:
+//       PACK (compute stream)            boundary cells -> send buffer
+//       COMM_START                       event: compute -> comm stream, then ONE
+//                                        ncclGroupStart/End with a send and a recv
+//                                        per peer (bundled fields/layers/tiles)
+//       STAGE(interior blocks)           overlaps the transfer
+//       COMM_WAIT                        event: comm -> compute stream
+//       STAGE(boundary blocks)           remote ghosts from the receive buffer
+//
+// The list is executed eagerly or captured once into a hipGraph (several steps
+// per graph) and replayed, which removes host launch overhead entirely
+// (SURVEY.md 7.1 "Step capture").  The comm stream has the highest priority
+// so halo traffic is never queued behind interior work.
+#include "runtime.h"
+
+#include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+struct Runtime {
+  std::vector<StspOp> ops;
+  int period = 1;
+  bool use_graph = false;
+  int graph_periods = 1;
+  hipStream_t stream = nullptr;
+  hipStream_t comm_stream = nullptr;
+  ncclComm_t comm = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  bool roctx = false;
+  bool warmed = false;   // one eager period has run (RCCL/stream lazy setup done)
+  std::string err;
+};
+
+#define RT_CHECK(expr)                                                                     \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess) {                                                                \
+      rt->err = std::string(#expr) + ": " + hipGetErrorString(e_);                         \
+      return -1;                                                                           \
+    }                                                                                      \
+  } while (0)
+
+#define NC_CHECK(expr)                                                                     \
+  do {                                                                                     \
+    ncclResult_t r_ = (expr);                                                              \
+    if (r_ != ncclSuccess) {                                                               \
+      rt->err = std::string(#expr) + ": " + ncclGetErrorString(r_);                        \
+      return -2;                                                                           \
+    }                                                                                      \
+  } while (0)
+
+ncclDataType_t nccl_type(int dtype) { return dtype == 1 ? ncclFloat64 : ncclFloat32; }
+size_t elem_bytes(int dtype) { return dtype == 1 ? 8 : 4; }
+
+int run_op(Runtime* rt, const StspOp& op) {
+  switch (op.type) {
+    case STSP_OP_STAGE: {
+      const int rc = stsp_stage_launch(op.phys, op.dtype, op.bx, op.by, &op.stage, rt->stream);
+      if (rc != 0) {
+        rt->err = "stage launch failed: " + std::to_string(rc);
+        return -3;
+      }
+      return 0;
+    }
+    case STSP_OP_PACK: {
+      const int rc = stsp_pack_launch(op.dtype, op.q, op.S, op.F, op.idx, op.ns, op.send, rt->stream);
+      if (rc != 0) {
+        rt->err = "pack launch failed: " + std::to_string(rc);
+        return -3;
+      }
+      return 0;
+    }
+    case STSP_OP_COMM_START: {
+      if (!rt->comm) {
+        rt->err = "COMM op without an RCCL communicator";
+        return -4;
+      }
+      RT_CHECK(hipEventRecord(rt->ev_fork, rt->stream));
+      RT_CHECK(hipStreamWaitEvent(rt->comm_stream, rt->ev_fork, 0));
+      const size_t eb = elem_bytes(op.dtype);
+      const ncclDataType_t ty = nccl_type(op.dtype);
+      NC_CHECK(ncclGroupStart());
+      for (int k = 0; k < op.npeers; ++k) {
+        const char* p = static_cast<const char*>(op.sendbuf) + (size_t)op.send_off[k] * op.slot_elems * eb;
+        NC_CHECK(ncclSend(p, (size_t)op.send_cnt[k] * op.slot_elems, ty, op.send_peer[k], rt->comm, rt->comm_stream));
+      }
+      for (int k = 0; k < op.nrecv; ++k) {
+        char* p = static_cast<char*>(op.recvbuf) + (size_t)op.recv_off[k] * op.slot_elems * eb;
+        NC_CHECK(ncclRecv(p, (size_t)op.recv_cnt[k] * op.slot_elems, ty, op.recv_peer[k], rt->comm, rt->comm_stream));
+      }
+      NC_CHECK(ncclGroupEnd());
+      return 0;
+    }
+    case STSP_OP_COMM_WAIT: {
+      RT_CHECK(hipEventRecord(rt->ev_join, rt->comm_stream));
+      RT_CHECK(hipStreamWaitEvent(rt->stream, rt->ev_join, 0));
+      return 0;
+    }
+  }
+  rt->err = "unknown op type " + std::to_string(op.type);
+  return -5;
+}
+
+bool debug_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("STSP_RT_DEBUG");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+
+int run_period(Runtime* rt, bool mark) {
+  for (const StspOp& op : rt->ops) {
+    if (debug_enabled()) {
+      std::fprintf(stderr, "[stsp_rt] op type=%d phys=%d nblocks=%d remote=%d npeers=%d nrecv=%d comm=%p\n", op.type,
+                   op.phys, op.stage.nblocks, op.stage.remote, op.npeers, op.nrecv, (void*)rt->comm);
+      std::fflush(stderr);
+    }
+    if (mark) {
+      const char* names[] = {"?", "stage", "pack", "comm", "comm_wait"};
+      roctxRangePush(names[op.type >= 1 && op.type <= 4 ? op.type : 0]);
+    }
+    const int rc = run_op(rt, op);
+    if (mark) roctxRangePop();
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+int ensure_graph(Runtime* rt) {
+  if (rt->exec) return 0;
+  RT_CHECK(hipStreamBeginCapture(rt->stream, hipStreamCaptureModeRelaxed));
+  int rc = 0;
+  for (int p = 0; p < rt->graph_periods && rc == 0; ++p) rc = run_period(rt, false);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(rt->stream, &g);
+  if (rc) {
+    if (g) hipGraphDestroy(g);
+    return rc;
+  }
+  if (e != hipSuccess) {
+    rt->err = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
+    return -1;
+  }
+  rt->graph = g;
+  RT_CHECK(hipGraphInstantiate(&rt->exec, rt->graph, nullptr, nullptr, 0));
+  return 0;
+}
+
+void drop_graph(Runtime* rt) {
+  if (rt->exec) hipGraphExecDestroy(rt->exec);
+  if (rt->graph) hipGraphDestroy(rt->graph);
+  rt->exec = nullptr;
+  rt->graph = nullptr;
+}
+
+}  // namespace
+
+extern "C" void* stsp_rt_create(const StspRtDesc* d) {
+  auto* rt = new Runtime();
+  if (debug_enabled())
+    std::fprintf(stderr, "[stsp_rt] create nops=%d period=%d graph=%d sizeof(StspOp)=%zu sizeof(StageDesc)=%zu\n",
+                 d->nops, d->period, d->use_graph, sizeof(StspOp), sizeof(StageDesc));
+  rt->ops.assign(d->ops, d->ops + d->nops);
+  rt->period = d->period > 0 ? d->period : 1;
+  rt->use_graph = d->use_graph != 0;
+  rt->graph_periods = d->graph_periods > 0 ? d->graph_periods : 1;
+  rt->stream = static_cast<hipStream_t>(d->stream);
+  rt->comm = static_cast<ncclComm_t>(d->nccl_comm);
+  rt->roctx = d->roctx != 0;
+  int lo = 0, hi = 0;
+  hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (hipStreamCreateWithPriority(&rt->comm_stream, hipStreamNonBlocking, hi) != hipSuccess ||
+      hipEventCreateWithFlags(&rt->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&rt->ev_join, hipEventDisableTiming) != hipSuccess) {
+    rt->err = "stream/event creation failed";
+  }
+  return rt;
+}
+
+extern "C" void stsp_rt_destroy(void* p) {
+  auto* rt = static_cast<Runtime*>(p);
+  if (!rt) return;
+  drop_graph(rt);
+  if (rt->ev_fork) hipEventDestroy(rt->ev_fork);
+  if (rt->ev_join) hipEventDestroy(rt->ev_join);
+  if (rt->comm_stream) hipStreamDestroy(rt->comm_stream);
+  delete rt;
+}
+
+extern "C" const char* stsp_rt_last_error(void* p) {
+  return static_cast<Runtime*>(p)->err.c_str();
+}
+
+extern "C" int stsp_rt_set_dt(void* p, double dt) {
+  auto* rt = static_cast<Runtime*>(p);
+  for (StspOp& op : rt->ops)
+    if (op.type == STSP_OP_STAGE) op.stage.dt = dt;
+  drop_graph(rt);
+  return 0;
+}
+
+extern "C" int stsp_rt_run(void* p, int nsteps) {
+  auto* rt = static_cast<Runtime*>(p);
+  if (!rt->err.empty() && !rt->comm_stream) return -6;
+  if (nsteps % rt->period) {
+    rt->err = "nsteps must be a multiple of the op-list period";
+    return -7;
+  }
+  int periods = nsteps / rt->period;
+  if (rt->use_graph && !rt->warmed && periods > 0) {
+    // RCCL and the comm stream do lazy one-time setup on first use, which is
+    // illegal inside a capture: run the first period eagerly (it counts).
+    const int rc = run_period(rt, rt->roctx);
+    if (rc) return rc;
+    RT_CHECK(hipStreamSynchronize(rt->stream));
+    rt->warmed = true;
+    --periods;
+  }
+  if (rt->use_graph && periods >= rt->graph_periods) {
+    const int rc = ensure_graph(rt);
+    if (rc) return rc;
+    const int launches = periods / rt->graph_periods;
+    for (int i = 0; i < launches; ++i) RT_CHECK(hipGraphLaunch(rt->exec, rt->stream));
+    periods -= launches * rt->graph_periods;
+  }
+  for (int i = 0; i < periods; ++i) {
+    const int rc = run_period(rt, rt->roctx);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// ---- RCCL bootstrap -----------------------------------------------------------
+
+extern "C" int stsp_nccl_id_bytes(void) { return NCCL_UNIQUE_ID_BYTES; }
+
+extern "C" int stsp_nccl_unique_id(void* out) {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
+  std::memcpy(out, &id, sizeof(id));
+  return 0;
+}
+
+extern "C" void* stsp_nccl_comm_init(int nranks, const void* idbytes, int rank, int device) {
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  ncclUniqueId id;
+  std::memcpy(&id, idbytes, sizeof(id));
+  ncclComm_t comm = nullptr;
+  if (ncclCommInitRank(&comm, nranks, id, rank) != ncclSuccess) return nullptr;
+  return comm;
+}
+
+extern "C" int stsp_nccl_comm_destroy(void* comm) {
+  if (!comm) return 0;
+  return ncclCommDestroy(static_cast<ncclComm_t>(comm)) == ncclSuccess ? 0 : -1;
+}
+
+extern "C" int stsp_nccl_selftest(void* comm, void* stream) {
+  // 1-element send/recv to self through the same grouped path the halo uses.
+  ncclComm_t c = static_cast<ncclComm_t>(comm);
+  int rank = 0;
+  if (ncclCommUserRank(c, &rank) != ncclSuccess) return -1;
+  double* buf = nullptr;
+  if (hipMalloc(&buf, 2 * sizeof(double)) != hipSuccess) return -2;
+  const double v = 42.0 + rank;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipMemcpyAsync(buf, &v, sizeof(double), hipMemcpyHostToDevice, s);
+  hipMemsetAsync(buf + 1, 0, sizeof(double), s);
+  ncclGroupStart();
+  ncclSend(buf, 1, ncclFloat64, rank, c, s);
+  ncclRecv(buf + 1, 1, ncclFloat64, rank, c, s);
+  const ncclResult_t r = ncclGroupEnd();
+  double out = 0;
+  hipMemcpyAsync(&out, buf + 1, sizeof(double), hipMemcpyDeviceToHost, s);
+  hipStreamSynchronize(s);
+  hipFree(buf);
+  if (r != ncclSuccess) return -3;
+  return out == v ? 0 : -4;
+}
+
+extern "C" int stsp_roctx_push(const char* msg) { return roctxRangePush(msg); }
+extern "C" int stsp_roctx_pop(void) { return roctxRangePop(); }

@@ -1,0 +1,59 @@
+// Native step runtime (C ABI): an op list for one integrator period, executed
+// eagerly or captured once into a hipGraph and replayed.  Owns the RCCL
+// communicator used for halo P2P and a high-priority comm stream.
+#pragma once
+#include "stsp_kernels.h"
+
+extern "C" {
+
+enum StspOpType { STSP_OP_STAGE = 1, STSP_OP_PACK = 2, STSP_OP_COMM_START = 3, STSP_OP_COMM_WAIT = 4 };
+
+#define STSP_MAX_PEERS 32
+
+typedef struct StspOp {
+  int type;
+  // STAGE
+  int phys, dtype, bx, by;
+  StageDesc stage;
+  // PACK
+  const void* q;
+  int S, F;
+  const int* idx;
+  int ns;
+  void* send;
+  // COMM_START: one grouped ncclSend/ncclRecv per peer on the comm stream
+  int npeers;
+  int send_peer[STSP_MAX_PEERS], send_off[STSP_MAX_PEERS], send_cnt[STSP_MAX_PEERS];
+  int nrecv;
+  int recv_peer[STSP_MAX_PEERS], recv_off[STSP_MAX_PEERS], recv_cnt[STSP_MAX_PEERS];
+  void* sendbuf;
+  void* recvbuf;
+  int slot_elems;  // elements per slot (= F)
+} StspOp;
+
+typedef struct StspRtDesc {
+  int nops;
+  const StspOp* ops;      // ops of `period` steps
+  int period;             // steps covered by the op list
+  int use_graph;          // capture graph_periods * period steps into one hipGraph
+  int graph_periods;
+  void* stream;           // compute stream (hipStream_t), never the legacy null stream when use_graph
+  void* nccl_comm;        // ncclComm_t (nullable when there is no COMM op)
+  int roctx;              // emit roctx ranges around ops (eager runs)
+} StspRtDesc;
+
+void* stsp_rt_create(const StspRtDesc* d);
+void stsp_rt_destroy(void* rt);
+int stsp_rt_run(void* rt, int nsteps);          // nsteps must be a multiple of period
+const char* stsp_rt_last_error(void* rt);
+int stsp_rt_set_dt(void* rt, double dt);         // rewrites dt in every stage op; drops the graph
+
+int stsp_nccl_id_bytes(void);
+int stsp_nccl_unique_id(void* out);              // out: stsp_nccl_id_bytes() bytes
+void* stsp_nccl_comm_init(int nranks, const void* id, int rank, int device);
+int stsp_nccl_comm_destroy(void* comm);
+int stsp_nccl_selftest(void* comm, void* stream);   // 1-element send/recv to self (rank-local check)
+
+int stsp_roctx_push(const char* msg);
+int stsp_roctx_pop(void);
+}

@@ -1,0 +1,239 @@
+"""Python side of the native step runtime (``ops/csrc/runtime.cpp``).
+
+``NativeStepper(engine)`` turns an engine's integrator period into a C++ op
+list (stage kernels; for ranks with remote neighbours also pack + RCCL grouped
+send/recv on a high-priority comm stream + interior/boundary split) and hands
+stepping to C++: eager, or captured once into a hipGraph and replayed.  The
+RCCL communicator is created here (``create_nccl_comm``) and owned natively;
+torch.distributed is used only to broadcast the unique id.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import torch
+
+from . import native
+from .native import StageDesc
+
+MAX_PEERS = 32
+OP_STAGE, OP_PACK, OP_COMM_START, OP_COMM_WAIT = 1, 2, 3, 4
+
+_I32x = ctypes.c_int * MAX_PEERS
+
+
+class StspOp(ctypes.Structure):
+    _fields_ = [
+        ("type", ctypes.c_int),
+        ("phys", ctypes.c_int), ("dtype", ctypes.c_int), ("bx", ctypes.c_int), ("by", ctypes.c_int),
+        ("stage", StageDesc),
+        ("q", ctypes.c_void_p), ("S", ctypes.c_int), ("F", ctypes.c_int), ("idx", ctypes.c_void_p),
+        ("ns", ctypes.c_int), ("send", ctypes.c_void_p),
+        ("npeers", ctypes.c_int), ("send_peer", _I32x), ("send_off", _I32x), ("send_cnt", _I32x),
+        ("nrecv", ctypes.c_int), ("recv_peer", _I32x), ("recv_off", _I32x), ("recv_cnt", _I32x),
+        ("sendbuf", ctypes.c_void_p), ("recvbuf", ctypes.c_void_p), ("slot_elems", ctypes.c_int),
+    ]
+
+
+class StspRtDesc(ctypes.Structure):
+    _fields_ = [
+        ("nops", ctypes.c_int), ("ops", ctypes.POINTER(StspOp)), ("period", ctypes.c_int),
+        ("use_graph", ctypes.c_int), ("graph_periods", ctypes.c_int), ("stream", ctypes.c_void_p),
+        ("nccl_comm", ctypes.c_void_p), ("roctx", ctypes.c_int),
+    ]
+
+
+def _declare(L):
+    vp, ci, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    L.stsp_rt_create.argtypes = [ctypes.POINTER(StspRtDesc)]
+    L.stsp_rt_create.restype = vp
+    L.stsp_rt_destroy.argtypes = [vp]
+    L.stsp_rt_destroy.restype = None
+    L.stsp_rt_run.argtypes = [vp, ci]
+    L.stsp_rt_run.restype = ci
+    L.stsp_rt_set_dt.argtypes = [vp, cd]
+    L.stsp_rt_set_dt.restype = ci
+    L.stsp_rt_last_error.argtypes = [vp]
+    L.stsp_rt_last_error.restype = ctypes.c_char_p
+    L.stsp_nccl_id_bytes.argtypes = []
+    L.stsp_nccl_id_bytes.restype = ci
+    L.stsp_nccl_unique_id.argtypes = [vp]
+    L.stsp_nccl_unique_id.restype = ci
+    L.stsp_nccl_comm_init.argtypes = [ci, vp, ci, ci]
+    L.stsp_nccl_comm_init.restype = vp
+    L.stsp_nccl_comm_destroy.argtypes = [vp]
+    L.stsp_nccl_comm_destroy.restype = ci
+    L.stsp_nccl_selftest.argtypes = [vp, vp]
+    L.stsp_nccl_selftest.restype = ci
+    L.stsp_roctx_push.argtypes = [ctypes.c_char_p]
+    L.stsp_roctx_push.restype = ci
+    L.stsp_roctx_pop.argtypes = []
+    L.stsp_roctx_pop.restype = ci
+    return L
+
+
+def lib():
+    return _declare(native.require_native())
+
+
+def create_nccl_comm(rank: int, world: int, device_index: int, group=None) -> int:
+    """RCCL communicator owned by the native runtime; the unique id travels
+    over the existing torch.distributed process group."""
+    import torch.distributed as dist
+    L = lib()
+    nb = L.stsp_nccl_id_bytes()
+    buf = (ctypes.c_char * nb)()
+    if rank == 0:
+        if L.stsp_nccl_unique_id(buf) != 0:
+            raise RuntimeError("ncclGetUniqueId failed")
+    dev = torch.device(f"cuda:{device_index}") if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    t = torch.tensor(list(bytes(buf)), dtype=torch.uint8, device=dev)
+    dist.broadcast(t, src=0, group=group)
+    raw = bytes(t.cpu().tolist())
+    idbuf = (ctypes.c_char * nb).from_buffer_copy(raw)
+    comm = L.stsp_nccl_comm_init(world, idbuf, rank, device_index)
+    if not comm:
+        raise RuntimeError("ncclCommInitRank failed")
+    return comm
+
+
+def nccl_selftest(comm: int) -> None:
+    L = lib()
+    s = torch.cuda.current_stream()
+    rc = L.stsp_nccl_selftest(comm, int(s.cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"RCCL self send/recv failed ({rc})")
+
+
+class NativeStepper:
+    """Steps an ``Engine(backend='hip')`` entirely from C++."""
+
+    def __init__(self, engine, nccl_comm: Optional[int] = None, use_graph: bool = True,
+                 steps_per_graph: int = 30, roctx: bool = False, stream: Optional[torch.cuda.Stream] = None):
+        from .hip_compute import HipCompute
+        e = engine
+        if not isinstance(e.compute, HipCompute):
+            raise RuntimeError("NativeStepper needs an Engine with backend='hip'")
+        self.e = e
+        self.L = lib()
+        hc = e.compute
+        plan = e.plan
+        self.remote = plan.num_recv > 0 or plan.num_send > 0
+        if self.remote and not nccl_comm:
+            raise RuntimeError("rank has remote neighbours: pass an RCCL communicator (create_nccl_comm)")
+        if len(plan.send_peers) > MAX_PEERS or len(plan.recv_peers) > MAX_PEERS:
+            raise RuntimeError("too many peers for the native runtime")
+        F = e.physics.F
+        self.send = torch.zeros((max(plan.num_send, 1), F), dtype=e.dtype, device=e.device)
+        self.send_idx = torch.as_tensor(plan.send_idx, dtype=torch.int32, device=e.device)
+        assert (plan.send_idx.size == 0) or int(plan.send_idx.max()) < plan.S
+        self.stream = stream or torch.cuda.Stream(device=e.device)
+        period = e.integ.period
+        self.period = period
+        ops: List[StspOp] = []
+        pool = list(e.pool)
+        saved_pool = e.pool
+        for _ in range(period):
+            e.pool = pool
+            for st in e.integ.stages:
+                if not hc.remote:
+                    ops.append(self._stage_op(hc.desc(st, e.dt, None, hc.nblocks)))
+                    continue
+                op = StspOp()
+                op.type = OP_PACK
+                op.dtype = hc.dcode
+                op.q = native.ptr(pool[st.Q])
+                op.S = plan.S
+                op.F = F
+                op.idx = native.ptr(self.send_idx)
+                op.ns = plan.num_send
+                op.send = native.ptr(self.send)
+                ops.append(op)
+                ops.append(self._comm_op(hc.dcode, F))
+                if hc.blk_interior.numel():
+                    ops.append(self._stage_op(hc.desc(st, e.dt, hc.blk_interior, hc.blk_interior.numel())))
+                w = StspOp()
+                w.type = OP_COMM_WAIT
+                ops.append(w)
+                if hc.blk_boundary.numel():
+                    ops.append(self._stage_op(hc.desc(st, e.dt, hc.blk_boundary, hc.blk_boundary.numel(), remote=True)))
+            pool = [pool[r] for r in e.integ.rotation]
+        e.pool = saved_pool
+        self._ops = (StspOp * len(ops))(*ops)
+        d = StspRtDesc()
+        d.nops = len(ops)
+        d.ops = self._ops
+        d.period = period
+        # hipGraph capture of the RCCL P2P ops segfaults inside the RCCL 2.26.6 that
+        # ships with this PyTorch (measured: eager loopback exact, captured crash), so
+        # op lists with comm run eagerly from C++ unless STSP_GRAPH_COMM=1.
+        import os
+        graph_ok = (not self.remote) or os.environ.get("STSP_GRAPH_COMM") == "1"
+        self.use_graph = bool(use_graph and graph_ok)
+        d.use_graph = 1 if self.use_graph else 0
+        d.graph_periods = max(1, steps_per_graph // period)
+        d.stream = int(self.stream.cuda_stream)
+        d.nccl_comm = nccl_comm or 0
+        d.roctx = 1 if roctx else 0
+        self._desc = d
+        self.h = self.L.stsp_rt_create(ctypes.byref(d))
+        if not self.h:
+            raise RuntimeError("stsp_rt_create failed")
+
+    def _stage_op(self, sd: StageDesc) -> StspOp:
+        hc = self.e.compute
+        op = StspOp()
+        op.type = OP_STAGE
+        op.phys, op.dtype, op.bx, op.by = hc.phys_id, hc.dcode, hc.bx, hc.by
+        op.stage = sd
+        return op
+
+    def _comm_op(self, dcode: int, F: int) -> StspOp:
+        p = self.e.plan
+        op = StspOp()
+        op.type = OP_COMM_START
+        op.dtype = dcode
+        op.npeers = len(p.send_peers)
+        for k, (peer, off, cnt) in enumerate(zip(p.send_peers, p.send_offsets, p.send_counts)):
+            op.send_peer[k], op.send_off[k], op.send_cnt[k] = peer, off, cnt
+        op.nrecv = len(p.recv_peers)
+        for k, (peer, off, cnt) in enumerate(zip(p.recv_peers, p.recv_offsets, p.recv_counts)):
+            op.recv_peer[k], op.recv_off[k], op.recv_cnt[k] = peer, off, cnt
+        op.sendbuf = native.ptr(self.send)
+        op.recvbuf = native.ptr(self.e.transport.recv)
+        op.slot_elems = F
+        return op
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            msg = self.L.stsp_rt_last_error(self.h)
+            raise RuntimeError(f"native runtime {what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def run(self, nsteps: int) -> None:
+        e = self.e
+        full = (nsteps // self.period) * self.period
+        if full:
+            # the compute stream follows torch's current stream and vice versa
+            self.stream.wait_stream(torch.cuda.current_stream(e.device))
+            self._check(self.L.stsp_rt_run(self.h, full), "run")
+            torch.cuda.current_stream(e.device).wait_stream(self.stream)
+            e.time += full * e.dt
+            e.step_count += full
+        if nsteps - full:
+            e.step(nsteps - full)
+
+    def set_dt(self, dt: float) -> None:
+        self.e.dt = dt
+        self._check(self.L.stsp_rt_set_dt(self.h, dt), "set_dt")
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.L.stsp_rt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

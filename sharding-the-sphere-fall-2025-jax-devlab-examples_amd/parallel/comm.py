@@ -168,3 +168,28 @@ class VirtualTransport(Transport):
             assert sc == cnt
             self.recv[off:off + cnt] = self.hub.sends[peer][so:so + sc].to(self.recv.device)
         return self.recv
+
+
+class NativeBuffers(Transport):
+    """Receive buffer for ranks whose halo traffic is driven by the native
+    runtime (RCCL inside ``ops.native_runtime.NativeStepper``); Python-side
+    stepping is not available through it."""
+
+    def start(self, q):
+        raise RuntimeError("halo traffic of this engine is owned by the native runtime; step with NativeStepper")
+
+    def finish(self):
+        raise RuntimeError("halo traffic of this engine is owned by the native runtime; step with NativeStepper")
+
+
+class LoopbackTransport(Transport):
+    """Single-rank loopback (layout.loopback): pack and copy into the receive
+    buffer in-process (the torch-side twin of an RCCL self send/recv)."""
+
+    def start(self, q):
+        self.send = self.pack_fn(q, self.send_idx)
+
+    def finish(self):
+        if self.recv.numel():
+            self.recv.copy_(self.send)
+        return self.recv

@@ -61,7 +61,7 @@ class TileLayout:
     """Global tiling of a C<N> cubed sphere into 6 t^2 tiles over `num_ranks`."""
 
     def __init__(self, N: int, tiles_per_edge: int = 1, num_ranks: int = 1, ng: int = 2,
-                 partition: str = "auto", owner: Optional[Sequence[int]] = None):
+                 partition: str = "auto", owner: Optional[Sequence[int]] = None, loopback: bool = False):
         if N % tiles_per_edge:
             raise ValueError(f"N = {N} is not divisible by tiles_per_edge = {tiles_per_edge}")
         validate_device_count(num_ranks, tiles_per_edge)
@@ -72,6 +72,9 @@ class TileLayout:
         if ng > self.n:
             raise ValueError(f"halo width ng = {ng} exceeds tile size n = {self.n}")
         self.num_ranks = num_ranks
+        # loopback (test/debug): every ghost, even a same-rank one, goes through
+        # the pack -> send/recv -> receive-buffer path with the rank as its own peer
+        self.loopback = loopback
         self.partition = partition
         self.owner = list(owner) if owner is not None else partition_tiles(tiles_per_edge, num_ranks, partition)
         self.num_tiles = 6 * tiles_per_edge ** 2
@@ -191,7 +194,7 @@ class RankPlan:
         tid, _, _ = L.locate(src)
         own = np.asarray(L.owner)[tid]
         gmap = np.empty(src.shape, dtype=np.int64)
-        local = own == self.rank
+        local = (own == self.rank) & (not L.loopback)
         if local.any():
             gmap[local] = L.local_flat(src[local])
         # remote: recv slots, peers in ascending order
@@ -217,7 +220,7 @@ class RankPlan:
         idx = []
         off = 0
         for p in range(L.num_ranks):
-            if p == self.rank:
+            if p == self.rank and not L.loopback:
                 continue
             need = L.needs(p, self.rank)
             if len(need) == 0:
@@ -244,7 +247,7 @@ class RankPlan:
                 for k in range(g):
                     x, y = ghost_xy(s, k, pos, n)
                     dst = (t * P + y + g) * P + x + g
-                    loc = own[t, s, k] == self.rank
+                    loc = (own[t, s, k] == self.rank) & (not L.loopback)
                     if not loc.any():
                         continue
                     c = src[t, s, k][loc]

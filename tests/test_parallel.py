@@ -65,3 +65,18 @@ def test_gloo_multiprocess_equals_single(world, t, staged):
     for f in range(4):
         glob = assemble_global(L, {r: np.load(os.path.join(out, f"r{r}.npy"))[f] for r in range(world)})
         assert np.array_equal(glob, single.global_field(f))
+
+
+def test_loopback_layout_equals_single():
+    from stsphere.parallel.comm import LoopbackTransport
+    N = 12
+    g = CubedSphereGrid(N)
+    L = TileLayout(N, 2, 1, ng=2, loopback=True)
+    p = L.plan(0)
+    assert p.recv_peers == [0] and p.send_peers == [0] and (p.ghost_map < 0).all() and (p.push_map < 0).all()
+    single = Engine(ShallowWater("tc5"), TileLayout(N, 2, 1, ng=2), grid=g)
+    lb = Engine(ShallowWater("tc5"), L, grid=g, dt=single.dt,
+                transport=LoopbackTransport(p, 4, torch.float64, torch.device("cpu")))
+    single.step(3)
+    lb.step(3)
+    assert torch.equal(single.tiles_view(), lb.tiles_view())
