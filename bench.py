@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--integrator", default="ssprk3")
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
-    ap.add_argument("--runtime", default="auto", choices=["auto", "native", "graph", "eager"])
+    ap.add_argument("--runtime", default="auto", choices=["auto", "persistent", "native", "graph", "eager"])
     ap.add_argument("--steps-per-graph", type=int, default=30)
     ap.add_argument("--partition", default="auto")
     ap.add_argument("--dt", type=float, default=None)
@@ -89,7 +89,11 @@ def main():
                  backend=backend, integrator=a.integrator, dt=a.dt)
 
     runner = None
-    if runtime == "native":
+    if runtime == "persistent":
+        from stsphere.ops.persistent import PersistentStepper
+        runner = PersistentStepper(eng, timeout_s=5.0, max_steps_per_launch=1000)
+        step = runner.run
+    elif runtime == "native":
         # C++ runtime: hipGraph replay on one GPU; RCCL grouped P2P on a
         # high-priority stream + interior/boundary overlap on several
         from stsphere.ops.native_runtime import NativeStepper, create_nccl_comm
@@ -120,6 +124,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if runtime == "persistent":
+        runner.check()
     diag = eng.diagnostics()
     if world > 1:
         t = torch.tensor([diag.get("mass", 0.0)], dtype=torch.float64, device=device)

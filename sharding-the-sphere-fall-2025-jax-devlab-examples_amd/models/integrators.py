@@ -88,3 +88,19 @@ def get_integrator(name: str) -> Integrator:
         return INTEGRATORS[name.lower()]()
     except KeyError:
         raise ValueError(f"unknown integrator {name!r}; choose from {sorted(INTEGRATORS)}")
+
+
+def persistent_safe(integ: Integrator) -> bool:
+    """True if the stage sequence can run in the persistent kernel, where
+    neighbouring blocks may be one stage apart: the buffer a stage writes must
+    never be the halo-read input of the previous stage (cyclically), and the
+    step must be buffer-invariant (period 1)."""
+    if integ.period != 1:
+        return False
+    st = integ.stages
+    n = len(st)
+    for k in range(n):
+        nxt = st[(k + 1) % n]
+        if nxt.out == st[k].Q:
+            return False
+    return True

@@ -149,8 +149,40 @@ __device__ __forceinline__ void swe_flux(const T (&wl)[4], const T (&wr)[4], con
   }
 }
 
-template <typename T, int P, int BX, int BY, int LIM, bool REMOTE, bool LIST>
-__global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
+// State access: plain in launch-per-stage kernels; in the persistent kernel,
+// agent-scope relaxed atomics, which gfx950 lowers to global_load/store ... sc1
+// (L1 bypass / write-through), the hand-off form of cdna_hip_programming.md
+// Guideline 16 (R1) measured valid for one workgroup per CU.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+template <bool SYNC, typename T>
+__device__ __forceinline__ T ld_state(const T* p) {
+  if constexpr (!SYNC) {
+    return *p;
+  } else if constexpr (sizeof(T) == 8) {
+    return __builtin_bit_cast(T, __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  } else {
+    return __builtin_bit_cast(T, __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
+}
+
+template <bool SYNC, typename T>
+__device__ __forceinline__ void st_state(T* p, T v) {
+  if constexpr (!SYNC) {
+    *p = v;
+  } else if constexpr (sizeof(T) == 8) {
+    __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __hip_atomic_store((gu32*)p, __builtin_bit_cast(unsigned int, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// One RK stage of one BX x BY block (all phases).  SYNC = persistent-kernel
+// mode: every access to state written by other workgroups in this launch is an
+// agent-scope sc1 access (L1 bypass, write-through), see persistent_kernel.
+template <typename T, int P, int BX, int BY, int LIM, bool REMOTE, bool SYNC>
+__device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   constexpr int F = Phys<P>::F;
   constexpr int NG = Phys<P>::NG;
   constexpr int FL = Phys<P>::FL;              // primitive fields (+ sound speed) in LDS
@@ -178,25 +210,8 @@ __global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
   __shared__ T s_lx[SW ? BY : 1][SW ? BX + 1 : 1];     // edge lengths (for the curvature balance)
   __shared__ T s_ly[SW ? BY + 1 : 1][SW ? BX : 1];
 
-  // Pin every kernel argument in SGPRs here: hipcc otherwise issues the
-  // kernarg scalar loads lazily, each behind its own lgkmcnt(0).
-  asm volatile("" ::"s"(a.X), "s"(a.Q), "s"(a.acc_in), "s"(a.out), "s"(a.acc_out), "s"(a.recv), "s"(a.gmap),
-               "s"(a.push), "s"(a.blocks));
-  asm volatile("" ::"s"(a.invA), "s"(a.ex), "s"(a.ey), "s"(a.mx), "s"(a.my), "s"(a.cgeo));
-  asm volatile("" ::"s"(a.ntile), "s"(a.n), "s"(a.S), "s"(a.mg), "s"(a.pw), "s"(a.nblocks));
-  asm volatile("" ::"s"(a.a0), "s"(a.a1), "s"(a.a2), "s"(a.c0), "s"(a.c1), "s"(a.c2), "s"(a.dt), "s"(a.g),
-               "s"(a.omega2));
   const int n = a.n, S = a.S, nn = n * n, mg = a.mg, pw = a.pw;
   const int nbx = (n + BX - 1) / BX, nby = (n + BY - 1) / BY;
-  int bid;
-  if constexpr (LIST) {
-    bid = a.blocks[blockIdx.x];
-  } else {
-    // XCD-aware bijective remap: logical blocks [k*nb/8, ...) share one XCD.
-    const int nb = a.nblocks, orig = blockIdx.x;
-    const int xcd = orig & 7, q = nb >> 3, r = nb & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  }
   const int tile = bid / (nbx * nby);
   const int rem = bid - tile * nbx * nby;
   const int yb = rem / nbx, xb = rem - yb * nbx;
@@ -222,11 +237,11 @@ __global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
   if (own) {
     if (need_x) {
 #pragma unroll
-      for (int f = 0; f < F; ++f) xs[f] = a.X[(long)f * S + pc];
+      for (int f = 0; f < F; ++f) xs[f] = ld_state<SYNC>(a.X + (long)f * S + pc);
     }
     if (need_acc) {
 #pragma unroll
-      for (int f = 0; f < F; ++f) acs[f] = a.acc_in[(long)f * S + pc];
+      for (int f = 0; f < F; ++f) acs[f] = ld_state<SYNC>(a.acc_in + (long)f * S + pc);
     }
     if constexpr (P == 2) {
       T rec[8];
@@ -284,7 +299,7 @@ __global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
       s_w[0][ly][lx] = v[0];
     }
   };
-  const bool pairs = !REMOTE && ((EX & 1) == 0) && (((mg - NG) & 1) == 0) && ((pw & 1) == 0);
+  const bool pairs = !REMOTE && !SYNC && ((EX & 1) == 0) && (((mg - NG) & 1) == 0) && ((pw & 1) == 0);
   if (pairs) {
     constexpr int HX = EX / 2;
     if (tid < HX * EY) {
@@ -304,7 +319,7 @@ __global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
           }
         } else {
 #pragma unroll
-          for (int f = 0; f < F; ++f) v0[f] = a.Q[(long)f * S + pa];
+          for (int f = 0; f < F; ++f) v0[f] = ld_state<SYNC>(a.Q + (long)f * S + pa);
         }
       }
       put(ly, lx, v0);
@@ -332,13 +347,13 @@ __global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
             from_recv = true;
             const T* rp = a.recv + (long)(-1 - m) * F;
 #pragma unroll
-            for (int f = 0; f < F; ++f) v[f] = rp[f];
+            for (int f = 0; f < F; ++f) v[f] = ld_state<SYNC>(rp + f);
           }
         }
       }
       if (!from_recv) {
 #pragma unroll
-        for (int f = 0; f < F; ++f) v[f] = a.Q[(long)f * S + pa];
+        for (int f = 0; f < F; ++f) v[f] = ld_state<SYNC>(a.Q + (long)f * S + pa);
       }
     }
     put(ly, lx, v);
@@ -486,18 +501,140 @@ __global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
       p[1] -= d * r0; p[2] -= d * r1; p[3] -= d * r2;
     }
 #pragma unroll
-    for (int f = 0; f < F; ++f) a.acc_out[(long)f * S + pc] = p[f];
+    for (int f = 0; f < F; ++f) st_state<SYNC>(a.acc_out + (long)f * S + pc, p[f]);
   }
 #pragma unroll
-  for (int f = 0; f < F; ++f) a.out[(long)f * S + pc] = o[f];
+  for (int f = 0; f < F; ++f) st_state<SYNC>(a.out + (long)f * S + pc, o[f]);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (pt[k] >= 0) {
 #pragma unroll
-      for (int f = 0; f < F; ++f) a.out[(long)f * S + pt[k]] = o[f];
+      for (int f = 0; f < F; ++f) st_state<SYNC>(a.out + (long)f * S + pt[k], o[f]);
     }
   }
   STAMP(6);
+}
+
+
+// XCD-aware bijective remap: logical blocks [k*nb/8, ...) share one XCD
+// (blocks b and b+8 are dealt to the same XCD), so neighbouring blocks, which
+// share halo cells, share an L2.  Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int orig, int nb) {
+  const int xcd = orig & 7, q = nb >> 3, r = nb & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+template <typename T>
+__device__ __forceinline__ void pin_args(const Args<T>& a) {
+  // Pin every kernel argument in SGPRs here: hipcc otherwise issues the
+  // kernarg scalar loads lazily, each behind its own lgkmcnt(0) (3-4 serial
+  // round trips in the prologue, seen with in-kernel stamps).
+  asm volatile("" ::"s"(a.X), "s"(a.Q), "s"(a.acc_in), "s"(a.out), "s"(a.acc_out), "s"(a.recv), "s"(a.gmap),
+               "s"(a.push), "s"(a.blocks));
+  asm volatile("" ::"s"(a.invA), "s"(a.ex), "s"(a.ey), "s"(a.mx), "s"(a.my), "s"(a.cgeo));
+  asm volatile("" ::"s"(a.ntile), "s"(a.n), "s"(a.S), "s"(a.mg), "s"(a.pw), "s"(a.nblocks));
+  asm volatile("" ::"s"(a.a0), "s"(a.a1), "s"(a.a2), "s"(a.c0), "s"(a.c1), "s"(a.c2), "s"(a.dt), "s"(a.g),
+               "s"(a.omega2));
+}
+
+template <typename T, int P, int BX, int BY, int LIM, bool REMOTE, bool LIST>
+__global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
+  pin_args(a);
+  const int bid = LIST ? a.blocks[blockIdx.x] : xcd_remap(blockIdx.x, a.nblocks);
+  stage_body<T, P, BX, BY, LIM, REMOTE, false>(a, bid);
+}
+
+// ---- persistent multi-step kernel (small grids) --------------------------------
+// One workgroup per CU, all co-resident (checked by the cooperative launch).
+// Each workgroup runs every stage of `nsteps` steps for its block; a stage
+// boundary is a neighbour-only hand-off instead of a kernel boundary:
+//   publish: all state stores are sc1 (write-through) -> every wave
+//            s_waitcnt vmcnt(0) -> barrier -> lane 0 stores flag[bid] = epoch (sc1)
+//   consume: lanes 0..nn-1 poll the flags of the blocks whose output this block
+//            reads (sc1 loads, s_sleep, bounded by a wall-clock timeout) -> barrier
+// so no block ever waits on the whole grid.  Any timeout sets *err and every
+// block drains out (no hang).
+template <typename T>
+struct PArgs {
+  Args<T> st[4];        // stage descriptors of one step (buffer-invariant period)
+  int nstages;
+  int nsteps;
+  unsigned* flags;      // [nblocks] epochs, zeroed before the launch
+  const int* nbr;       // [nblocks][maxnbr] producer blocks (-1 padded)
+  int maxnbr;
+  int* err;             // 0 ok; 1 timeout
+  unsigned long long timeout_ticks;   // s_memrealtime ticks (100 MHz)
+};
+
+__device__ __forceinline__ unsigned flag_load(const unsigned* p) {
+  return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename T, int P, int BX, int BY, int LIM>
+__global__ __launch_bounds__((Geom<BX, BY>::NT)) void persistent_kernel(PArgs<T> pa) {
+  pin_args(pa.st[0]);
+  const int bid = xcd_remap(blockIdx.x, pa.st[0].nblocks);
+  const int tid = threadIdx.x;
+  __shared__ int s_abort;
+  if (tid == 0) s_abort = 0;
+  __syncthreads();
+  unsigned epoch = 0;
+#ifdef STSP_STAMPS
+  unsigned long long acc_body = 0, acc_drain = 0, acc_wait = 0, tA = 0, tB = 0, tC = 0;
+#endif
+  for (int step = 0; step < pa.nsteps; ++step) {
+    for (int s = 0; s < pa.nstages; ++s) {
+#ifdef STSP_STAMPS
+      if (tid == 0) tA = __builtin_amdgcn_s_memtime();
+#endif
+      stage_body<T, P, BX, BY, LIM, false, true>(pa.st[s], bid);
+#ifdef STSP_STAMPS
+      if (tid == 0) tB = __builtin_amdgcn_s_memtime();
+#endif
+      // -- publish this block's stage output
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#ifdef STSP_STAMPS
+      if (tid == 0) tC = __builtin_amdgcn_s_memtime();
+#endif
+      ++epoch;
+      if (tid == 0) __hip_atomic_store((gu32*)&pa.flags[bid], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // -- wait for every producer of the next stage's window
+      if (tid < pa.maxnbr) {
+        const int nb = pa.nbr[bid * pa.maxnbr + tid];
+        if (nb >= 0) {
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          while (flag_load(&pa.flags[nb]) < epoch) {
+            if (__hip_atomic_load((gu32*)pa.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+              s_abort = 1;
+              break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > pa.timeout_ticks) {
+              __hip_atomic_store((gu32*)pa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              s_abort = 1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+      }
+      __syncthreads();
+#ifdef STSP_STAMPS
+      if (tid == 0) {
+        const unsigned long long tD = __builtin_amdgcn_s_memtime();
+        acc_body += tB - tA; acc_drain += tC - tB; acc_wait += tD - tC;
+      }
+#endif
+      if (s_abort) return;
+    }
+  }
+#ifdef STSP_STAMPS
+  if (tid == 0 && pa.st[0].stamps) {
+    pa.st[0].stamps[(long)blockIdx.x * 8 + 0] = acc_body;
+    pa.st[0].stamps[(long)blockIdx.x * 8 + 1] = acc_drain;
+    pa.st[0].stamps[(long)blockIdx.x * 8 + 2] = acc_wait;
+  }
+#endif
 }
 
 template <typename T>
@@ -586,7 +723,67 @@ __global__ __launch_bounds__(256) void copy_index_kernel(const T* __restrict__ s
   dst[b * ds + didx[i]] = src[b * ss + sidx[i]];
 }
 
+template <typename T, int P, int BX, int BY, int LIM>
+int launch_persist(const StageDesc* st, int nstages, int nsteps, unsigned* flags, const int* nbr, int maxnbr,
+                   int* err, double timeout_s, hipStream_t s) {
+  PArgs<T> pa;
+  for (int k = 0; k < nstages; ++k) pa.st[k] = make_args<T>(&st[k]);
+  pa.nstages = nstages;
+  pa.nsteps = nsteps;
+  pa.flags = flags;
+  pa.nbr = nbr;
+  pa.maxnbr = maxnbr;
+  pa.err = err;
+  pa.timeout_ticks = (unsigned long long)(timeout_s * 1e8);
+  const int nb = st[0].nblocks;
+  hipError_t e = hipMemsetAsync(flags, 0, sizeof(unsigned) * ((nb + 3) & ~3), s);
+  if (e != hipSuccess) return (int)e;
+  void* args[] = {&pa};
+  e = hipLaunchCooperativeKernel((const void*)persistent_kernel<T, P, BX, BY, LIM>, dim3(nb),
+                                 dim3(Geom<BX, BY>::NT), args, 0, s);
+  return (int)e;
+}
+
+template <typename T, int P>
+int persist_p(int bx, int by, const StageDesc* st, int nstages, int nsteps, unsigned* flags, const int* nbr,
+              int maxnbr, int* err, double timeout_s, hipStream_t s) {
+  if (bx != 16 || by != 16) return -2;
+  if (P == 1) return launch_persist<T, P, 16, 16, 0>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
+  switch (st[0].limiter) {
+    case 0: return launch_persist<T, P, 16, 16, 0>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
+    case 1: return launch_persist<T, P, 16, 16, 1>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
+    case 2: return launch_persist<T, P, 16, 16, 2>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
+    case 3: return launch_persist<T, P, 16, 16, 3>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
+  }
+  return -7;
+}
+
 }  // namespace
+
+extern "C" int stsp_persistent_launch(int phys, int dtype, int bx, int by, const StageDesc* stages, int nstages,
+                                      int nsteps, unsigned* flags, const int* nbr, int maxnbr, int* err,
+                                      double timeout_s, hipStream_t stream) {
+  if (nstages < 1 || nstages > 4 || nsteps < 1) return -8;
+  for (int k = 0; k < nstages; ++k) {
+    const StageDesc* d = &stages[k];
+    if (d->blocks || d->remote || !d->push || d->pw != d->n + 2 * d->mg) return -6;
+    if (d->nblocks != stages[0].nblocks) return -9;
+  }
+  if (dtype == 1) {
+    switch (phys) {
+      case 0: return persist_p<double, 0>(bx, by, stages, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, stream);
+      case 1: return persist_p<double, 1>(bx, by, stages, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, stream);
+      case 2: return persist_p<double, 2>(bx, by, stages, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, stream);
+    }
+  } else if (dtype == 0) {
+    switch (phys) {
+      case 0: return persist_p<float, 0>(bx, by, stages, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, stream);
+      case 1: return persist_p<float, 1>(bx, by, stages, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, stream);
+      case 2: return persist_p<float, 2>(bx, by, stages, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, stream);
+    }
+  }
+  return -3;
+}
 
 extern "C" int stsp_stage_launch(int phys, int dtype, int bx, int by, const StageDesc* d, hipStream_t stream) {
   if (dtype == 1) return launch_d<double>(phys, bx, by, d, stream);

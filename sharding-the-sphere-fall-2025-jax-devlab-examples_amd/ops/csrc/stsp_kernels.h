@@ -36,6 +36,11 @@ typedef struct StageDesc {
 } StageDesc;
 
 int stsp_stage_launch(int phys, int dtype, int bx, int by, const StageDesc* d, hipStream_t stream);
+// Persistent multi-step kernel (single rank, small grids): nsteps x nstages
+// stages in one cooperative launch with neighbour-only flag hand-offs.
+int stsp_persistent_launch(int phys, int dtype, int bx, int by, const StageDesc* stages, int nstages, int nsteps,
+                           unsigned* flags, const int* nbr, int maxnbr, int* err, double timeout_s,
+                           hipStream_t stream);
 int stsp_pack_launch(int dtype, const void* q, int S, int F, const int* idx, int ns, void* send, hipStream_t stream);
 int stsp_copy_index_launch(int dtype, const void* src, const int* sidx, void* dst, const int* didx, int k,
                            int batch, long src_stride, long dst_stride, hipStream_t stream);

@@ -78,3 +78,34 @@ def test_rccl_loopback_full_multigpu_path(nccl_comm, use_graph, phys):
     torch.cuda.synchronize()
     assert torch.equal(ref.tiles_view(), e.tiles_view())
     ns.close()
+
+
+@pytest.mark.parametrize("N,t,phys,dtype", [(24, 2, "swe", torch.float64), (96, 2, "swe", torch.float64),
+                                            (48, 1, "adv", torch.float64), (32, 2, "diff", torch.float64),
+                                            (96, 2, "swe", torch.float32)])
+def test_persistent_kernel_matches_launch_per_stage(N, t, phys, dtype):
+    from stsphere.models.diffusion import Diffusion
+    from stsphere.ops.persistent import PersistentStepper
+    mk = {"swe": lambda: ShallowWater("tc5"), "adv": lambda: Advection(), "diff": lambda: Diffusion()}[phys]
+    g = CubedSphereGrid(N)
+    L = TileLayout(N, t, 1, ng=2)
+    a = Engine(mk(), L, grid=g, device="cuda", backend="hip", dtype=dtype)
+    b = Engine(mk(), L, grid=g, device="cuda", backend="hip", dtype=dtype, dt=a.dt)
+    ps = PersistentStepper(b, timeout_s=2.0, max_steps_per_launch=7)
+    a.step(20)
+    ps.run(20)
+    torch.cuda.synchronize()
+    ps.check()
+    if dtype == torch.float64:
+        assert torch.equal(a.tiles_view(), b.tiles_view())
+    else:   # fp32: the two instantiations may contract FMAs differently
+        x, y = a.tiles_view().reshape(4, -1), b.tiles_view().reshape(4, -1)
+        assert ((x - y).abs().amax(1) / x.abs().amax(1)).max().item() < 1e-5
+
+
+def test_persistent_rejects_unsafe_integrators():
+    from stsphere.models.integrators import get_integrator, persistent_safe
+    assert persistent_safe(get_integrator("ssprk3"))
+    assert not persistent_safe(get_integrator("rk4"))
+    assert not persistent_safe(get_integrator("ssprk2"))
+    assert not persistent_safe(get_integrator("euler"))

@@ -6,7 +6,7 @@ OUT=$ROOT/gpurun_out
 mkdir -p $OUT
 cd $ROOT
 python -m stsphere.ops.build --all > $OUT/build.log 2>&1 || exit 2
-for v in "--runtime native" "--runtime graph" "--runtime native --dtype fp32" "--runtime native --tiles-per-edge 1"; do
+for v in "--runtime persistent" "--runtime native" "--runtime persistent --dtype fp32" "--runtime persistent --tiles-per-edge 1" "--runtime native --N 720 --steps 40 --warmup 4"; do
   timeout -k 10 240 python bench.py --steps 600 --warmup 60 $v > $OUT/bench_tmp.log 2>&1 || { echo "bench failed: $v"; tail -5 $OUT/bench_tmp.log; exit 3; }
   echo "$v :: $(tail -1 $OUT/bench_tmp.log)" >> $OUT/bench_variants.log
 done

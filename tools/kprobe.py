@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=300)
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--blocks", default="16x16,16x8,8x16,32x8,8x8")
+    ap.add_argument("--limit", type=int, default=0, help="launch only this many blocks (latency probe)")
     a = ap.parse_args()
     if a.stamps:
         os.environ["STSP_VARIANT"] = "diag"
@@ -48,6 +49,10 @@ def main():
         hc.nblocks = e.plan.T * hc.nbx * hc.nby
         st = e.integ.stages[1]
         d = hc.desc(st, e.dt, None, hc.nblocks)
+        if a.limit:
+            # first `limit` logical blocks through an explicit work list (no XCD remap)
+            lst = torch.arange(a.limit, dtype=torch.int32, device="cuda")
+            d = hc.desc(st, e.dt, lst, a.limit)
         stamps = None
         if a.stamps:
             stamps = torch.zeros(hc.nblocks * 8, dtype=torch.int64, device="cuda")
