@@ -1,0 +1,84 @@
+"""Command line:  python -m stsphere <command> ...
+
+    run CONFIG.yaml [--days D | --nsteps K] [--plot]   run the solver
+    info CONFIG.yaml                                   validate config, print sharding + halo plan
+    schedule                                           print the reference 4-stage halo schedule
+    roofline                                           slide-19 roofline / TT model for MI355X
+    plot HISTORY.zarr FIELD OUTDIR [--log]             render history frames
+    build                                              compile the gfx950 library
+"""
+import argparse
+import json
+import os
+import sys
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="stsphere")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    r = sub.add_parser("run")
+    r.add_argument("config")
+    r.add_argument("--days", type=float)
+    r.add_argument("--nsteps", type=int)
+    r.add_argument("--plot", action="store_true")
+    i = sub.add_parser("info")
+    i.add_argument("config")
+    sub.add_parser("schedule")
+    sub.add_parser("roofline")
+    p = sub.add_parser("plot")
+    p.add_argument("history")
+    p.add_argument("field")
+    p.add_argument("outdir")
+    p.add_argument("--log", action="store_true")
+    sub.add_parser("build")
+    a = ap.parse_args(argv)
+
+    if a.cmd == "build":
+        from .ops import build
+        for v in sorted(build.VARIANT_FLAGS):
+            print(build.build(force=True, variant=v))
+        return 0
+    if a.cmd == "schedule":
+        from .ops.halo import make_halo_exchange
+        from .parallel.topology import create_communication_schedule
+        make_halo_exchange(create_communication_schedule(), 4)
+        return 0
+    if a.cmd == "roofline":
+        from .utils.roofline import report
+        print(report())
+        return 0
+    if a.cmd == "plot":
+        from .models.geometry import CubedSphereGrid
+        from .utils import zarr_lite
+        from .utils.viz import history_frames
+        N = int(zarr_lite.read_attrs(a.history)["N"])
+        for f in history_frames(a.history, a.field, CubedSphereGrid(N), a.outdir, log=a.log):
+            print(f)
+        return 0
+    from .driver import Solver
+    s = Solver(a.config)
+    if a.cmd == "info":
+        s.setup_sharding()
+        from .parallel.layout import TileLayout
+        c = s.cfg
+        L = TileLayout(c.grid.N, c.parallelization.tiles_per_edge, c.parallelization.num_devices,
+                       ng=c.grid.halo, owner=s.sharding.owner)
+        for rk in range(L.num_ranks):
+            print(L.plan(rk).summary())
+        return 0
+    s.initialize()
+    summary = s.run(nsteps=a.nsteps, days=a.days)
+    if s.rank == 0:
+        print(json.dumps(summary, default=float))
+        if a.plot:
+            from .utils.viz import six_panel, sphere_plot
+            g = s.gather_global()
+            out = s.cfg.io.output_dir
+            os.makedirs(out, exist_ok=True)
+            print(sphere_plot(g[0], s.grid, os.path.join(out, f"{s.fields[0]}_final.png"),
+                              log=s.physics.name == "diffusion"))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

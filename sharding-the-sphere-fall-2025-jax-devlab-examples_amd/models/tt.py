@@ -1,0 +1,247 @@
+"""Tensor-Train (TT) numerics (PDF s.3, s.5, s.19).
+
+The reference's research direction: compress N x N panel fields to
+O(d N r^2) TT form and run the FV numerics on the compressed representation
+(LANL: 124x on Cartesian shallow water, PDF s.3), turning a memory-bound
+stencil into matrix-shaped (compute-bound) work (PDF s.5, s.19).
+
+Implemented here (PyTorch; every heavy op is a GEMM / QR / small SVD, which on
+MI355X runs on the matrix cores through hipBLASLt / rocSOLVER):
+
+* ``tt_svd``        TT decomposition of a d-way tensor (Oseledets 2011), by
+                    relative accuracy or maximal rank
+* ``tt_full``       reconstruction;  ``tt_round`` re-compression (QR + SVD)
+* ``tt_add``, ``tt_scale``, ``tt_dot``, ``tt_norm``
+* ``qtt_reshape`` / ``qtt_unreshape``: quantized TT of a 2^k x 2^k field
+* ``LowRankField``  a 2-D field U = A B^T (the d = 2 TT)
+* ``LowRankDiffusion``: explicit diffusion  U <- U + dt kappa (D U + U D^T)
+                    on a uniform panel, carried out entirely in factored form:
+                    factors grow to rank 3r, then QR + SVD truncation back to
+                    <= r (rank-adaptive with a tolerance)
+* ``compress_cubed_sphere``: per-panel TT ranks / errors of a [6, N, N] field
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+
+# ----------------------------------------------------------------------------
+# general d-way TT
+# ----------------------------------------------------------------------------
+
+def _trunc_rank(s: torch.Tensor, delta: float, max_rank: Optional[int]) -> int:
+    """Smallest rank whose discarded tail has Frobenius norm <= delta."""
+    tail = torch.flip(torch.cumsum(torch.flip(s * s, [0]), 0), [0])   # tail[k] = sum_{i>=k} s_i^2
+    ok = (tail <= delta * delta).nonzero()
+    r = int(ok[0]) if ok.numel() else len(s)
+    r = max(1, r)
+    if max_rank is not None:
+        r = min(r, max_rank)
+    return r
+
+
+def tt_svd(x: torch.Tensor, eps: float = 1e-10, max_rank: Optional[int] = None) -> List[torch.Tensor]:
+    """Cores G_k of shape (r_{k-1}, n_k, r_k) with ||x - tt_full(G)|| <= eps ||x||."""
+    dims = list(x.shape)
+    d = len(dims)
+    delta = eps * float(torch.linalg.norm(x)) / math.sqrt(max(d - 1, 1))
+    cores = []
+    c = x.reshape(dims[0], -1)
+    r = 1
+    for k in range(d - 1):
+        c = c.reshape(r * dims[k], -1)
+        u, s, vh = torch.linalg.svd(c, full_matrices=False)
+        rk = _trunc_rank(s, delta, max_rank)
+        cores.append(u[:, :rk].reshape(r, dims[k], rk))
+        c = s[:rk, None] * vh[:rk]
+        r = rk
+    cores.append(c.reshape(r, dims[-1], 1))
+    return cores
+
+
+def tt_full(cores: Sequence[torch.Tensor]) -> torch.Tensor:
+    out = cores[0]
+    for g in cores[1:]:
+        out = torch.tensordot(out, g, dims=([out.ndim - 1], [0]))
+    return out.squeeze(0).squeeze(-1)
+
+
+def tt_ranks(cores) -> List[int]:
+    return [1] + [g.shape[2] for g in cores]
+
+
+def tt_storage(cores) -> int:
+    return sum(g.numel() for g in cores)
+
+
+def tt_scale(cores, a: float):
+    out = [g.clone() for g in cores]
+    out[0] = out[0] * a
+    return out
+
+
+def tt_add(a, b):
+    """Exact sum (ranks add)."""
+    d = len(a)
+    out = []
+    for k in range(d):
+        ga, gb = a[k], b[k]
+        if k == 0:
+            out.append(torch.cat([ga, gb], dim=2))
+        elif k == d - 1:
+            out.append(torch.cat([ga, gb], dim=0))
+        else:
+            ra0, n, ra1 = ga.shape
+            rb0, _, rb1 = gb.shape
+            z = ga.new_zeros((ra0 + rb0, n, ra1 + rb1))
+            z[:ra0, :, :ra1] = ga
+            z[ra0:, :, ra1:] = gb
+            out.append(z)
+    return out
+
+
+def tt_dot(a, b) -> torch.Tensor:
+    """<a, b> without forming the full tensors."""
+    v = a[0].new_ones((1, 1))
+    for ga, gb in zip(a, b):
+        # v[i,j] -> sum over i,j,n of v[i,j] ga[i,n,k] gb[j,n,l]
+        t = torch.tensordot(v, ga, dims=([0], [0]))           # (j, n, k)
+        v = torch.tensordot(t, gb, dims=([0, 1], [0, 1]))     # (k, l)
+    return v.reshape(())
+
+
+def tt_norm(a) -> float:
+    return float(torch.sqrt(torch.clamp(tt_dot(a, a), min=0)))
+
+
+def tt_round(cores, eps: float = 1e-10, max_rank: Optional[int] = None):
+    """Right-to-left QR orthogonalisation, then left-to-right truncated SVD."""
+    cores = [g.clone() for g in cores]
+    d = len(cores)
+    for k in range(d - 1, 0, -1):
+        r0, n, r1 = cores[k].shape
+        q, rr = torch.linalg.qr(cores[k].reshape(r0, n * r1).T)
+        cores[k] = q.T.reshape(-1, n, r1)
+        cores[k - 1] = torch.tensordot(cores[k - 1], rr.T, dims=([2], [0]))
+    nrm = float(torch.linalg.norm(cores[0]))
+    delta = eps * nrm / math.sqrt(max(d - 1, 1))
+    for k in range(d - 1):
+        r0, n, r1 = cores[k].shape
+        u, s, vh = torch.linalg.svd(cores[k].reshape(r0 * n, r1), full_matrices=False)
+        rk = _trunc_rank(s, delta, max_rank)
+        cores[k] = u[:, :rk].reshape(r0, n, rk)
+        cores[k + 1] = torch.tensordot(s[:rk, None] * vh[:rk], cores[k + 1], dims=([1], [0]))
+    return cores
+
+
+def qtt_reshape(f: torch.Tensor) -> torch.Tensor:
+    """2^k x 2^k field -> 2 x 4 x ... quantized tensor with interleaved
+    (row bit, column bit) pairs, most significant first: a smooth field has low
+    QTT ranks."""
+    n = f.shape[0]
+    k = int(round(math.log2(n)))
+    assert f.shape == (n, n) and 2 ** k == n
+    t = f.reshape([2] * (2 * k))
+    perm = [p for i in range(k) for p in (i, k + i)]
+    return t.permute(perm).reshape([4] * k)
+
+
+def qtt_unreshape(t: torch.Tensor) -> torch.Tensor:
+    k = t.ndim
+    n = 2 ** k
+    x = t.reshape([2] * (2 * k))
+    perm = [2 * i for i in range(k)] + [2 * i + 1 for i in range(k)]
+    return x.permute(perm).reshape(n, n)
+
+
+# ----------------------------------------------------------------------------
+# d = 2: low-rank panel fields and factored diffusion
+# ----------------------------------------------------------------------------
+
+@dataclass
+class LowRankField:
+    A: torch.Tensor   # [N, r]
+    B: torch.Tensor   # [M, r]
+
+    @classmethod
+    def from_dense(cls, U: torch.Tensor, eps: float = 1e-10, max_rank: Optional[int] = None) -> "LowRankField":
+        u, s, vh = torch.linalg.svd(U, full_matrices=False)
+        r = _trunc_rank(s, eps * float(torch.linalg.norm(U)), max_rank)
+        return cls(u[:, :r] * s[:r], vh[:r].T.contiguous())
+
+    @property
+    def rank(self) -> int:
+        return self.A.shape[1]
+
+    def dense(self) -> torch.Tensor:
+        return self.A @ self.B.T
+
+    def storage(self) -> int:
+        return self.A.numel() + self.B.numel()
+
+
+def recompress(A: torch.Tensor, B: torch.Tensor, eps: float, max_rank: Optional[int]) -> LowRankField:
+    """A B^T of rank k -> rank <= max_rank with relative accuracy eps:
+    two thin QRs (N x k) and one k x k SVD."""
+    qa, ra = torch.linalg.qr(A)
+    qb, rb = torch.linalg.qr(B)
+    u, s, vh = torch.linalg.svd(ra @ rb.T)
+    r = _trunc_rank(s, eps * float(torch.linalg.norm(s)), max_rank)
+    return LowRankField(qa @ (u[:, :r] * s[:r]), qb @ vh[:r].T)
+
+
+def second_difference(n: int, h: float, bc: str = "dirichlet", dtype=torch.float64, device="cpu") -> torch.Tensor:
+    D = torch.zeros((n, n), dtype=dtype, device=device)
+    i = torch.arange(n, device=device)
+    D[i, i] = -2.0
+    D[i[:-1], i[:-1] + 1] = 1.0
+    D[i[1:], i[1:] - 1] = 1.0
+    if bc == "periodic":
+        D[0, n - 1] = 1.0
+        D[n - 1, 0] = 1.0
+    return D / (h * h)
+
+
+class LowRankDiffusion:
+    """u_t = kappa (u_xx + u_yy) on a uniform N x N panel, forward Euler, in
+    factored form U = A B^T:  D U + U D^T = (D A) B^T + A (D B)^T, so
+    U + dt kappa lap U = [A, c D A, c A] [B, B, D B]^T  (c = dt kappa), rank 3r,
+    recompressed every step."""
+
+    def __init__(self, N: int, L: float = 1.0, kappa: float = 1.0, bc: str = "dirichlet",
+                 eps: float = 1e-10, max_rank: Optional[int] = None, dtype=torch.float64, device="cpu"):
+        self.h = L / (N + 1) if bc == "dirichlet" else L / N
+        self.D = second_difference(N, self.h, bc, dtype, device)
+        self.kappa = kappa
+        self.eps = eps
+        self.max_rank = max_rank
+        self.dt_max = self.h * self.h / (4.0 * kappa)
+
+    def step(self, U: LowRankField, dt: float) -> LowRankField:
+        c = dt * self.kappa
+        A = torch.cat([U.A, c * (self.D @ U.A), c * U.A], dim=1)
+        B = torch.cat([U.B, U.B, self.D @ U.B], dim=1)
+        return recompress(A, B, self.eps, self.max_rank)
+
+    def dense_step(self, U: torch.Tensor, dt: float) -> torch.Tensor:
+        return U + dt * self.kappa * (self.D @ U + U @ self.D.T)
+
+
+def compress_cubed_sphere(field: np.ndarray, eps: float = 1e-6, qtt: bool = False) -> List[dict]:
+    """Per-panel TT ranks, compression and error of a [6, N, N] field."""
+    out = []
+    for f in range(6):
+        x = torch.as_tensor(field[f], dtype=torch.float64)
+        t = qtt_reshape(x) if qtt else x
+        cores = tt_svd(t, eps)
+        rec = tt_full(cores)
+        rec = qtt_unreshape(rec) if qtt else rec
+        err = float(torch.linalg.norm(rec - x) / max(float(torch.linalg.norm(x)), 1e-300))
+        out.append({"face": f, "ranks": tt_ranks(cores), "storage": tt_storage(cores),
+                    "compression": x.numel() / tt_storage(cores), "rel_error": err})
+    return out

@@ -1,0 +1,97 @@
+"""TT numerics (S10), roofline model (S14), visualisation (S13)."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from stsphere.models import tt
+from stsphere.models.geometry import CubedSphereGrid
+from stsphere.utils import roofline
+
+
+def test_tt_svd_roundtrip_and_accuracy():
+    torch.manual_seed(0)
+    x = torch.randn(4, 5, 6, 3, dtype=torch.float64)
+    cores = tt.tt_svd(x, eps=1e-12)
+    assert torch.allclose(tt.tt_full(cores), x, atol=1e-10)
+    # low-rank tensor compresses exactly
+    a, b, c = (torch.randn(n, dtype=torch.float64) for n in (8, 9, 10))
+    y = torch.einsum("i,j,k->ijk", a, b, c) + 2 * torch.einsum("i,j,k->ijk", b[:8], a[:8].repeat(2)[:9], c)
+    cy = tt.tt_svd(y, eps=1e-12)
+    assert max(tt.tt_ranks(cy)) <= 2
+    assert torch.allclose(tt.tt_full(cy), y, atol=1e-10)
+
+
+def test_tt_arithmetic_and_rounding():
+    torch.manual_seed(1)
+    x = torch.randn(3, 4, 5, dtype=torch.float64)
+    y = torch.randn(3, 4, 5, dtype=torch.float64)
+    cx, cy = tt.tt_svd(x), tt.tt_svd(y)
+    s = tt.tt_add(cx, tt.tt_scale(cy, 2.0))
+    assert torch.allclose(tt.tt_full(s), x + 2 * y, atol=1e-10)
+    assert abs(float(tt.tt_dot(cx, cy)) - float((x * y).sum())) < 1e-9
+    assert abs(tt.tt_norm(cx) - float(x.norm())) < 1e-9
+    r = tt.tt_round(tt.tt_add(cx, cx), eps=1e-12)
+    assert torch.allclose(tt.tt_full(r), 2 * x, atol=1e-9) and tt.tt_ranks(r) == tt.tt_ranks(cx)
+
+
+def test_qtt_smooth_field_low_rank():
+    n = 256
+    xx = torch.linspace(0, 1, n, dtype=torch.float64)
+    f = torch.sin(3 * xx)[:, None] * torch.cos(2 * xx)[None, :] + torch.exp(-((xx[:, None] - .5) ** 2 + (xx[None] - .5) ** 2) * 8)
+    t = tt.qtt_reshape(f)
+    assert torch.equal(tt.qtt_unreshape(t), f)
+    cores = tt.tt_svd(t, eps=1e-6)
+    assert tt.tt_storage(cores) < f.numel() / 4
+    assert float((tt.qtt_unreshape(tt.tt_full(cores)) - f).norm() / f.norm()) < 1e-6
+
+
+def test_low_rank_diffusion_matches_dense():
+    N = 48
+    solver = tt.LowRankDiffusion(N, kappa=1.0, eps=1e-12, max_rank=20)
+    x = torch.linspace(0, 1, N + 2, dtype=torch.float64)[1:-1]
+    U = torch.sin(math.pi * x)[:, None] * torch.sin(2 * math.pi * x)[None, :] + \
+        0.3 * torch.sin(3 * math.pi * x)[:, None] * torch.sin(math.pi * x)[None, :]
+    lr = tt.LowRankField.from_dense(U, eps=1e-14)
+    assert lr.rank == 2
+    dt = 0.5 * solver.dt_max
+    dense = U.clone()
+    for _ in range(50):
+        lr = solver.step(lr, dt)
+        dense = solver.dense_step(dense, dt)
+    assert lr.rank <= 4
+    assert float((lr.dense() - dense).norm() / dense.norm()) < 1e-10
+
+
+def test_compress_cubed_sphere_field():
+    g = CubedSphereGrid(32)
+    from stsphere.models.initial_conditions import williamson_tc2
+    h, _, _ = williamson_tc2(g.centers())
+    rep = tt.compress_cubed_sphere(h, eps=1e-6, qtt=False)   # panel rank 4 at C32
+    assert all(r["rel_error"] < 1e-5 for r in rep)
+    assert np.mean([r["compression"] for r in rep]) > 3 and max(max(r["ranks"]) for r in rep) <= 6
+
+
+def test_roofline_reproduces_slide19():
+    assert abs(roofline.TPU_V4_CLASS.ridge - 305.6) < 0.1
+    assert abs(roofline.fv_plr_cell_rate(roofline.TPU_V4_CLASS) - 2.586e8) < 1e6
+    table = {c["r"]: c for c in roofline.tt_savings_table()}
+    for r, (fl, mem, ai, tot) in {10: (8.3, 5.3, 17.5, 144), 16: (2.0, 2.0, 28, 56), 20: (1.05, 1.3, 35, 35),
+                                  30: (0.31, 0.59, 52, 16)}.items():
+        c = table[r]
+        for got, want in ((c["flop_reduction"], fl), (c["memory_reduction"], mem), (c["tt_ai"], ai),
+                          (c["total_savings"], tot)):
+            assert abs(got / want - 1) < 0.12, (r, got, want)
+
+
+def test_viz_products(tmp_path):
+    from stsphere.utils import viz
+    from stsphere.models.initial_conditions import cosine_bell, lima_flag
+    g = CubedSphereGrid(12)
+    bell = cosine_bell(g.centers())
+    assert os.path.getsize(viz.latlon_band(bell, g, str(tmp_path / "band.png"))) > 1000
+    assert os.path.getsize(viz.sphere_plot(lima_flag(12), g, str(tmp_path / "s.png"), log=True)) > 1000
+    assert os.path.getsize(viz.six_panel(bell, bell, str(tmp_path / "six.png"))) > 1000
+    assert os.path.getsize(viz.mesh_plot(g, str(tmp_path / "mesh.png"))) > 1000
