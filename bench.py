@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--runtime", default="auto", choices=["auto", "persistent", "native", "graph", "eager"])
     ap.add_argument("--steps-per-graph", type=int, default=30)
+    ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "rccl"],
+                    help="multi-GPU halo exchange of the native runtime: direct xGMI stores from the stage "
+                         "kernels (graph-captured; default) or RCCL grouped send/recv (eager)")
     ap.add_argument("--partition", default="auto")
     ap.add_argument("--dt", type=float, default=None)
     return ap.parse_args()
@@ -66,11 +69,17 @@ def main():
     if a.gpus != world:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus > 1 needs a torch.distributed launch (one process per GPU)")
-    device = torch.device(f"cuda:{local}") if torch.cuda.is_available() else torch.device("cpu")
+    # STSP_SHARE_GPU=1: rehearsal mode, every rank on cuda:0 with a gloo group
+    # (functional check of the multi-rank paths on a one-GPU box; not a benchmark)
+    share = os.environ.get("STSP_SHARE_GPU") == "1"
+    device = torch.device(f"cuda:{0 if share else local}") if torch.cuda.is_available() else torch.device("cpu")
     if device.type == "cuda":
         torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl" if device.type == "cuda" else "gloo", device_id=device if device.type == "cuda" else None)
+        if device.type == "cuda" and not share:
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
     dtype = torch.float64 if a.dtype == "fp64" else torch.float32
     layout = TileLayout(a.N, a.tiles_per_edge, world, ng=2, partition=a.partition)
     grid = CubedSphereGrid(a.N)
@@ -79,32 +88,61 @@ def main():
     runtime = a.runtime
     if runtime == "auto":
         runtime = "native" if (device.type == "cuda" and backend == "hip") else "eager"
-    transport = None
-    if world > 1:
-        if runtime == "native":
-            transport = NativeBuffers(layout.plan(rank), phys.F, dtype, device)
-        else:
-            transport = TorchDistTransport(layout.plan(rank), phys.F, dtype, device)
-    eng = Engine(phys, layout, rank, grid=grid, dtype=dtype, device=device, transport=transport,
-                 backend=backend, integrator=a.integrator, dt=a.dt)
+    comm = a.comm if world > 1 else "none"
+    if world > 1 and runtime != "native":
+        comm = "torch.distributed"
+    elif comm == "auto":
+        comm = "xgmi" if world > 1 else "none"
 
-    runner = None
-    if runtime == "persistent":
-        from stsphere.ops.persistent import PersistentStepper
-        runner = PersistentStepper(eng, timeout_s=5.0, max_steps_per_launch=1000)
-        step = runner.run
-    elif runtime == "native":
-        # C++ runtime: hipGraph replay on one GPU; RCCL grouped P2P on a
-        # high-priority stream + interior/boundary overlap on several
-        from stsphere.ops.native_runtime import NativeStepper, create_nccl_comm
-        comm = create_nccl_comm(rank, world, local) if world > 1 else None
-        runner = NativeStepper(eng, nccl_comm=comm, use_graph=True, steps_per_graph=a.steps_per_graph)
-        step = runner.run
-    elif runtime == "graph":
-        runner = GraphStepper(eng, a.steps_per_graph)
-        step = runner.run
-    else:
-        step = eng.step
+    def build(comm):
+        transport = None
+        if world > 1:
+            if runtime == "native":
+                transport = NativeBuffers(layout.plan(rank), phys.F, dtype, device)
+            else:
+                transport = TorchDistTransport(layout.plan(rank), phys.F, dtype, device)
+        eng = Engine(phys, layout, rank, grid=grid, dtype=dtype, device=device, transport=transport,
+                     backend=backend, integrator=a.integrator, dt=a.dt)
+        runner = None
+        if runtime == "persistent":
+            from stsphere.ops.persistent import PersistentStepper
+            runner = PersistentStepper(eng, timeout_s=5.0, max_steps_per_launch=1000)
+        elif runtime == "native":
+            # C++ runtime, hipGraph replay; between GPUs either direct xGMI
+            # stores from the stage kernels (graph-captured) or RCCL grouped
+            # P2P on a high-priority stream + interior/boundary overlap (eager)
+            from stsphere.ops.native_runtime import NativeStepper, create_nccl_comm
+            xg = None
+            nc = None
+            if comm == "xgmi":
+                from stsphere.ops.xgmi import XgmiHalo
+                xg = XgmiHalo(eng, timeout_s=2.0)
+            elif comm == "rccl":
+                nc = create_nccl_comm(rank, world, local)
+            runner = NativeStepper(eng, nccl_comm=nc, use_graph=True, steps_per_graph=a.steps_per_graph, xgmi=xg)
+        elif runtime == "graph":
+            runner = GraphStepper(eng, a.steps_per_graph)
+        return eng, runner
+
+    def agree(ok: bool) -> bool:
+        if world == 1:
+            return ok
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    try:
+        eng, runner = build(comm)
+        ok = True
+    except Exception as exc:   # e.g. no IPC between these GPUs
+        print(f"[bench] rank {rank}: {comm} setup failed: {exc}", file=sys.stderr, flush=True)
+        ok = False
+    if comm == "xgmi" and not agree(ok):
+        comm = "rccl"
+        eng, runner = build(comm)
+    elif not ok:
+        raise SystemExit(1)
+    step = runner.run if runner is not None else eng.step
 
     def sync():
         if device.type == "cuda":
@@ -116,6 +154,19 @@ def main():
 
     step(a.warmup)
     sync()
+    if comm == "xgmi":
+        ok = True
+        try:
+            runner.check()
+        except RuntimeError as exc:
+            print(f"[bench] rank {rank}: {exc}", file=sys.stderr, flush=True)
+            ok = False
+        if not agree(ok):   # fall back to RCCL from a fresh state
+            comm = "rccl"
+            eng, runner = build(comm)
+            step = runner.run
+            step(a.warmup)
+            sync()
     t0 = time.perf_counter()
     step(a.steps)
     sync()
@@ -124,7 +175,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    if runtime == "persistent":
+    if runtime in ("persistent", "native"):
         runner.check()
     diag = eng.diagnostics()
     if world > 1:
@@ -160,6 +211,7 @@ def main():
                 "dt_s": eng.dt,
                 "backend": backend,
                 "runtime": runtime,
+                "comm": comm,
             },
             "simulated_days_per_day": sdpd,
             "finite": finite,

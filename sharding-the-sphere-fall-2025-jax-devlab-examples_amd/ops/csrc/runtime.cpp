@@ -294,5 +294,63 @@ extern "C" int stsp_nccl_selftest(void* comm, void* stream) {
   return out == v ? 0 : -4;
 }
 
+// ---- direct xGMI halo memory (ops/xgmi.py) -------------------------------------
+// One uncached device allocation per rank holds its arrival counters and its
+// receive ring; peers map it through a dmabuf IPC handle and store into it
+// over xGMI.  Uncached (MTYPE UC) so neither the owner's nor a peer's L2 keeps
+// a line of it; every kernel access is additionally system scope.
+
+extern "C" int stsp_xg_alloc(size_t bytes, void** out) {
+  *out = nullptr;
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) return -1;
+  if (hipMemset(p, 0, bytes) != hipSuccess) {
+    hipFree(p);
+    return -2;
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return -3;
+  *out = p;
+  return 0;
+}
+
+extern "C" int stsp_xg_free(void* p) { return p && hipFree(p) != hipSuccess ? -1 : 0; }
+
+extern "C" int stsp_ipc_handle_bytes(void) { return HIP_IPC_HANDLE_SIZE; }
+
+extern "C" int stsp_ipc_get(void* p, void* handle_out) {
+  hipIpcMemHandle_t h;
+  const hipError_t e = hipIpcGetMemHandle(&h, p);
+  if (e != hipSuccess) return (int)e;
+  std::memcpy(handle_out, &h, sizeof(h));
+  return 0;
+}
+
+extern "C" int stsp_ipc_open(const void* handle, void** out) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  *out = nullptr;
+  const hipError_t e = hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+extern "C" int stsp_ipc_close(void* p) { return hipIpcCloseMemHandle(p) == hipSuccess ? 0 : -1; }
+
+// Best effort: map every other visible GPU for peer access (already-enabled and
+// not-possible are not errors here; IPC mappings carry their own access).
+extern "C" int stsp_enable_peers(int device) {
+  int n = 0, ok = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return -1;
+  for (int p = 0; p < n; ++p) {
+    if (p == device) continue;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, device, p) == hipSuccess && can) {
+      const hipError_t e = hipDeviceEnablePeerAccess(p, 0);
+      if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) ++ok;
+      else (void)hipGetLastError();
+    }
+  }
+  return ok;
+}
+
 extern "C" int stsp_roctx_push(const char* msg) { return roctxRangePush(msg); }
 extern "C" int stsp_roctx_pop(void) { return roctxRangePop(); }

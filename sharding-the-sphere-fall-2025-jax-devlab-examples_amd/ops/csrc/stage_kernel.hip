@@ -112,6 +112,16 @@ struct Args {
   int ntile, n, S, mg, pw, nblocks, limiter;
   T a0, a1, a2, c0, c1, c2, dt, g, omega2;
   unsigned long long* stamps;
+  // direct xGMI halo (XG kernels only, see stsp_kernels.h)
+  int ring;
+  T* const* peer_ring;
+  unsigned long long* const* peer_cnt;
+  const unsigned long long* cnt;
+  const unsigned long long* nprod;
+  const int* bmask;
+  int* epoch;
+  int* err;
+  long long timeout_ticks;
 };
 
 #ifdef STSP_STAMPS
@@ -167,6 +177,24 @@ __device__ __forceinline__ T ld_state(const T* p) {
   }
 }
 
+// System-scope (cross-GPU) accesses of the direct xGMI halo: sc0 sc1, i.e.
+// no GPU cache keeps a copy, so a peer's store is seen by the next poll/load.
+template <typename T>
+__device__ __forceinline__ T ld_sys(const T* p) {
+  if constexpr (sizeof(T) == 8)
+    return __builtin_bit_cast(T, __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  else
+    return __builtin_bit_cast(T, __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+
+template <typename T>
+__device__ __forceinline__ void st_sys(T* p, T v) {
+  if constexpr (sizeof(T) == 8)
+    __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else
+    __hip_atomic_store((gu32*)p, __builtin_bit_cast(unsigned int, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <bool SYNC, typename T>
 __device__ __forceinline__ void st_state(T* p, T v) {
   if constexpr (!SYNC) {
@@ -181,7 +209,17 @@ __device__ __forceinline__ void st_state(T* p, T v) {
 // One RK stage of one BX x BY block (all phases).  SYNC = persistent-kernel
 // mode: every access to state written by other workgroups in this launch is an
 // agent-scope sc1 access (L1 bypass, write-through), see persistent_kernel.
-template <typename T, int P, int BX, int BY, int LIM, bool REMOTE, bool SYNC>
+// XG = direct xGMI halo: a block that reads remote ghosts first waits for the
+// arrival counters of those peers, reads the ghosts from this rank's receive
+// ring (slot epoch % 3), and every block stores the cells its peers need into
+// their rings (slot (epoch + 1) % 3) before bumping their counters.
+//
+// Why three ring slots and no reset: a rank can run at most one stage ahead of
+// a peer it exchanges with (it waits for that peer's previous stage), so a
+// write into slot (e + 1) % 3 never lands on the slot (e % 3) the peer may still
+// be reading, nor on the one before it; counters only grow (stage e of a peer
+// is complete once its counter reaches (e + 1) * nprod).
+template <typename T, int P, int BX, int BY, int LIM, bool REMOTE, bool SYNC, bool XG = false>
 __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   constexpr int F = Phys<P>::F;
   constexpr int NG = Phys<P>::NG;
@@ -281,6 +319,33 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   }
   STAMP(1);
 
+  // ---- 0b. direct xGMI: wait for the peers whose ghosts this block reads ------
+  int xe = 0, feed = 0;
+  bool rblk = REMOTE;
+  const T* rring = a.recv;
+  if constexpr (XG) {
+    xe = a.epoch[bid];
+    const int need = a.bmask[2 * bid];
+    feed = a.bmask[2 * bid + 1];
+    rblk = need != 0;
+    rring = a.recv + (long)(xe % 3) * a.ring;
+    if (rblk) {
+      if (tid < 32 && ((need >> tid) & 1)) {
+        const unsigned long long want = (unsigned long long)xe * a.nprod[tid];
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load((gu64*)(a.cnt + tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+          if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+          if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
+            __hip_atomic_store((gu32*)a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+    }
+  }
+
   // ---- 1. window (block + NG halo) -> LDS --------------------------------------
   // Same-rank blocks load cell PAIRS with 16-byte (fp64) loads when the padded
   // rows are pair-aligned; remote-boundary blocks load cell by cell (a ghost
@@ -299,7 +364,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       s_w[0][ly][lx] = v[0];
     }
   };
-  const bool pairs = !REMOTE && !SYNC && ((EX & 1) == 0) && (((mg - NG) & 1) == 0) && ((pw & 1) == 0);
+  const bool pairs = !rblk && !SYNC && ((EX & 1) == 0) && (((mg - NG) & 1) == 0) && ((pw & 1) == 0);
   if (pairs) {
     constexpr int HX = EX / 2;
     if (tid < HX * EY) {
@@ -334,9 +399,9 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     if (x < n + NG && y < n + NG) {          // false only past a partial block
       const long pa = tb + (long)(y + mg) * pw + (x + mg);
       bool from_recv = false;
-      if constexpr (REMOTE) {
+      if constexpr (REMOTE || XG) {
         const bool oxx = (x < 0) | (x >= n), oyy = (y < 0) | (y >= n);
-        if (oxx != oyy) {
+        if (rblk && oxx != oyy) {
           int side, layer, pos;
           if (x < 0) { side = 0; layer = -1 - x; pos = y; }
           else if (x >= n) { side = 1; layer = x - n; pos = y; }
@@ -345,9 +410,14 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
           const int m = a.gmap[((tile * 4 + side) * mg + layer) * n + pos];
           if (m < 0) {
             from_recv = true;
-            const T* rp = a.recv + (long)(-1 - m) * F;
+            const T* rp = rring + (long)(-1 - m) * F;
+            if constexpr (XG) {
 #pragma unroll
-            for (int f = 0; f < F; ++f) v[f] = ld_state<SYNC>(rp + f);
+              for (int f = 0; f < F; ++f) v[f] = ld_sys(rp + f);
+            } else {
+#pragma unroll
+              for (int f = 0; f < F; ++f) v[f] = ld_state<SYNC>(rp + f);
+            }
           }
         }
       }
@@ -444,73 +514,95 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   __syncthreads();
 
   // ---- 3. divergence + sources + RK combination + push -------------------------
-  if (!own) return;
-  T qs[F];
-  if constexpr (P == 2) {
+  if (own) {
+    T qs[F];
+    if constexpr (P == 2) {
 #pragma unroll
-    for (int f = 0; f < 4; ++f) qs[f] = s_c[f][NG + oy][NG + ox];
-  } else {
-    qs[0] = s_w[0][NG + oy][NG + ox];
-  }
-  T dq[F];
-#pragma unroll
-  for (int f = 0; f < F; ++f)
-    dq[f] = -((s_fx[f][oy][ox + 1] - s_fx[f][oy][ox]) + (s_fy[f][oy + 1][ox] - s_fy[f][oy][ox])) * iA;
-  if constexpr (P == 2) {
-    const T fc = a.omega2 * r2;
-    const T h = qs[0];
-    const T cor[3] = {r1 * qs[3] - r2 * qs[2], r2 * qs[1] - r0 * qs[3], r0 * qs[2] - r1 * qs[1]};
-    // curvature balance g/2 h^2 sum(+-L m)/A: a constant depth is force-free
-    const T Lw = s_lx[oy][ox], Le = s_lx[oy][ox + 1], Ls = s_ly[oy][ox], Ln = s_ly[oy + 1][ox];
-    const T pb = T(0.5) * a.g * h * h * iA, gh = a.g * h;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const T Sk = Le * s_nx[k][ox + 1] - Lw * s_nx[k][ox] + Ln * s_ny[k][oy + 1] - Ls * s_ny[k][oy];
-      dq[1 + k] += -fc * cor[k] + pb * Sk - gh * gb[k];
+      for (int f = 0; f < 4; ++f) qs[f] = s_c[f][NG + oy][NG + ox];
+    } else {
+      qs[0] = s_w[0][NG + oy][NG + ox];
     }
-  }
-  T o[F];
+    T dq[F];
 #pragma unroll
-  for (int f = 0; f < F; ++f) o[f] = a.a2 * a.dt * dq[f];
-  if (a.a1 != T(0)) {
+    for (int f = 0; f < F; ++f)
+      dq[f] = -((s_fx[f][oy][ox + 1] - s_fx[f][oy][ox]) + (s_fy[f][oy + 1][ox] - s_fy[f][oy][ox])) * iA;
+    if constexpr (P == 2) {
+      const T fc = a.omega2 * r2;
+      const T h = qs[0];
+      const T cor[3] = {r1 * qs[3] - r2 * qs[2], r2 * qs[1] - r0 * qs[3], r0 * qs[2] - r1 * qs[1]};
+      // curvature balance g/2 h^2 sum(+-L m)/A: a constant depth is force-free
+      const T Lw = s_lx[oy][ox], Le = s_lx[oy][ox + 1], Ls = s_ly[oy][ox], Ln = s_ly[oy + 1][ox];
+      const T pb = T(0.5) * a.g * h * h * iA, gh = a.g * h;
 #pragma unroll
-    for (int f = 0; f < F; ++f) o[f] += a.a1 * qs[f];
-  }
-  if (a.a0 != T(0)) {
-#pragma unroll
-    for (int f = 0; f < F; ++f) o[f] += a.a0 * xs[f];
-  }
-  if constexpr (P == 2) {
-    const T d = o[1] * r0 + o[2] * r1 + o[3] * r2;
-    o[1] -= d * r0; o[2] -= d * r1; o[3] -= d * r2;
-  }
-  if (a.acc_out) {
-    T p[F];
-#pragma unroll
-    for (int f = 0; f < F; ++f) p[f] = a.c2 * a.dt * dq[f];
-    if (a.c1 != T(0)) {
-#pragma unroll
-      for (int f = 0; f < F; ++f) p[f] += a.c1 * xs[f];
+      for (int k = 0; k < 3; ++k) {
+        const T Sk = Le * s_nx[k][ox + 1] - Lw * s_nx[k][ox] + Ln * s_ny[k][oy + 1] - Ls * s_ny[k][oy];
+        dq[1 + k] += -fc * cor[k] + pb * Sk - gh * gb[k];
+      }
     }
-    if (need_acc) {
+    T o[F];
 #pragma unroll
-      for (int f = 0; f < F; ++f) p[f] += a.c0 * acs[f];
+    for (int f = 0; f < F; ++f) o[f] = a.a2 * a.dt * dq[f];
+    if (a.a1 != T(0)) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) o[f] += a.a1 * qs[f];
+    }
+    if (a.a0 != T(0)) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) o[f] += a.a0 * xs[f];
     }
     if constexpr (P == 2) {
-      const T d = p[1] * r0 + p[2] * r1 + p[3] * r2;
-      p[1] -= d * r0; p[2] -= d * r1; p[3] -= d * r2;
+      const T d = o[1] * r0 + o[2] * r1 + o[3] * r2;
+      o[1] -= d * r0; o[2] -= d * r1; o[3] -= d * r2;
+    }
+    if (a.acc_out) {
+      T p[F];
+#pragma unroll
+      for (int f = 0; f < F; ++f) p[f] = a.c2 * a.dt * dq[f];
+      if (a.c1 != T(0)) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) p[f] += a.c1 * xs[f];
+      }
+      if (need_acc) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) p[f] += a.c0 * acs[f];
+      }
+      if constexpr (P == 2) {
+        const T d = p[1] * r0 + p[2] * r1 + p[3] * r2;
+        p[1] -= d * r0; p[2] -= d * r1; p[3] -= d * r2;
+      }
+#pragma unroll
+      for (int f = 0; f < F; ++f) st_state<SYNC>(a.acc_out + (long)f * S + pc, p[f]);
     }
 #pragma unroll
-    for (int f = 0; f < F; ++f) st_state<SYNC>(a.acc_out + (long)f * S + pc, p[f]);
+    for (int f = 0; f < F; ++f) st_state<SYNC>(a.out + (long)f * S + pc, o[f]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (pt[k] >= 0) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) st_state<SYNC>(a.out + (long)f * S + pt[k], o[f]);
+      }
+    }
+    if constexpr (XG) {   // remote ghosts: straight into the consumer's ring
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (pt[k] < -1) {
+          const int code = -2 - pt[k];
+          T* dst = a.peer_ring[code >> 24] + (long)((xe + 1) % 3) * a.ring + (long)(code & 0xFFFFFF) * F;
+#pragma unroll
+          for (int f = 0; f < F; ++f) st_sys(dst + f, o[f]);
+        }
+      }
+    }
   }
-#pragma unroll
-  for (int f = 0; f < F; ++f) st_state<SYNC>(a.out + (long)f * S + pc, o[f]);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (pt[k] >= 0) {
-#pragma unroll
-      for (int f = 0; f < F; ++f) st_state<SYNC>(a.out + (long)f * S + pt[k], o[f]);
+  if constexpr (XG) {
+    if (feed) {   // publish: every storing wave drains, then one lane per peer counts
+      __threadfence_system();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid < 32 && ((feed >> tid) & 1))
+        __hip_atomic_fetch_add((gu64*)a.peer_cnt[tid], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    if (tid == 0) a.epoch[bid] = xe + 1;
   }
   STAMP(6);
 }
@@ -537,11 +629,11 @@ __device__ __forceinline__ void pin_args(const Args<T>& a) {
                "s"(a.omega2));
 }
 
-template <typename T, int P, int BX, int BY, int LIM, bool REMOTE, bool LIST>
+template <typename T, int P, int BX, int BY, int LIM, bool REMOTE, bool LIST, bool XG>
 __global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
   pin_args(a);
   const int bid = LIST ? a.blocks[blockIdx.x] : xcd_remap(blockIdx.x, a.nblocks);
-  stage_body<T, P, BX, BY, LIM, REMOTE, false>(a, bid);
+  stage_body<T, P, BX, BY, LIM, REMOTE, false, XG>(a, bid);
 }
 
 // ---- persistent multi-step kernel (small grids) --------------------------------
@@ -650,6 +742,15 @@ Args<T> make_args(const StageDesc* d) {
   a.a0 = (T)d->a0; a.a1 = (T)d->a1; a.a2 = (T)d->a2; a.c0 = (T)d->c0; a.c1 = (T)d->c1; a.c2 = (T)d->c2;
   a.dt = (T)d->dt; a.g = (T)d->g; a.omega2 = (T)d->omega2;
   a.stamps = (unsigned long long*)d->stamps;
+  a.ring = d->ring;
+  a.peer_ring = (T* const*)d->peer_ring;
+  a.peer_cnt = d->peer_cnt;
+  a.cnt = d->cnt;
+  a.nprod = d->nprod;
+  a.bmask = d->bmask;
+  a.epoch = d->epoch;
+  a.err = d->err;
+  a.timeout_ticks = d->timeout_ticks;
   return a;
 }
 
@@ -658,12 +759,14 @@ int launch_l(const StageDesc* d, hipStream_t s) {
   Args<T> a = make_args<T>(d);
   constexpr int NT = Geom<BX, BY>::NT;
   const dim3 grid(d->nblocks), block(NT);
-  if (d->remote)
-    hipLaunchKernelGGL((stage_kernel<T, P, BX, BY, LIM, true, true>), grid, block, 0, s, a);
+  if (d->xg)
+    hipLaunchKernelGGL((stage_kernel<T, P, BX, BY, LIM, false, false, true>), grid, block, 0, s, a);
+  else if (d->remote)
+    hipLaunchKernelGGL((stage_kernel<T, P, BX, BY, LIM, true, true, false>), grid, block, 0, s, a);
   else if (d->blocks)
-    hipLaunchKernelGGL((stage_kernel<T, P, BX, BY, LIM, false, true>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((stage_kernel<T, P, BX, BY, LIM, false, true, false>), grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL((stage_kernel<T, P, BX, BY, LIM, false, false>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((stage_kernel<T, P, BX, BY, LIM, false, false, false>), grid, block, 0, s, a);
   return (int)hipGetLastError();
 }
 
@@ -672,6 +775,9 @@ int launch_t(const StageDesc* d, hipStream_t s) {
   if (d->nblocks <= 0) return 0;
   if (d->pw != d->n + 2 * d->mg || d->mg < Phys<P>::NG) return -5;
   if (!d->push || (d->remote && (!d->gmap || !d->blocks))) return -6;
+  if (d->xg && (d->remote || d->blocks || !d->gmap || !d->recv || !d->peer_ring || !d->peer_cnt || !d->cnt ||
+                !d->nprod || !d->bmask || !d->epoch || !d->err || d->ring <= 0))
+    return -10;
   if constexpr (P == 1) return launch_l<T, P, BX, BY, 0>(d, s);  // diffusion: no reconstruction
   switch (d->limiter) {
     case 0: return launch_l<T, P, BX, BY, 0>(d, s);
@@ -710,6 +816,20 @@ __global__ __launch_bounds__(256) void pack_kernel(const T* __restrict__ q, int 
   if (k >= ns) return;
   const int src = idx[k];
   for (int f = 0; f < F; ++f) send[(long)k * F + f] = q[(long)f * S + src];
+}
+
+// ---- direct xGMI halo: initial ghost delivery (no counter bump) -------------
+template <typename T>
+__global__ __launch_bounds__(256) void xg_prime_kernel(const T* __restrict__ q, int S, int F,
+                                                       const int* __restrict__ src, const int* __restrict__ code,
+                                                       int nent, T* const* peer_ring, int ring, int slot_ring) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nent) {
+    const int c = code[i];
+    T* dst = peer_ring[c >> 24] + (long)slot_ring * ring + (long)(c & 0xFFFFFF) * F;
+    for (int f = 0; f < F; ++f) st_sys(dst + f, q[(long)f * S + src[i]]);
+  }
+  __threadfence_system();
 }
 
 // ---- generic indexed copy: dst[b][didx[k]] = src[b][sidx[k]] ------------------
@@ -814,5 +934,19 @@ extern "C" int stsp_copy_index_launch(int dtype, const void* src, const int* sid
   else
     hipLaunchKernelGGL(copy_index_kernel<float>, grid, dim3(256), 0, stream, (const float*)src, sidx, (float*)dst,
                        didx, k, src_stride, dst_stride);
+  return (int)hipGetLastError();
+}
+
+extern "C" int stsp_xg_prime_launch(int dtype, const void* q, int S, int F, const int* src, const int* code, int nent,
+                                    void* const* peer_ring, int ring, int slot_ring, hipStream_t stream) {
+  if (nent <= 0) return 0;
+  if (slot_ring < 0 || slot_ring > 2 || ring <= 0) return -6;
+  const int nb = (nent + 255) / 256;
+  if (dtype == 1)
+    hipLaunchKernelGGL(xg_prime_kernel<double>, dim3(nb), dim3(256), 0, stream, (const double*)q, S, F, src, code,
+                       nent, (double* const*)peer_ring, ring, slot_ring);
+  else
+    hipLaunchKernelGGL(xg_prime_kernel<float>, dim3(nb), dim3(256), 0, stream, (const float*)q, S, F, src, code,
+                       nent, (float* const*)peer_ring, ring, slot_ring);
   return (int)hipGetLastError();
 }

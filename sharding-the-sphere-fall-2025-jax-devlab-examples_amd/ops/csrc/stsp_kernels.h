@@ -33,6 +33,22 @@ typedef struct StageDesc {
   double a0, a1, a2, c0, c1, c2, dt;
   double g, omega2;
   void* stamps;         // diagnostic builds only (-DSTSP_STAMPS): [nblocks][8] s_memtime per phase
+  // ---- direct xGMI halo (xg = 1; see ops/xgmi.py) ----------------------------
+  // The producing block stores remote ghost cells straight into the consumer
+  // rank's receive ring (IPC-mapped, uncached) and bumps that rank's arrival
+  // counter; a consumer block polls only the counters of the peers it reads.
+  // `recv` is then this rank's ring base; `push` entries < -1 encode
+  // -2 - (peer << 24 | slot).
+  int xg;
+  int ring;             // elements per ring slot (= max receive slots over ranks * F)
+  void* const* peer_ring;                  // [world] ring base of rank p (device array)
+  unsigned long long* const* peer_cnt;     // [world] &counter[my rank] on rank p
+  const unsigned long long* cnt;           // [world] arrival counters on this rank
+  const unsigned long long* nprod;         // [world] producer blocks of rank p feeding this rank
+  const int* bmask;     // [nblocks][2] (peers read, peers fed) bit masks
+  int* epoch;           // [nblocks] stages completed
+  int* err;             // set to 1 on a poll timeout (all later polls fall through)
+  long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
 } StageDesc;
 
 int stsp_stage_launch(int phys, int dtype, int bx, int by, const StageDesc* d, hipStream_t stream);
@@ -44,4 +60,8 @@ int stsp_persistent_launch(int phys, int dtype, int bx, int by, const StageDesc*
 int stsp_pack_launch(int dtype, const void* q, int S, int F, const int* idx, int ns, void* send, hipStream_t stream);
 int stsp_copy_index_launch(int dtype, const void* src, const int* sidx, void* dst, const int* didx, int k,
                            int batch, long src_stride, long dst_stride, hipStream_t stream);
+// Direct xGMI halo: write the remote ghost cells of state q (entries src[i] ->
+// code[i] = peer << 24 | slot) into ring slot `slot_ring` of every peer.
+int stsp_xg_prime_launch(int dtype, const void* q, int S, int F, const int* src, const int* code, int nent,
+                         void* const* peer_ring, int ring, int slot_ring, hipStream_t stream);
 }

@@ -34,6 +34,11 @@ class StageDesc(ctypes.Structure):
         ("c0", ctypes.c_double), ("c1", ctypes.c_double), ("c2", ctypes.c_double), ("dt", ctypes.c_double),
         ("g", ctypes.c_double), ("omega2", ctypes.c_double),
         ("stamps", ctypes.c_void_p),
+        # direct xGMI halo (ops/xgmi.py)
+        ("xg", ctypes.c_int), ("ring", ctypes.c_int),
+        ("peer_ring", ctypes.c_void_p), ("peer_cnt", ctypes.c_void_p), ("cnt", ctypes.c_void_p),
+        ("nprod", ctypes.c_void_p), ("bmask", ctypes.c_void_p), ("epoch", ctypes.c_void_p), ("err", ctypes.c_void_p),
+        ("timeout_ticks", ctypes.c_longlong),
     ]
 
 

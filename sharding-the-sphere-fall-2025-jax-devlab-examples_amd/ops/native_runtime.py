@@ -107,10 +107,15 @@ def nccl_selftest(comm: int) -> None:
 
 
 class NativeStepper:
-    """Steps an ``Engine(backend='hip')`` entirely from C++."""
+    """Steps an ``Engine(backend='hip')`` entirely from C++.
+
+    Halo traffic between ranks: RCCL (``nccl_comm``; eager, pack + grouped
+    send/recv + interior/boundary split) or the direct xGMI exchange
+    (``xgmi=XgmiHalo``; one kernel per stage, graph-captured)."""
 
     def __init__(self, engine, nccl_comm: Optional[int] = None, use_graph: bool = True,
-                 steps_per_graph: int = 30, roctx: bool = False, stream: Optional[torch.cuda.Stream] = None):
+                 steps_per_graph: int = 30, roctx: bool = False, stream: Optional[torch.cuda.Stream] = None,
+                 xgmi=None):
         from .hip_compute import HipCompute
         e = engine
         if not isinstance(e.compute, HipCompute):
@@ -120,6 +125,9 @@ class NativeStepper:
         hc = e.compute
         plan = e.plan
         self.remote = plan.num_recv > 0 or plan.num_send > 0
+        self.xgmi = xgmi
+        if xgmi is not None:
+            self.remote = False      # the exchange lives inside the stage kernels
         if self.remote and not nccl_comm:
             raise RuntimeError("rank has remote neighbours: pass an RCCL communicator (create_nccl_comm)")
         if len(plan.send_peers) > MAX_PEERS or len(plan.recv_peers) > MAX_PEERS:
@@ -137,6 +145,9 @@ class NativeStepper:
         for _ in range(period):
             e.pool = pool
             for st in e.integ.stages:
+                if xgmi is not None:
+                    ops.append(self._stage_op(xgmi.fill(hc.desc(st, e.dt, None, hc.nblocks))))
+                    continue
                 if not hc.remote:
                     ops.append(self._stage_op(hc.desc(st, e.dt, None, hc.nblocks)))
                     continue
@@ -209,6 +220,10 @@ class NativeStepper:
         if rc != 0:
             msg = self.L.stsp_rt_last_error(self.h)
             raise RuntimeError(f"native runtime {what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def check(self) -> None:
+        if self.xgmi is not None:
+            self.xgmi.check()
 
     def run(self, nsteps: int) -> None:
         e = self.e

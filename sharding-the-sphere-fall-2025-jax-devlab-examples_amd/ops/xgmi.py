@@ -1,0 +1,340 @@
+"""Direct xGMI halo exchange: stage kernels store remote ghost cells straight
+into the neighbour GPU's memory, with no RCCL and no host in the loop.
+
+Why (BASELINE configs "C96 on 6 MI355X", "C180 on 8"):
+at C96 a stage takes about 6.5 us on one GPU.  An RCCL grouped send/recv per
+stage costs as much as a whole stage.  It is host-driven, and RCCL 2.26 in
+this image cannot be captured into a hipGraph (ops/native_runtime.py).
+MI355X GPUs in a node are fully connected by xGMI, and a GPU can store
+directly into a peer's HBM through a dmabuf IPC mapping.  The exchange
+therefore becomes part of the stage kernel itself (ops/csrc/stage_kernel.hip,
+XG variant):
+
+* Every rank owns one uncached allocation holding ``[world]`` u64 arrival
+  counters and a 3-slot receive ring (``ring = max receive slots x F``
+  elements per slot).  Peers map it with ``hipIpcOpenMemHandle``.
+* A block whose cells are ghosts of another rank stores them into that rank's
+  ring slot ``(epoch + 1) % 3``.  Its waves drain their stores, then one lane
+  per peer adds 1 to that peer's counter (system-scope release).  The push map
+  carries the destination: ``-2 - (peer << 24 | slot)``.
+* A block that reads remote ghosts polls the counters of those peers until
+  ``counter[p] >= epoch * nprod[p]``.  ``nprod[p]`` is the number of producer
+  blocks on p that feed this rank.  The poll is bounded by a timeout that sets
+  ``err``; after that every poll falls through.  The block then reads ring
+  slot ``epoch % 3``.
+* ``epoch`` is a per-block count of completed stages.  Counters never reset.
+
+Three slots are enough because a rank waits for its peers' previous stage, so
+it can run at most one stage ahead of any peer it exchanges with (the proof is
+in the kernel comment).  The whole step is plain kernels, so multi-GPU steps
+are captured in a hipGraph like single-GPU ones.
+
+``XgmiPlan`` is the host-side index math (numpy only, tested on CPU).
+``XgmiHalo`` owns the memory, the IPC mappings and the initial delivery.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..parallel.layout import TileLayout
+
+CNT_BYTES = 256          # counter block at the start of each rank's allocation (<= 32 ranks)
+MAX_WORLD = 32
+SLOT_BITS = 24
+
+
+def _side_cell(s2: np.ndarray, kk: np.ndarray, pp: np.ndarray, n: int):
+    """(side, layer, pos) of a push entry -> own-cell (i, j); inverse of the
+    kernel's push lookup (stage_kernel.hip, phase 0)."""
+    i = np.select([s2 == 0, s2 == 1, s2 == 2], [kk, n - 1 - kk, pp], pp)
+    j = np.select([s2 == 0, s2 == 1, s2 == 2], [pp, pp, kk], n - 1 - kk)
+    return i, j
+
+
+class XgmiPlan:
+    """Index tables of the direct exchange for one rank (host side)."""
+
+    def __init__(self, layout: TileLayout, rank: int, bx: int, by: int, halo: int):
+        L = layout
+        self.layout, self.rank, self.bx, self.by, self.halo = L, rank, bx, by, halo
+        world = L.num_ranks
+        if world > MAX_WORLD:
+            raise ValueError(f"direct xGMI halo supports at most {MAX_WORLD} ranks")
+        plan = L.plan(rank)
+        self.plan = plan
+        n, g = plan.n, plan.ng
+        self.nbx, self.nby = -(-n // bx), -(-n // by)
+        self.nblocks = plan.T * self.nbx * self.nby
+        tnbr = L.tile_neighbors()
+        plans = [L.plan(p) for p in range(world)]
+        self.ring_slots = max(1, max(p.num_recv for p in plans))
+        if self.ring_slots >= (1 << SLOT_BITS):
+            raise ValueError("receive ring too large for the push-map encoding")
+
+        # ---- producer side: my cells that are remote ghosts of rank p ----------
+        push = plan.push_map.astype(np.int64).copy()
+        src_l, code_l, feed_blk, feed_peer = [], [], [], []
+        for p in plan.send_peers:
+            pp_ = plans[p]
+            gs = L.ghost_sources(p)                          # [Tp,4,g,n] global source cells
+            tid, _, _ = L.locate(gs)
+            sel = (np.asarray(L.owner)[tid] == rank) & (pp_.ghost_map < 0)
+            if not sel.any():
+                continue
+            slot = (-1 - pp_.ghost_map[sel]).astype(np.int64)
+            c = gs[sel]
+            tid2, i2, j2 = L.locate(c)
+            recv_tile = np.asarray(pp_.tiles)[np.nonzero(sel)[0]]
+            # side of the source tile facing the receiving tile with the cell inside the strip
+            cand = np.stack([(i2, j2), (n - 1 - i2, j2), (j2, i2), (n - 1 - j2, i2)], 0)   # [4, 2, M]
+            kk_all, pp_all = cand[:, 0], cand[:, 1]
+            ok = (tnbr[tid2].T == recv_tile[None, :]) & (kk_all < g)
+            if not ok.any(axis=0).all():
+                raise AssertionError("a remote ghost slot has no feeding strip cell")
+            s2 = np.argmax(ok, axis=0)
+            m = np.arange(len(c))
+            kk, pp = kk_all[s2, m], pp_all[s2, m]
+            li = L._local_arr[tid2]
+            code = (np.int64(p) << SLOT_BITS) | slot
+            cur = push[li, s2, kk, pp]
+            if not ((cur == -1) | (cur == -2 - code)).all():
+                raise AssertionError("push-map collision between a local and a remote ghost")
+            push[li, s2, kk, pp] = -2 - code
+            src_l.append(L.local_flat(c))
+            code_l.append(code)
+            ii, jj = _side_cell(s2, kk, pp, n)
+            feed_blk.append((li * self.nby + jj // by) * self.nbx + ii // bx)
+            feed_peer.append(np.full(len(c), p, dtype=np.int64))
+        self.push = push.astype(np.int32)
+        if src_l:
+            src = np.concatenate(src_l)
+            code = np.concatenate(code_l)
+            # one prime entry per (source cell, destination slot)
+            key = np.unique(np.stack([src, code], 1), axis=0)
+            self.prime_src = key[:, 0].astype(np.int32)
+            self.prime_code = key[:, 1].astype(np.int32)
+            fb, fp = np.concatenate(feed_blk), np.concatenate(feed_peer)
+        else:
+            self.prime_src = np.zeros(0, np.int32)
+            self.prime_code = np.zeros(0, np.int32)
+            fb = fp = np.zeros(0, np.int64)
+        bmask = np.zeros((self.nblocks, 2), dtype=np.int64)
+        np.bitwise_or.at(bmask[:, 1], fb, np.left_shift(1, fp))
+
+        # ---- consumer side ----------------------------------------------------
+        gm = plan.ghost_map
+        slot_peer = np.full(max(plan.num_recv, 1), -1, dtype=np.int64)
+        for p, off, cnt in zip(plan.recv_peers, plan.recv_offsets, plan.recv_counts):
+            slot_peer[off:off + cnt] = p
+        NG = halo
+        for t in range(plan.T):
+            for yb in range(self.nby):
+                y0 = yb * by
+                for xb in range(self.nbx):
+                    x0 = xb * bx
+                    bits = 0
+                    rows = slice(max(0, y0 - NG), min(n, y0 + by + NG))
+                    cols = slice(max(0, x0 - NG), min(n, x0 + bx + NG))
+                    parts = []
+                    if x0 < NG:
+                        parts.append(gm[t, 0, :NG - x0, rows])
+                    if x0 + bx + NG > n:
+                        parts.append(gm[t, 1, :min(NG, x0 + bx + NG - n), rows])
+                    if y0 < NG:
+                        parts.append(gm[t, 2, :NG - y0, cols])
+                    if y0 + by + NG > n:
+                        parts.append(gm[t, 3, :min(NG, y0 + by + NG - n), cols])
+                    for q in parts:
+                        r = q[q < 0]
+                        for p in np.unique(slot_peer[-1 - r]):
+                            bits |= 1 << int(p)
+                    bmask[(t * self.nby + yb) * self.nbx + xb, 0] = bits
+        self.bmask = bmask.astype(np.int32)
+
+        # producer blocks of each peer that feed this rank (cells of my ghosts, all layers)
+        self.nprod = np.zeros(MAX_WORLD, dtype=np.int64)
+        gs = L.ghost_sources(rank)
+        for p in plan.recv_peers:
+            sel = gm < 0
+            c = gs[sel]
+            tid, i, j = L.locate(c)
+            own = np.asarray(L.owner)[tid]
+            c_t, c_i, c_j = tid[own == p], i[own == p], j[own == p]
+            blk = (L._local_arr[c_t] * self.nby + c_j // by) * self.nbx + c_i // bx
+            self.nprod[p] = len(np.unique(blk))
+
+
+class XgmiHalo:
+    """Memory, IPC mappings and initial delivery of the direct exchange for
+    one ``Engine(backend='hip')``; ``fill(desc)`` turns a stage descriptor into
+    its XG form."""
+
+    def __init__(self, engine, group=None, timeout_s: float = 2.0):
+        from . import native
+        from .hip_compute import HipCompute
+        import torch.distributed as dist
+        e = engine
+        if not isinstance(e.compute, HipCompute):
+            raise RuntimeError("XgmiHalo needs an Engine with backend='hip'")
+        self.e = e
+        self.group = group
+        hc = e.compute
+        L = self._lib = _declare(native.require_native())
+        world = e.layout.num_ranks
+        self.world = world
+        self.rank = e.rank
+        self.xp = XgmiPlan(e.layout, e.rank, hc.bx, hc.by, e.physics.halo)
+        self._check_chain(e.integ)
+        dev = e.device
+        F = e.physics.F
+        self.esize = torch.tensor([], dtype=e.dtype).element_size()
+        self.ring = self.xp.ring_slots * F
+        nbytes = CNT_BYTES + 3 * self.ring * self.esize
+        base = ctypes.c_void_p()
+        rc = L.stsp_xg_alloc(ctypes.c_size_t(nbytes), ctypes.byref(base))
+        if rc != 0:
+            raise RuntimeError(f"uncached allocation for the xGMI ring failed ({rc})")
+        self.base = base.value
+        self.opened: List[int] = []
+        peers = sorted(set(self.xp.plan.send_peers) | set(self.xp.plan.recv_peers))
+        bases = {self.rank: self.base}
+        distributed = dist.is_available() and dist.is_initialized() and world > 1
+        if distributed:
+            L.stsp_enable_peers(dev.index if dev.index is not None else torch.cuda.current_device())
+            hb = L.stsp_ipc_handle_bytes()
+            h = (ctypes.c_char * hb)()
+            rc = L.stsp_ipc_get(ctypes.c_void_p(self.base), h)
+            if rc != 0:
+                raise RuntimeError(f"hipIpcGetMemHandle failed ({rc})")
+            allh = [None] * world
+            dist.all_gather_object(allh, bytes(h), group=group)
+            for p in peers:
+                if p == self.rank:
+                    continue
+                ptr = ctypes.c_void_p()
+                rc = L.stsp_ipc_open((ctypes.c_char * hb).from_buffer_copy(allh[p]), ctypes.byref(ptr))
+                if rc != 0:
+                    raise RuntimeError(f"hipIpcOpenMemHandle of rank {p} failed ({rc})")
+                self.opened.append(ptr.value)
+                bases[p] = ptr.value
+        elif any(p != self.rank for p in peers):
+            raise RuntimeError("remote peers but no initialised torch.distributed group to exchange IPC handles")
+        pr = np.zeros(MAX_WORLD, dtype=np.int64)
+        pc = np.zeros(MAX_WORLD, dtype=np.int64)
+        for p, b in bases.items():
+            pr[p] = b + CNT_BYTES
+            pc[p] = b + 8 * self.rank
+        self.peer_ring = torch.as_tensor(pr, device=dev)
+        self.peer_cnt = torch.as_tensor(pc, device=dev)
+        self.nprod = torch.as_tensor(self.xp.nprod, device=dev)
+        self.bmask = torch.as_tensor(self.xp.bmask, device=dev)
+        self.epoch = torch.zeros(self.xp.nblocks, dtype=torch.int32, device=dev)
+        self.err = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.push = torch.as_tensor(self.xp.push, device=dev)
+        self.prime_src = torch.as_tensor(self.xp.prime_src, device=dev)
+        self.prime_code = torch.as_tensor(self.xp.prime_code, device=dev)
+        assert int(self.xp.push.max(initial=-1)) < e.plan.S
+        assert self.prime_src.numel() == 0 or int(self.xp.prime_src.max()) < e.plan.S
+        self.timeout_ticks = int(timeout_s * 1e8)
+        self.prime()
+
+    @staticmethod
+    def _check_chain(integ) -> None:
+        """The ring carries the ghosts of each stage's output to the next
+        stage: every stage's halo input must be the previous stage's output."""
+        st = integ.stages
+        rot = integ.rotation
+        for k in range(len(st)):
+            prev = st[k - 1]
+            q = st[k].Q
+            out_prev = prev.out if k > 0 else [i for i in range(integ.nbuf) if rot[i] == prev.out][0]
+            if q != out_prev:
+                raise ValueError(f"integrator {integ.name}: stage {k} reads buffer {q}, not the previous output")
+
+    # ---- descriptors --------------------------------------------------------
+    def fill(self, d):
+        from . import native
+        d.xg = 1
+        d.remote = 0
+        d.blocks = 0
+        d.nblocks = self.xp.nblocks
+        d.ring = self.ring
+        d.recv = self.base + CNT_BYTES
+        d.push = native.ptr(self.push)
+        d.peer_ring = native.ptr(self.peer_ring)
+        d.peer_cnt = native.ptr(self.peer_cnt)
+        d.cnt = self.base
+        d.nprod = native.ptr(self.nprod)
+        d.bmask = native.ptr(self.bmask)
+        d.epoch = native.ptr(self.epoch)
+        d.err = native.ptr(self.err)
+        d.timeout_ticks = self.timeout_ticks
+        return d
+
+    # ---- initial / re-delivery ------------------------------------------------
+    def prime(self) -> None:
+        """Deliver the ghosts of the current state (pool[0]) into every peer's
+        ring slot for the next stage.  Collective: all ranks, quiescent."""
+        import torch.distributed as dist
+        from . import native
+        e = self.e
+        torch.cuda.synchronize(e.device)
+        ep = self.epoch
+        e0 = int(ep[0].item())
+        if not bool((ep == e0).all()):
+            raise RuntimeError("xGMI epochs diverged across blocks")
+        if dist.is_available() and dist.is_initialized() and self.world > 1:
+            dist.barrier(group=self.group)   # nobody still reads the slot we are about to fill
+        rc = self._lib.stsp_xg_prime_launch(native.dtype_code(e.dtype), native.ptr(e.pool[0]), e.plan.S,
+                                            e.physics.F, native.ptr(self.prime_src), native.ptr(self.prime_code),
+                                            int(self.prime_src.numel()), native.ptr(self.peer_ring), self.ring,
+                                            e0 % 3, native.current_stream_handle())
+        native.check(rc, "xGMI prime")
+        torch.cuda.synchronize(e.device)
+        if dist.is_available() and dist.is_initialized() and self.world > 1:
+            dist.barrier(group=self.group)
+
+    def check(self) -> None:
+        if int(self.err[0].item()) != 0:
+            raise RuntimeError("direct xGMI halo: a peer's ghosts did not arrive in time (poll timeout)")
+
+    def close(self) -> None:
+        L = self._lib
+        for p in self.opened:
+            L.stsp_ipc_close(ctypes.c_void_p(p))
+        self.opened = []
+        if getattr(self, "base", None):
+            torch.cuda.synchronize(self.e.device)
+            L.stsp_xg_free(ctypes.c_void_p(self.base))
+            self.base = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _declare(L):
+    vp, ci = ctypes.c_void_p, ctypes.c_int
+    L.stsp_xg_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]
+    L.stsp_xg_alloc.restype = ci
+    L.stsp_xg_free.argtypes = [vp]
+    L.stsp_xg_free.restype = ci
+    L.stsp_ipc_handle_bytes.argtypes = []
+    L.stsp_ipc_handle_bytes.restype = ci
+    L.stsp_ipc_get.argtypes = [vp, vp]
+    L.stsp_ipc_get.restype = ci
+    L.stsp_ipc_open.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p)]
+    L.stsp_ipc_open.restype = ci
+    L.stsp_ipc_close.argtypes = [vp]
+    L.stsp_ipc_close.restype = ci
+    L.stsp_enable_peers.argtypes = [ci]
+    L.stsp_enable_peers.restype = ci
+    L.stsp_xg_prime_launch.argtypes = [ci, vp, ci, ci, vp, vp, ci, vp, ci, ci, vp]
+    L.stsp_xg_prime_launch.restype = ci
+    return L
