@@ -142,9 +142,18 @@ int run_period(Runtime* rt, bool mark) {
   return 0;
 }
 
+int graph_mode() {
+  static const int m = [] {
+    const char* v = std::getenv("STSP_GRAPH_MODE");
+    return v ? std::atoi(v) : 0;
+  }();
+  return m;
+}
+
 int ensure_graph(Runtime* rt) {
   if (rt->exec) return 0;
-  RT_CHECK(hipStreamBeginCapture(rt->stream, hipStreamCaptureModeRelaxed));
+  const int gm = graph_mode();
+  RT_CHECK(hipStreamBeginCapture(rt->stream, (gm & 1) ? hipStreamCaptureModeGlobal : hipStreamCaptureModeRelaxed));
   int rc = 0;
   for (int p = 0; p < rt->graph_periods && rc == 0; ++p) rc = run_period(rt, false);
   hipGraph_t g = nullptr;
@@ -158,7 +167,13 @@ int ensure_graph(Runtime* rt) {
     return -1;
   }
   rt->graph = g;
-  RT_CHECK(hipGraphInstantiate(&rt->exec, rt->graph, nullptr, nullptr, 0));
+  if (gm & 2) {
+    const char* fv = std::getenv("STSP_GRAPH_IFLAGS");
+    RT_CHECK(hipGraphInstantiateWithFlags(&rt->exec, rt->graph, fv ? std::strtoull(fv, nullptr, 0) : 0));
+  }
+  else
+    RT_CHECK(hipGraphInstantiate(&rt->exec, rt->graph, nullptr, nullptr, 0));
+  if (gm & 4) RT_CHECK(hipGraphUpload(rt->exec, rt->stream));
   return 0;
 }
 
@@ -236,7 +251,16 @@ extern "C" int stsp_rt_run(void* p, int nsteps) {
     const int rc = ensure_graph(rt);
     if (rc) return rc;
     const int launches = periods / rt->graph_periods;
-    for (int i = 0; i < launches; ++i) RT_CHECK(hipGraphLaunch(rt->exec, rt->stream));
+    hipStream_t ls = (graph_mode() & 8) ? nullptr : rt->stream;
+    if (ls != rt->stream) {
+      RT_CHECK(hipEventRecord(rt->ev_fork, rt->stream));
+      RT_CHECK(hipStreamWaitEvent(ls, rt->ev_fork, 0));
+    }
+    for (int i = 0; i < launches; ++i) RT_CHECK(hipGraphLaunch(rt->exec, ls));
+    if (ls != rt->stream) {
+      RT_CHECK(hipEventRecord(rt->ev_join, ls));
+      RT_CHECK(hipStreamWaitEvent(rt->stream, rt->ev_join, 0));
+    }
     periods -= launches * rt->graph_periods;
   }
   for (int i = 0; i < periods; ++i) {

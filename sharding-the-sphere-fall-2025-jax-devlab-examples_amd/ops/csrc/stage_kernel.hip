@@ -28,6 +28,7 @@
 // (PDF s.12), 2 = shallow water with Cartesian momentum (PY:2).
 #include "stsp_kernels.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -43,11 +44,32 @@ template <int BX, int BY> struct Geom {
   static constexpr int NT = ((NX + NY + 63) / 64) * 64;
 };
 
-template <typename T> __device__ __forceinline__ T tabs(T x) { return x < T(0) ? -x : x; }
-template <typename T> __device__ __forceinline__ T tmin(T a, T b) { return a < b ? a : b; }
-template <typename T> __device__ __forceinline__ T tmax(T a, T b) { return a > b ? a : b; }
+// Hardware min/max/abs/copysign (v_max_f64, |x| source modifier, v_bfi):
+// one VALU op each where compare + select pairs cost three (wave64 fp64 and
+// integer VALU ops issue at the same 4 cycles, so every instruction counts).
+__device__ __forceinline__ double tabs(double x) { return __builtin_fabs(x); }
+__device__ __forceinline__ float tabs(float x) { return __builtin_fabsf(x); }
+__device__ __forceinline__ double tmin(double a, double b) { return __builtin_fmin(a, b); }
+__device__ __forceinline__ float tmin(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ double tmax(double a, double b) { return __builtin_fmax(a, b); }
+__device__ __forceinline__ float tmax(float a, float b) { return __builtin_fmaxf(a, b); }
+__device__ __forceinline__ double tsign(double m, double s) { return __builtin_copysign(m, s); }
+__device__ __forceinline__ float tsign(float m, float s) { return __builtin_copysignf(m, s); }
 __device__ __forceinline__ double tsqrt(double x) { return sqrt(x); }
 __device__ __forceinline__ float tsqrt(float x) { return sqrtf(x); }
+// 1/x: hardware reciprocal + two Newton steps (within an ulp of IEEE division,
+// 5 VALU ops instead of the 12-op div_scale/div_fmas/div_fixup sequence)
+__device__ __forceinline__ double trcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = __builtin_fma(-x, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-x, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+__device__ __forceinline__ float trcp(float x) {
+  float r = __builtin_amdgcn_rcpf(x);
+  return __builtin_fmaf(r, __builtin_fmaf(-x, r, 1.0f), r);
+}
 
 // Limited slope, identical to models/base.py::limited_slope; LIM is a
 // compile-time constant and every form is branch-free (selects only).
@@ -59,12 +81,10 @@ __device__ __forceinline__ T slope(T dl, T dr) {
     const bool same = dl * dr > T(0);
     T s;
     if constexpr (LIM == 1) {
-      const T m = tmin(tabs(dl), tabs(dr));
-      s = dl > T(0) ? m : -m;
+      s = tsign(tmin(tabs(dl), tabs(dr)), dl);
     } else if constexpr (LIM == 2) {
       const T c = T(0.5) * (dl + dr);
-      const T m = tmin(tmin(T(2) * tabs(dl), T(2) * tabs(dr)), tabs(c));
-      s = c > T(0) ? m : -m;
+      s = tsign(tmin(T(2) * tmin(tabs(dl), tabs(dr)), tabs(c)), c);
     } else {
       const T den = same ? dl + dr : T(1);
       s = T(2) * dl * dr / den;
@@ -78,6 +98,18 @@ __device__ __forceinline__ T slope(T dl, T dr) {
 template <typename T> struct V16;
 template <> struct V16<double> { using type = double2; static constexpr int W = 2; };
 template <> struct V16<float> { using type = float4; static constexpr int W = 4; };
+
+// base + i with a 32-bit byte offset: keeps the address in the global_load
+// saddr + voffset form (uniform 64-bit base in SGPRs, one 32-bit VGPR offset)
+// instead of a 64-bit VALU add per access.  Every buffer here is < 4 GiB.
+template <typename T>
+__device__ __forceinline__ const T* o32(const T* base, unsigned i) {
+  return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (unsigned)(i * (unsigned)sizeof(T)));
+}
+template <typename T>
+__device__ __forceinline__ T* o32(T* base, unsigned i) {
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (unsigned)(i * (unsigned)sizeof(T)));
+}
 
 template <typename T>
 __device__ __forceinline__ void load_rec8(const T* __restrict__ p, T (&r)[8]) {
@@ -112,6 +144,8 @@ struct Args {
   int ntile, n, S, mg, pw, nblocks, limiter;
   T a0, a1, a2, c0, c1, c2, dt, g, omega2;
   unsigned long long* stamps;
+  unsigned mdiv_t, mdiv_r;   // ceil(2^32 / (nbx nby)), ceil(2^32 / nbx); 0 = divide
+  int diag_repeat;           // diag build only: run the block body this many extra times
   // direct xGMI halo (XG kernels only, see stsp_kernels.h)
   int ring;
   T* const* peer_ring;
@@ -125,12 +159,14 @@ struct Args {
 };
 
 #ifdef STSP_STAMPS
-// Diagnostic build: wave 0 of each block records the shader clock at phase
-// boundaries (shares only; never quote a stamped build's run time).
+// Diagnostic build: lane 0 of every wave records the shader clock at phase
+// boundaries into stamps[block][wave < 16][8] (shares only; never quote a
+// stamped build's run time).
 #define STAMP(k)                                                                        \
   do {                                                                                  \
     __builtin_amdgcn_sched_barrier(0);                                                  \
-    if (threadIdx.x == 0 && a.stamps) a.stamps[(long)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+    if ((threadIdx.x & 63) == 0 && a.stamps)                                            \
+      a.stamps[((long)blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0);                                                  \
   } while (0)
 #else
@@ -234,28 +270,34 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   constexpr int NFX = (BX + 2) * BY;           // x-direction face tasks
   constexpr int NFY = BX * (BY + 2);           // y-direction face tasks
   static_assert(EX * EY <= NT, "window load assumes one cell per thread");
+  // LDS.  Face values, fluxes, normals and lengths are stored flat, x part then
+  // y part, indexed by task / edge id, so the x- and y-direction work of the
+  // face and flux phases is ONE code path (a wave that holds both kinds of
+  // task would otherwise execute both paths back to back).
+  constexpr int WS = EX + 1;                   // LDS row stride of the window
+  constexpr int WF = EY * WS;                  // LDS field stride of the window
+  constexpr int NE = NX + NY;                  // edges
+  constexpr int NFT = NFX + NFY;               // face tasks
+  constexpr bool SW = (P == 2);
   __shared__ T s_w[FL][EY][EX + 1];
   __shared__ T s_c[FC > 0 ? FC : 1][FC > 0 ? EY : 1][FC > 0 ? EX + 1 : 1];
-  __shared__ T s_xw[RECON ? F : 1][RECON ? BY : 1][RECON ? BX + 2 : 1];
-  __shared__ T s_xe[RECON ? F : 1][RECON ? BY : 1][RECON ? BX + 2 : 1];
-  __shared__ T s_ys[RECON ? F : 1][RECON ? BY + 2 : 1][RECON ? BX : 1];
-  __shared__ T s_yn[RECON ? F : 1][RECON ? BY + 2 : 1][RECON ? BX : 1];
-  __shared__ T s_fx[F][BY][BX + 1];
-  __shared__ T s_fy[F][BY + 1][BX];
-  constexpr bool SW = (P == 2);
-  __shared__ T s_nx[SW ? 3 : 1][SW ? BX + 1 : 1];      // x-edge normals of the block's columns
-  __shared__ T s_ny[SW ? 3 : 1][SW ? BY + 1 : 1];      // y-edge normals of the block's rows
-  __shared__ T s_lx[SW ? BY : 1][SW ? BX + 1 : 1];     // edge lengths (for the curvature balance)
-  __shared__ T s_ly[SW ? BY + 1 : 1][SW ? BX : 1];
+  __shared__ T s_fm[RECON ? F : 1][RECON ? NFT : 1];   // face value on the cell's minus side
+  __shared__ T s_fp[RECON ? F : 1][RECON ? NFT : 1];   // ... and plus side
+  __shared__ T s_fl[F][NE];                            // edge fluxes
+  __shared__ T s_nrm[SW ? 3 : 1][SW ? BX + BY + 2 : 1];  // edge normals: x columns, then y rows
+  __shared__ T s_len[SW ? NE : 1];                     // edge lengths (for the curvature balance)
 
   const int n = a.n, S = a.S, nn = n * n, mg = a.mg, pw = a.pw;
   const int nbx = (n + BX - 1) / BX, nby = (n + BY - 1) / BY;
-  const int tile = bid / (nbx * nby);
+  // bid -> (tile, yb, xb) by multiply-high with host-checked magic numbers
+  // (one s_mul_hi each; the generic division is a ~50-op float-reciprocal chain)
+  const int tile = a.mdiv_t ? (int)__umulhi((unsigned)bid, a.mdiv_t) : bid / (nbx * nby);
   const int rem = bid - tile * nbx * nby;
-  const int yb = rem / nbx, xb = rem - yb * nbx;
+  const int yb = a.mdiv_r ? (int)__umulhi((unsigned)rem, a.mdiv_r) : rem / nbx;
+  const int xb = rem - yb * nbx;
   const int x0 = xb * BX, y0 = yb * BY;
   const int tid = threadIdx.x;
-  const long tb = (long)tile * pw * pw;       // padded tile base
+  const unsigned tb = (unsigned)(tile * pw * pw);   // padded tile base
   const int gbase = tile * nn;                 // compact geometry base
   STAMP(0);
 
@@ -264,8 +306,8 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   const int ox = tid % BX, oy = tid / BX;
   const int cx = x0 + ox, cy = y0 + oy;
   const bool own = (tid < BX * BY) && (cx < n) && (cy < n);
-  const long pc = tb + (long)(cy + mg) * pw + (cx + mg);
-  const int gc = gbase + cy * n + cx;
+  const unsigned pc = tb + (unsigned)((cy + mg) * pw + (cx + mg));
+  const unsigned gc = (unsigned)(gbase + cy * n + cx);
   T xs[F], acs[F];
   T iA = T(0), r0 = T(0), r1 = T(0), r2 = T(0);
   T gb[3] = {T(0), T(0), T(0)};
@@ -275,34 +317,39 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   if (own) {
     if (need_x) {
 #pragma unroll
-      for (int f = 0; f < F; ++f) xs[f] = ld_state<SYNC>(a.X + (long)f * S + pc);
+      for (int f = 0; f < F; ++f) xs[f] = ld_state<SYNC>(o32(a.X + f * S, pc));
     }
     if (need_acc) {
 #pragma unroll
-      for (int f = 0; f < F; ++f) acs[f] = ld_state<SYNC>(a.acc_in + (long)f * S + pc);
+      for (int f = 0; f < F; ++f) acs[f] = ld_state<SYNC>(o32(a.acc_in + f * S, pc));
     }
     if constexpr (P == 2) {
       T rec[8];
-      load_rec8<T>(a.cgeo + (long)gc * 8, rec);
+      load_rec8<T>(o32(a.cgeo, gc * 8u), rec);
       iA = rec[0]; r0 = rec[1]; r1 = rec[2]; r2 = rec[3];
       gb[0] = rec[4]; gb[1] = rec[5]; gb[2] = rec[6];
     } else {
-      iA = a.invA[gc];
+      iA = *o32(a.invA, gc);
     }
     const int* pm = a.push + (long)tile * 4 * mg * n;
-    if (cx < mg) pt[0] = pm[(0 * mg + cx) * n + cy];
-    if (cx >= n - mg) pt[1] = pm[(1 * mg + (n - 1 - cx)) * n + cy];
-    if (cy < mg) pt[2] = pm[(2 * mg + cy) * n + cx];
-    if (cy >= n - mg) pt[3] = pm[(3 * mg + (n - 1 - cy)) * n + cx];
+    if (cx < mg) pt[0] = *o32(pm, (unsigned)((0 * mg + cx) * n + cy));
+    if (cx >= n - mg) pt[1] = *o32(pm, (unsigned)((1 * mg + (n - 1 - cx)) * n + cy));
+    if (cy < mg) pt[2] = *o32(pm, (unsigned)((2 * mg + cy) * n + cx));
+    if (cy >= n - mg) pt[3] = *o32(pm, (unsigned)((3 * mg + (n - 1 - cy)) * n + cx));
   }
-  if constexpr (P == 2) {   // edge normals of this block's columns / rows -> LDS
+  // edge normals of this block's columns / rows: into a register now, into LDS
+  // only after the window loads are issued (an LDS store of a global load makes
+  // the wave wait for it, and vmcnt waits are in order: storing here would put a
+  // whole memory round trip in front of the window load)
+  T nrm = T(0);
+  if constexpr (P == 2) {
     if (tid < 3 * (BX + 1)) {
       const int k = tid / (BX + 1), c = tid - k * (BX + 1);
-      s_nx[k][c] = (x0 + c <= n) ? a.mx[((long)tile * 3 + k) * (n + 1) + x0 + c] : T(0);
+      if (x0 + c <= n) nrm = *o32(a.mx, (unsigned)((tile * 3 + k) * (n + 1) + x0 + c));
     } else if (tid < 3 * (BX + 1) + 3 * (BY + 1)) {
       const int u = tid - 3 * (BX + 1);
       const int k = u / (BY + 1), c = u - k * (BY + 1);
-      s_ny[k][c] = (y0 + c <= n) ? a.my[((long)tile * 3 + k) * (n + 1) + y0 + c] : T(0);
+      if (y0 + c <= n) nrm = *o32(a.my, (unsigned)((tile * 3 + k) * (n + 1) + y0 + c));
     }
   }
   // (b) this thread's edge (threads < NX: x-edge, NX <= tid < NX+NY: y-edge)
@@ -314,8 +361,8 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   const bool edge_ok = is_x ? (ex_ <= n && ey_ < n) : (tid < NX + NY && ex_ < n && ey_ <= n);
   T coef = T(0);
   if (edge_ok) {
-    coef = is_x ? a.ex[(long)tile * n * (n + 1) + ey_ * (n + 1) + ex_]
-                : a.ey[(long)tile * (n + 1) * n + ey_ * n + ex_];
+    coef = is_x ? *o32(a.ex, (unsigned)(tile * n * (n + 1) + ey_ * (n + 1) + ex_))
+                : *o32(a.ey, (unsigned)(tile * (n + 1) * n + ey_ * n + ex_));
   }
   STAMP(1);
 
@@ -354,7 +401,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     if constexpr (P == 2) {  // keep conserved (h, M); primitive (h, v) + sqrt(g h)
 #pragma unroll
       for (int f = 0; f < 4; ++f) s_c[f][ly][lx] = v[f];
-      const T inv = v[0] != T(0) ? T(1) / v[0] : T(0);
+      const T inv = v[0] != T(0) ? trcp(v[0]) : T(0);
       s_w[0][ly][lx] = v[0];
       s_w[1][ly][lx] = v[1] * inv;
       s_w[2][ly][lx] = v[2] * inv;
@@ -374,17 +421,17 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 #pragma unroll
       for (int f = 0; f < F; ++f) { v0[f] = T(0); v1[f] = T(0); }
       if (y < n + NG && x < n + NG) {
-        const long pa = tb + (long)(y + mg) * pw + (x + mg);
+        const unsigned pa = tb + (unsigned)((y + mg) * pw + (x + mg));
         if (x + 1 < n + NG) {
           using V2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
 #pragma unroll
           for (int f = 0; f < F; ++f) {
-            const V2 w = *reinterpret_cast<const V2*>(a.Q + (long)f * S + pa);
+            const V2 w = *reinterpret_cast<const V2*>(o32(a.Q + f * S, pa));
             v0[f] = w.x; v1[f] = w.y;
           }
         } else {
 #pragma unroll
-          for (int f = 0; f < F; ++f) v0[f] = ld_state<SYNC>(a.Q + (long)f * S + pa);
+          for (int f = 0; f < F; ++f) v0[f] = ld_state<SYNC>(o32(a.Q + f * S, pa));
         }
       }
       put(ly, lx, v0);
@@ -397,7 +444,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 #pragma unroll
     for (int f = 0; f < F; ++f) v[f] = T(0);
     if (x < n + NG && y < n + NG) {          // false only past a partial block
-      const long pa = tb + (long)(y + mg) * pw + (x + mg);
+      const unsigned pa = tb + (unsigned)((y + mg) * pw + (x + mg));
       bool from_recv = false;
       if constexpr (REMOTE || XG) {
         const bool oxx = (x < 0) | (x >= n), oyy = (y < 0) | (y >= n);
@@ -423,44 +470,45 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       }
       if (!from_recv) {
 #pragma unroll
-        for (int f = 0; f < F; ++f) v[f] = ld_state<SYNC>(a.Q + (long)f * S + pa);
+        for (int f = 0; f < F; ++f) v[f] = ld_state<SYNC>(o32(a.Q + f * S, pa));
       }
     }
     put(ly, lx, v);
+  }
+  if constexpr (P == 2) {
+    if (tid < 3 * (BX + 1)) {
+      const int k = tid / (BX + 1), c = tid - k * (BX + 1);
+      s_nrm[k][c] = nrm;
+    } else if (tid < 3 * (BX + 1) + 3 * (BY + 1)) {
+      const int u = tid - 3 * (BX + 1);
+      const int k = u / (BY + 1), c = u - k * (BY + 1);
+      s_nrm[k][BX + 1 + c] = nrm;
+    }
   }
   STAMP(2);
   __syncthreads();
   STAMP(3);
 
   // ---- 1b. PLR face values, one (cell, direction) per thread -------------------
+  // task t < NFX: x-direction, cell (x0 + c - 1, y0 + r), t = r (BX + 2) + c;
+  // else y-direction, cell (x0 + c, y0 + r - 1), t - NFX = r BX + c.
   if constexpr (RECON) {
-    for (int t = tid; t < NFX + NFY; t += NT) {
-      if (t < NFX) {
-        const int r = t / (BX + 2), c = t - r * (BX + 2);
-        const int x = x0 + c - 1, y = y0 + r;
-        if (x <= n && y < n) {
-          const int ly = NG + r, lx = NG - 1 + c;
+    const T* w0 = &s_w[0][0][0];
+    for (int t = tid; t < NFT; t += NT) {
+      const bool tx = t < NFX;
+      const int u = tx ? t : t - NFX;
+      const int r = tx ? u / (BX + 2) : u / BX;
+      const int c = u - r * (tx ? BX + 2 : BX);
+      const int x = x0 + (tx ? c - 1 : c), y = y0 + (tx ? r : r - 1);
+      if (x <= n && y <= n) {
+        const int ci = (tx ? NG + r : NG - 1 + r) * WS + (tx ? NG - 1 + c : NG + c);
+        const int st = tx ? 1 : WS;
 #pragma unroll
-          for (int f = 0; f < F; ++f) {
-            const T m1 = s_w[f][ly][lx - 1], c0 = s_w[f][ly][lx], p1 = s_w[f][ly][lx + 1];
-            const T hs = T(0.5) * slope<LIM>(c0 - m1, p1 - c0);
-            s_xw[f][r][c] = c0 - hs;
-            s_xe[f][r][c] = c0 + hs;
-          }
-        }
-      } else {
-        const int u = t - NFX;
-        const int r = u / BX, c = u - r * BX;
-        const int x = x0 + c, y = y0 + r - 1;
-        if (x < n && y <= n) {
-          const int ly = NG - 1 + r, lx = NG + c;
-#pragma unroll
-          for (int f = 0; f < F; ++f) {
-            const T m1 = s_w[f][ly - 1][lx], c0 = s_w[f][ly][lx], p1 = s_w[f][ly + 1][lx];
-            const T hs = T(0.5) * slope<LIM>(c0 - m1, p1 - c0);
-            s_ys[f][r][c] = c0 - hs;
-            s_yn[f][r][c] = c0 + hs;
-          }
+        for (int f = 0; f < F; ++f) {
+          const T m1 = w0[f * WF + ci - st], c0 = w0[f * WF + ci], p1 = w0[f * WF + ci + st];
+          const T hs = T(0.5) * slope<LIM>(c0 - m1, p1 - c0);
+          s_fm[f][t] = c0 - hs;
+          s_fp[f][t] = c0 + hs;
         }
       }
     }
@@ -468,53 +516,43 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   }
   STAMP(4);
 
-  // ---- 2. one edge flux per thread --------------------------------------------
+  // ---- 2. one edge flux per thread (edge id = tid: x-edges, then y-edges) -------
+  // x-edge (e_r, e_c) lies between cells e_c - 1 and e_c of row e_r (face tasks
+  // e_r (BX + 2) + e_c and + 1); y-edge (e_r, e_c) between rows e_r - 1 and e_r
+  // (face tasks NFX + e_r BX + e_c and + BX).
   if (edge_ok) {
-    if (is_x) {
-      const int ly = NG + e_r, lr = NG + e_c, ll = lr - 1;
-      if constexpr (P == 1) {
-        s_fx[0][e_r][e_c] = -coef * (s_w[0][ly][lr] - s_w[0][ly][ll]);
-      } else if constexpr (P == 0) {
-        const T wl = s_xe[0][e_r][e_c], wr = s_xw[0][e_r][e_c + 1];
-        s_fx[0][e_r][e_c] = coef * (coef > T(0) ? wl : wr);
-      } else {
-        T wl[4], wr[4], cl[5], cr[5];
-#pragma unroll
-        for (int f = 0; f < 4; ++f) { wl[f] = s_xe[f][e_r][e_c]; wr[f] = s_xw[f][e_r][e_c + 1]; }
-#pragma unroll
-        for (int f = 0; f < 5; ++f) { cl[f] = s_w[f][ly][ll]; cr[f] = s_w[f][ly][lr]; }
-        T fl[4];
-        swe_flux<T>(wl, wr, cl, cr, s_nx[0][e_c], s_nx[1][e_c], s_nx[2][e_c], coef, a.g, fl);
-#pragma unroll
-        for (int f = 0; f < 4; ++f) s_fx[f][e_r][e_c] = fl[f];
-        s_lx[e_r][e_c] = coef;
-      }
+    const int fl_ = is_x ? e_r * (BX + 2) + e_c : NFX + e_r * BX + e_c;   // face task of the left cell
+    const int fst = is_x ? 1 : BX;
+    const int cl_ = is_x ? (NG + e_r) * WS + NG - 1 + e_c : (NG - 1 + e_r) * WS + NG + e_c;
+    const int cst = is_x ? 1 : WS;
+    const T* w0 = &s_w[0][0][0];
+    if constexpr (P == 1) {
+      s_fl[0][tid] = -coef * (w0[cl_ + cst] - w0[cl_]);
+    } else if constexpr (P == 0) {
+      const T wl = s_fp[0][fl_], wr = s_fm[0][fl_ + fst];
+      s_fl[0][tid] = coef * (coef > T(0) ? wl : wr);
     } else {
-      const int lx = NG + e_c, lt = NG + e_r, lb = lt - 1;
-      if constexpr (P == 1) {
-        s_fy[0][e_r][e_c] = -coef * (s_w[0][lt][lx] - s_w[0][lb][lx]);
-      } else if constexpr (P == 0) {
-        const T wl = s_yn[0][e_r][e_c], wr = s_ys[0][e_r + 1][e_c];
-        s_fy[0][e_r][e_c] = coef * (coef > T(0) ? wl : wr);
-      } else {
-        T wl[4], wr[4], cl[5], cr[5];
+      T wl[4], wr[4], cl[5], cr[5];
 #pragma unroll
-        for (int f = 0; f < 4; ++f) { wl[f] = s_yn[f][e_r][e_c]; wr[f] = s_ys[f][e_r + 1][e_c]; }
+      for (int f = 0; f < 4; ++f) { wl[f] = s_fp[f][fl_]; wr[f] = s_fm[f][fl_ + fst]; }
 #pragma unroll
-        for (int f = 0; f < 5; ++f) { cl[f] = s_w[f][lb][lx]; cr[f] = s_w[f][lt][lx]; }
-        T fl[4];
-        swe_flux<T>(wl, wr, cl, cr, s_ny[0][e_r], s_ny[1][e_r], s_ny[2][e_r], coef, a.g, fl);
+      for (int f = 0; f < 5; ++f) { cl[f] = w0[f * WF + cl_]; cr[f] = w0[f * WF + cl_ + cst]; }
+      const int ni = is_x ? e_c : BX + 1 + e_r;
+      T fl[4];
+      swe_flux<T>(wl, wr, cl, cr, s_nrm[0][ni], s_nrm[1][ni], s_nrm[2][ni], coef, a.g, fl);
 #pragma unroll
-        for (int f = 0; f < 4; ++f) s_fy[f][e_r][e_c] = fl[f];
-        s_ly[e_r][e_c] = coef;
-      }
+      for (int f = 0; f < 4; ++f) s_fl[f][tid] = fl[f];
+      s_len[tid] = coef;
     }
   }
   STAMP(5);
   __syncthreads();
+  STAMP(7);
 
   // ---- 3. divergence + sources + RK combination + push -------------------------
   if (own) {
+    const int ew = oy * (BX + 1) + ox;          // west x-edge of the cell
+    const int es = NX + oy * BX + ox;           // south y-edge
     T qs[F];
     if constexpr (P == 2) {
 #pragma unroll
@@ -525,17 +563,17 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     T dq[F];
 #pragma unroll
     for (int f = 0; f < F; ++f)
-      dq[f] = -((s_fx[f][oy][ox + 1] - s_fx[f][oy][ox]) + (s_fy[f][oy + 1][ox] - s_fy[f][oy][ox])) * iA;
+      dq[f] = -((s_fl[f][ew + 1] - s_fl[f][ew]) + (s_fl[f][es + BX] - s_fl[f][es])) * iA;
     if constexpr (P == 2) {
       const T fc = a.omega2 * r2;
       const T h = qs[0];
       const T cor[3] = {r1 * qs[3] - r2 * qs[2], r2 * qs[1] - r0 * qs[3], r0 * qs[2] - r1 * qs[1]};
       // curvature balance g/2 h^2 sum(+-L m)/A: a constant depth is force-free
-      const T Lw = s_lx[oy][ox], Le = s_lx[oy][ox + 1], Ls = s_ly[oy][ox], Ln = s_ly[oy + 1][ox];
+      const T Lw = s_len[ew], Le = s_len[ew + 1], Ls = s_len[es], Ln = s_len[es + BX];
       const T pb = T(0.5) * a.g * h * h * iA, gh = a.g * h;
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const T Sk = Le * s_nx[k][ox + 1] - Lw * s_nx[k][ox] + Ln * s_ny[k][oy + 1] - Ls * s_ny[k][oy];
+        const T Sk = Le * s_nrm[k][ox + 1] - Lw * s_nrm[k][ox] + Ln * s_nrm[k][BX + 2 + oy] - Ls * s_nrm[k][BX + 1 + oy];
         dq[1 + k] += -fc * cor[k] + pb * Sk - gh * gb[k];
       }
     }
@@ -571,15 +609,15 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
         p[1] -= d * r0; p[2] -= d * r1; p[3] -= d * r2;
       }
 #pragma unroll
-      for (int f = 0; f < F; ++f) st_state<SYNC>(a.acc_out + (long)f * S + pc, p[f]);
+      for (int f = 0; f < F; ++f) st_state<SYNC>(o32(a.acc_out + f * S, pc), p[f]);
     }
 #pragma unroll
-    for (int f = 0; f < F; ++f) st_state<SYNC>(a.out + (long)f * S + pc, o[f]);
+    for (int f = 0; f < F; ++f) st_state<SYNC>(o32(a.out + f * S, pc), o[f]);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (pt[k] >= 0) {
 #pragma unroll
-        for (int f = 0; f < F; ++f) st_state<SYNC>(a.out + (long)f * S + pt[k], o[f]);
+        for (int f = 0; f < F; ++f) st_state<SYNC>(o32(a.out + f * S, (unsigned)pt[k]), o[f]);
       }
     }
     if constexpr (XG) {   // remote ghosts: straight into the consumer's ring
@@ -634,6 +672,14 @@ __global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
   pin_args(a);
   const int bid = LIST ? a.blocks[blockIdx.x] : xcd_remap(blockIdx.x, a.nblocks);
   stage_body<T, P, BX, BY, LIM, REMOTE, false, XG>(a, bid);
+#ifdef STSP_STAMPS
+  // warm-instruction-cache experiment: repeat the (idempotent, for stages
+  // without an in-place accumulator) body; the stamps keep the last pass
+  for (int r = 0; r < a.diag_repeat; ++r) {
+    __syncthreads();
+    stage_body<T, P, BX, BY, LIM, REMOTE, false, XG>(a, bid);
+  }
+#endif
 }
 
 // ---- persistent multi-step kernel (small grids) --------------------------------
@@ -722,9 +768,9 @@ __global__ __launch_bounds__((Geom<BX, BY>::NT)) void persistent_kernel(PArgs<T>
   }
 #ifdef STSP_STAMPS
   if (tid == 0 && pa.st[0].stamps) {
-    pa.st[0].stamps[(long)blockIdx.x * 8 + 0] = acc_body;
-    pa.st[0].stamps[(long)blockIdx.x * 8 + 1] = acc_drain;
-    pa.st[0].stamps[(long)blockIdx.x * 8 + 2] = acc_wait;
+    pa.st[0].stamps[(long)blockIdx.x * 128 + 0] = acc_body;
+    pa.st[0].stamps[(long)blockIdx.x * 128 + 1] = acc_drain;
+    pa.st[0].stamps[(long)blockIdx.x * 128 + 2] = acc_wait;
   }
 #endif
 }
@@ -742,6 +788,7 @@ Args<T> make_args(const StageDesc* d) {
   a.a0 = (T)d->a0; a.a1 = (T)d->a1; a.a2 = (T)d->a2; a.c0 = (T)d->c0; a.c1 = (T)d->c1; a.c2 = (T)d->c2;
   a.dt = (T)d->dt; a.g = (T)d->g; a.omega2 = (T)d->omega2;
   a.stamps = (unsigned long long*)d->stamps;
+  a.diag_repeat = 0;
   a.ring = d->ring;
   a.peer_ring = (T* const*)d->peer_ring;
   a.peer_cnt = d->peer_cnt;
@@ -754,9 +801,29 @@ Args<T> make_args(const StageDesc* d) {
   return a;
 }
 
+// ceil(2^32 / dv) if floor(x * M / 2^32) == x / dv for every x < xmax (holds
+// when xmax * dv <= 2^32: the rounding excess x (M dv - 2^32) / 2^32 < 1), else 0.
+inline unsigned magic_div(unsigned dv, unsigned long long xmax) {
+  if (dv <= 1 || xmax * dv > (1ull << 32)) return 0;
+  return (unsigned)(((1ull << 32) + dv - 1) / dv);
+}
+
+template <typename T, int BX, int BY>
+void set_magic(Args<T>& a) {
+  const unsigned nbx = (a.n + BX - 1) / BX, nby = (a.n + BY - 1) / BY;
+  const unsigned long long total = (unsigned long long)a.ntile * nbx * nby;
+  a.mdiv_t = magic_div(nbx * nby, total);
+  a.mdiv_r = magic_div(nbx, (unsigned long long)nbx * nby);
+}
+
 template <typename T, int P, int BX, int BY, int LIM>
 int launch_l(const StageDesc* d, hipStream_t s) {
   Args<T> a = make_args<T>(d);
+  set_magic<T, BX, BY>(a);
+#ifdef STSP_STAMPS
+  const char* rp = std::getenv("STSP_DIAG_REPEAT");
+  a.diag_repeat = rp ? std::atoi(rp) : 0;
+#endif
   constexpr int NT = Geom<BX, BY>::NT;
   const dim3 grid(d->nblocks), block(NT);
   if (d->xg)
@@ -847,7 +914,10 @@ template <typename T, int P, int BX, int BY, int LIM>
 int launch_persist(const StageDesc* st, int nstages, int nsteps, unsigned* flags, const int* nbr, int maxnbr,
                    int* err, double timeout_s, hipStream_t s) {
   PArgs<T> pa;
-  for (int k = 0; k < nstages; ++k) pa.st[k] = make_args<T>(&st[k]);
+  for (int k = 0; k < nstages; ++k) {
+    pa.st[k] = make_args<T>(&st[k]);
+    set_magic<T, BX, BY>(pa.st[k]);
+  }
   pa.nstages = nstages;
   pa.nsteps = nsteps;
   pa.flags = flags;

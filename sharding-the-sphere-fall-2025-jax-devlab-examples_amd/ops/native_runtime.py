@@ -182,8 +182,18 @@ class NativeStepper:
         import os
         graph_ok = (not self.remote) or os.environ.get("STSP_GRAPH_COMM") == "1"
         self.use_graph = bool(use_graph and graph_ok)
-        d.use_graph = 1 if self.use_graph else 0
-        d.graph_periods = max(1, steps_per_graph // period)
+        # Graph container: the C++ runtime's eager op list recorded by
+        # torch.cuda.graph and replayed on torch's current stream.  Measured on
+        # MI355X (tools/runtime_ab.py, C96): 17.2 us/step, against 20-21 us/step
+        # for the same launches replayed on a side stream (C++-side graph or
+        # torch graph alike; capture mode, instantiate flags and upload made no
+        # difference).  STSP_NATIVE_GRAPH=1 selects the C++-side graph.
+        self._cxx_graph = self.use_graph and os.environ.get("STSP_NATIVE_GRAPH") == "1"
+        d.use_graph = 1 if self._cxx_graph else 0
+        self.graph_periods = max(1, steps_per_graph // period)
+        d.graph_periods = self.graph_periods
+        self._tg = None
+        self._warmed = False
         d.stream = int(self.stream.cuda_stream)
         d.nccl_comm = nccl_comm or 0
         d.roctx = 1 if roctx else 0
@@ -225,14 +235,44 @@ class NativeStepper:
         if self.xgmi is not None:
             self.xgmi.check()
 
+    def _run_native(self, nsteps: int) -> None:
+        """Eager op list on self.stream, ordered after and before torch's
+        current stream."""
+        if nsteps:
+            cur = torch.cuda.current_stream(self.e.device)
+            self.stream.wait_stream(cur)
+            self._check(self.L.stsp_rt_run(self.h, nsteps), "run")
+            cur.wait_stream(self.stream)
+
+    def _run(self, nsteps: int) -> None:
+        """nsteps (a multiple of the period)."""
+        if not self.use_graph or self._cxx_graph:
+            self._run_native(nsteps)
+            return
+        k = self.graph_periods * self.period
+        if not self._warmed:
+            # lazy one-time setup (RCCL, streams) must not happen under capture:
+            # the first period runs eagerly and counts
+            self._run_native(self.period)
+            nsteps -= self.period
+            torch.cuda.synchronize(self.e.device)
+            self._warmed = True
+        if self._tg is None:          # record once, up front (after a set_dt: again)
+            self._tg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._tg, stream=self.stream):
+                self._check(self.L.stsp_rt_run(self.h, k), "capture")   # recorded, not executed
+        full = nsteps // k if self._tg is not None else 0
+        # replay on torch's current stream: measured 17.2 us/step at C96 there
+        # against 20-21 us/step when the same graph is launched on a side stream
+        for _ in range(full):
+            self._tg.replay()
+        self._run_native(nsteps - full * k)
+
     def run(self, nsteps: int) -> None:
         e = self.e
         full = (nsteps // self.period) * self.period
         if full:
-            # the compute stream follows torch's current stream and vice versa
-            self.stream.wait_stream(torch.cuda.current_stream(e.device))
-            self._check(self.L.stsp_rt_run(self.h, full), "run")
-            torch.cuda.current_stream(e.device).wait_stream(self.stream)
+            self._run(full)
             e.time += full * e.dt
             e.step_count += full
         if nsteps - full:
@@ -241,8 +281,10 @@ class NativeStepper:
     def set_dt(self, dt: float) -> None:
         self.e.dt = dt
         self._check(self.L.stsp_rt_set_dt(self.h, dt), "set_dt")
+        self._tg = None       # recorded launches carry the old dt
 
     def close(self) -> None:
+        self._tg = None
         if getattr(self, "h", None):
             self.L.stsp_rt_destroy(self.h)
             self.h = None

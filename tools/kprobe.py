@@ -55,7 +55,7 @@ def main():
             d = hc.desc(st, e.dt, lst, a.limit)
         stamps = None
         if a.stamps:
-            stamps = torch.zeros(hc.nblocks * 8, dtype=torch.int64, device="cuda")
+            stamps = torch.zeros(hc.nblocks * 16 * 8, dtype=torch.int64, device="cuda")
             d.stamps = native.ptr(stamps)
         s = torch.cuda.Stream()
         with torch.cuda.stream(s):
@@ -78,17 +78,18 @@ def main():
         us = t0.elapsed_time(t1) * 1e3 / (3 * a.reps)
         r = {"us_per_launch": us, "nblocks": hc.nblocks}
         if a.stamps:
-            st_ = stamps.view(-1, 8).cpu().numpy().astype("float64")
             import numpy as np
-            ph = np.diff(st_[:, :7], axis=1)
-            tot = st_[:, 6] - st_[:, 0]
-            r["phase_cycles_median"] = {k: float(np.median(ph[:, i])) for i, k in enumerate(
-                ["prefetch_issue", "window_load", "barrier1", "faces+barrier", "flux", "barrier2+update"])}
+            nw = -(-((bx + 1) * by + bx * (by + 1)) // 64)        # waves per block
+            st_ = stamps.view(-1, 16, 8).cpu().numpy().astype("float64")[:, :nw]   # [block, wave, k]
+            t0_ = st_[:, :, 0].min(axis=1)                         # block start (first wave)
+            rel = st_ - t0_[:, None, None]
+            names = ["start", "prefetch", "window", "barrier1", "faces+barrier", "flux", "end", "barrier2"]
+            # median over blocks of each wave's time at each stamp, relative to block start
+            r["wave_stamp_cycles_median"] = {names[k]: [float(np.median(rel[:, w, k])) for w in range(nw)]
+                                             for k in range(8)}
+            tot = st_[:, :, 6].max(axis=1) - t0_
             r["block_cycles_median"] = float(np.median(tot))
             r["block_cycles_max"] = float(tot.max())
-            span = st_[:, 6].max() - st_[:, 0].min()
-            r["grid_span_cycles"] = float(span)
-            r["start_skew_cycles"] = float(st_[:, 0].max() - st_[:, 0].min())
         res[bs] = r
     # launch floor: a 1-element indexed-copy kernel, same graph method
     src = torch.zeros(8, dtype=dtype, device="cuda")
