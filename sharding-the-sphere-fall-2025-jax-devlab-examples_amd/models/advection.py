@@ -16,7 +16,7 @@ from typing import Dict
 import numpy as np
 import torch
 
-from .base import Physics, RankGeometry, plr_x, plr_y
+from .base import Physics, RankGeometry, plr_x, plr_y, recon_halo
 from .geometry import DAY, CubedSphereGrid
 from . import initial_conditions as ic
 
@@ -25,7 +25,10 @@ class Advection(Physics):
     name = "advection"
     kernel_id = 0
     fields = ["q"]
-    halo = 2
+
+    @property
+    def halo(self) -> int:
+        return recon_halo(self.limiter)
 
     def __init__(self, case: str = "cosine_bell", alpha: float = 0.0, limiter: int = 2, u0: float = None):
         self.case = case
@@ -59,16 +62,17 @@ class Advection(Physics):
         ux = np.sum(self.wind(geo.grid, geo.xmid) * geo.mx[:, None, :, :], axis=-1) * geo.lx
         uy = np.sum(self.wind(geo.grid, geo.ymid) * geo.my[:, :, None, :], axis=-1) * geo.ly
         t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=device)
-        return {"area": t(geo.area), "invA": t(1.0 / geo.area), "ex": t(ux), "ey": t(uy)}
+        return {"area": t(geo.area), "invA": t(1.0 / geo.area), "ex": t(ux), "ey": t(uy),
+                "pedge": torch.as_tensor(geo.pedge, device=device)}   # [T] panel-edge side bits (PPM)
 
     def kernel_params(self):
         return {"limiter": self.limiter}
 
     def rhs(self, qe, qi, tens, n, g):
-        qL, qR = plr_x(qe, g, n, self.limiter)
+        qL, qR = plr_x(qe, g, n, self.limiter, tens.get("pedge"))
         U = tens["ex"]
         Fx = U * torch.where(U > 0, qL, qR)
-        qL, qR = plr_y(qe, g, n, self.limiter)
+        qL, qR = plr_y(qe, g, n, self.limiter, tens.get("pedge"))
         V = tens["ey"]
         Gy = V * torch.where(V > 0, qL, qR)
         return -((Fx[..., 1:] - Fx[..., :-1]) + (Gy[..., 1:, :] - Gy[..., :-1, :])) * tens["invA"]

@@ -24,7 +24,13 @@ import torch
 from ..parallel.layout import RankPlan, TileLayout
 from .geometry import CubedSphereGrid, arc_angle, tangent_project
 
-LIMITERS = {"none": 0, "central": 0, "minmod": 1, "mc": 2, "vanleer": 3}
+LIMITERS = {"none": 0, "central": 0, "minmod": 1, "mc": 2, "vanleer": 3, "ppm": 4}
+PPM = 4          # piecewise-parabolic faces (Colella & Woodward 1984), needs halo 3
+
+
+def recon_halo(lim: int) -> int:
+    """Ghost layers the reconstruction reads: 2 for PLR, 3 for PPM."""
+    return 3 if lim == PPM else 2
 
 
 def limiter_code(name) -> int:
@@ -66,9 +72,12 @@ class RankGeometry:
         self.ymid = np.empty((self.T, n + 1, n, 3))
         self.ext1 = np.empty((self.T, n + 2, n + 2), dtype=np.int64)
         self.face = np.empty(self.T, dtype=np.int64)
+        # bit s set: tile side s (W, E, S, N) lies on a cube (panel) edge
+        self.pedge = np.zeros(self.T, dtype=np.int32)
         for li, tid in enumerate(tiles):
             f, I0, J0 = layout.tile_origin(tid)
             self.face[li] = f
+            self.pedge[li] = (1 * (I0 == 0)) | (2 * (I0 + n == N)) | (4 * (J0 == 0)) | (8 * (J0 + n == N))
             sj, si = slice(J0, J0 + n), slice(I0, I0 + n)
             self.area[li] = A[f, sj, si]
             self.center[li] = C[f, sj, si]
@@ -184,19 +193,68 @@ def limited_slope(dl: torch.Tensor, dr: torch.Tensor, lim: int) -> torch.Tensor:
     raise ValueError(lim)
 
 
-def plr_x(qe: torch.Tensor, g: int, n: int, lim: int):
-    """Left/right PLR states at the n+1 x-edges of the interior rows:
-    returns (qL, qR) each [..., n, n+1]."""
+def ppm_faces(q: torch.Tensor, g: int, n: int, lo_edge=None, hi_edge=None):
+    """PPM face values of cells -1..n of each row (q: [..., W], cell c at index
+    c + g, g >= 3).  Fourth-order interface values
+    a_{k-1/2} = 7/12 (q_{k-1} + q_k) - 1/12 (q_{k-2} + q_{k+1}), then the
+    Colella-Woodward monotonicity limiter.  Returns (aL, aR) each [..., n+2].
+
+    Panel edges: grid lines bend where two cube faces meet, so a 4-cell
+    stencil across a panel edge samples a kinked line and the interface value
+    drops to first order there (measured on TC2).  Cells whose stencil crosses
+    a panel edge (lo_edge / hi_edge: bool, broadcastable to q[..., :1], true
+    where the row's low / high end is a panel edge) therefore use the MC-limited
+    PLR faces instead, the usual second-order edge treatment."""
+    def cell(c0, c1):          # cells c0..c1-1
+        return q[..., c0 + g:c1 + g]
+    # interfaces k - 1/2 for k = -1 .. n + 1 (between cells k - 1 and k)
+    a = (7.0 / 12.0) * (cell(-2, n + 1) + cell(-1, n + 2)) - (1.0 / 12.0) * (cell(-3, n) + cell(0, n + 3))
+    aL, aR = a[..., :-1], a[..., 1:]
+    qc = cell(-1, n + 1)
+    flat = (aR - qc) * (qc - aL) <= 0
+    d = aR - aL
+    m6 = 6.0 * (qc - 0.5 * (aL + aR))
+    over_l = d * m6 > d * d
+    over_r = -(d * d) > d * m6
+    aL2 = torch.where(flat, qc, torch.where(over_l, 3.0 * qc - 2.0 * aR, aL))
+    aR2 = torch.where(flat, qc, torch.where(~over_l & over_r, 3.0 * qc - 2.0 * aL, aR))
+    if lo_edge is not None or hi_edge is not None:
+        s = 0.5 * limited_slope(qc - cell(-2, n), cell(0, n + 2) - qc, 2)
+        x = torch.arange(-1, n + 1, device=q.device)
+        near = torch.zeros(q.shape[:-1] + (n + 2,), dtype=torch.bool, device=q.device)
+        if lo_edge is not None:
+            near = near | (lo_edge & (x <= 1))
+        if hi_edge is not None:
+            near = near | (hi_edge & (x >= n - 2))
+        aL2 = torch.where(near, qc - s, aL2)
+        aR2 = torch.where(near, qc + s, aR2)
+    return aL2, aR2
+
+
+def plr_x(qe: torch.Tensor, g: int, n: int, lim: int, pedge: Optional[torch.Tensor] = None):
+    """Left/right PLR (or PPM, lim = 4) states at the n+1 x-edges of the
+    interior rows: returns (qL, qR) each [..., n, n+1].  qe: [..., T, W, W];
+    pedge: [T] panel-edge side bits (RankGeometry.pedge), used by PPM."""
     rows = qe[..., g:g + n, :]
+    if lim == PPM:
+        if g < 3:
+            raise ValueError("PPM reconstruction needs a halo of 3")
+        lo = hi = None
+        if pedge is not None:
+            lo = ((pedge & 1) != 0)[:, None, None]
+            hi = ((pedge & 2) != 0)[:, None, None]
+        aL, aR = ppm_faces(rows, g, n, lo, hi)    # cells -1..n
+        return aR[..., :-1], aL[..., 1:]
     d = rows[..., 1:] - rows[..., :-1]
     s = limited_slope(d[..., g - 2:g + n], d[..., g - 1:g + n + 1], lim)
     c = rows[..., g - 1:g + n + 1]
     return (c + 0.5 * s)[..., :-1], (c - 0.5 * s)[..., 1:]
 
 
-def plr_y(qe: torch.Tensor, g: int, n: int, lim: int):
+def plr_y(qe: torch.Tensor, g: int, n: int, lim: int, pedge: Optional[torch.Tensor] = None):
     """(qL, qR) each [..., n+1, n] at the y-edges of the interior columns."""
-    qL, qR = plr_x(qe.transpose(-1, -2), g, n, lim)
+    pe = None if pedge is None else (pedge >> 2)      # S, N bits -> low, high
+    qL, qR = plr_x(qe.transpose(-1, -2), g, n, lim, pe)
     return qL.transpose(-1, -2), qR.transpose(-1, -2)
 
 

@@ -24,7 +24,7 @@ from typing import Dict
 import numpy as np
 import torch
 
-from .base import Physics, RankGeometry, cells_x, cells_y, plr_x, plr_y
+from .base import Physics, RankGeometry, cells_x, cells_y, plr_x, plr_y, recon_halo
 from .geometry import GRAVITY, OMEGA, CubedSphereGrid
 from . import initial_conditions as ic
 
@@ -33,7 +33,10 @@ class ShallowWater(Physics):
     name = "swe"
     kernel_id = 2
     fields = ["h", "mx", "my", "mz"]
-    halo = 2
+
+    @property
+    def halo(self) -> int:
+        return recon_halo(self.limiter)
 
     def __init__(self, case: str = "tc5", limiter: int = 2, g: float = GRAVITY, omega: float = OMEGA,
                  alpha: float = 0.0):
@@ -94,6 +97,7 @@ class ShallowWater(Physics):
             "cgeo": t(np.concatenate([(1.0 / geo.area)[..., None], geo.center, gb,
                                       np.zeros(geo.area.shape + (1,))], axis=-1)),   # [T,n,n,8]
             "b": t(geo.gather_global(b)),
+            "pedge": torch.as_tensor(geo.pedge, device=device),   # [T] panel-edge side bits (PPM)
         }
 
     def kernel_params(self):
@@ -118,11 +122,11 @@ class ShallowWater(Physics):
         safe = torch.where(h != 0, h, torch.ones_like(h))
         w = torch.stack([h, qe[1] / safe, qe[2] / safe, qe[3] / safe])
         lim = self.limiter
-        wL, wR = plr_x(w, g, n, lim)                                  # [4,T,n,n+1]
+        wL, wR = plr_x(w, g, n, lim, tens.get("pedge"))                                  # [4,T,n,n+1]
         cL, cR = cells_x(w, g, n)
         mx = tens["mx"].permute(1, 0, 2)[:, :, None, :]              # [3,T,1,n+1]
         Fx = self._flux(wL, wR, cL, cR, mx, tens["ex"])
-        wL, wR = plr_y(w, g, n, lim)                                  # [4,T,n+1,n]
+        wL, wR = plr_y(w, g, n, lim, tens.get("pedge"))                                  # [4,T,n+1,n]
         cL, cR = cells_y(w, g, n)
         my = tens["my"].permute(1, 0, 2)[:, :, :, None]              # [3,T,n+1,1]
         Gy = self._flux(wL, wR, cL, cR, my, tens["ey"])

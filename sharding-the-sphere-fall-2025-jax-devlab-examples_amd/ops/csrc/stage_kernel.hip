@@ -156,6 +156,7 @@ struct Args {
   int* epoch;
   int* err;
   long long timeout_ticks;
+  const int* pedge;
 };
 
 #ifdef STSP_STAMPS
@@ -258,7 +259,7 @@ __device__ __forceinline__ void st_state(T* p, T v) {
 template <typename T, int P, int BX, int BY, int LIM, bool REMOTE, bool SYNC, bool XG = false>
 __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   constexpr int F = Phys<P>::F;
-  constexpr int NG = Phys<P>::NG;
+  constexpr int NG = (LIM == 4) ? 3 : Phys<P>::NG;   // PPM reads 3 ghost layers
   constexpr int FL = Phys<P>::FL;              // primitive fields (+ sound speed) in LDS
   constexpr bool RECON = (P != 1);             // PLR reconstruction (not for diffusion)
   constexpr int FC = (P == 2) ? F : 0;         // conserved copy in LDS (SWE only)
@@ -494,6 +495,9 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   // else y-direction, cell (x0 + c, y0 + r - 1), t - NFX = r BX + c.
   if constexpr (RECON) {
     const T* w0 = &s_w[0][0][0];
+    // PPM: tile sides on a cube (panel) edge; cells whose 5-cell stencil
+    // crosses one use MC-limited PLR faces (models/base.py::ppm_faces)
+    const int pe = (LIM == 4) ? a.pedge[tile] : 0;
     for (int t = tid; t < NFT; t += NT) {
       const bool tx = t < NFX;
       const int u = tx ? t : t - NFX;
@@ -506,9 +510,32 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 #pragma unroll
         for (int f = 0; f < F; ++f) {
           const T m1 = w0[f * WF + ci - st], c0 = w0[f * WF + ci], p1 = w0[f * WF + ci + st];
-          const T hs = T(0.5) * slope<LIM>(c0 - m1, p1 - c0);
-          s_fm[f][t] = c0 - hs;
-          s_fp[f][t] = c0 + hs;
+          const int xc = tx ? x : y;                  // cell index along the task direction
+          const bool edge_cell = (LIM == 4) && (((pe & (tx ? 1 : 4)) && xc <= 1) || ((pe & (tx ? 2 : 8)) && xc >= n - 2));
+          if (LIM == 4 && edge_cell) {
+            const T hs = T(0.5) * slope<2>(c0 - m1, p1 - c0);
+            s_fm[f][t] = c0 - hs;
+            s_fp[f][t] = c0 + hs;
+          } else if constexpr (LIM == 4) {
+            // PPM (models/base.py::ppm_faces): 4th-order interface values,
+            // Colella-Woodward monotonicity limiter
+            const T m2 = w0[f * WF + ci - 2 * st], p2 = w0[f * WF + ci + 2 * st];
+            T aL = T(7.0 / 12.0) * (m1 + c0) - T(1.0 / 12.0) * (m2 + p1);
+            T aR = T(7.0 / 12.0) * (c0 + p1) - T(1.0 / 12.0) * (m1 + p2);
+            const bool flat = (aR - c0) * (c0 - aL) <= T(0);
+            const T d = aR - aL;
+            const T m6 = T(6) * (c0 - T(0.5) * (aL + aR));
+            const bool ovl = d * m6 > d * d;
+            const bool ovr = -(d * d) > d * m6;
+            const T nL = flat ? c0 : (ovl ? T(3) * c0 - T(2) * aR : aL);
+            const T nR = flat ? c0 : ((!ovl && ovr) ? T(3) * c0 - T(2) * aL : aR);
+            s_fm[f][t] = nL;
+            s_fp[f][t] = nR;
+          } else {
+            const T hs = T(0.5) * slope<LIM>(c0 - m1, p1 - c0);
+            s_fm[f][t] = c0 - hs;
+            s_fp[f][t] = c0 + hs;
+          }
         }
       }
     }
@@ -798,6 +825,7 @@ Args<T> make_args(const StageDesc* d) {
   a.epoch = d->epoch;
   a.err = d->err;
   a.timeout_ticks = d->timeout_ticks;
+  a.pedge = d->pedge;
   return a;
 }
 
@@ -840,7 +868,7 @@ int launch_l(const StageDesc* d, hipStream_t s) {
 template <typename T, int P, int BX, int BY>
 int launch_t(const StageDesc* d, hipStream_t s) {
   if (d->nblocks <= 0) return 0;
-  if (d->pw != d->n + 2 * d->mg || d->mg < Phys<P>::NG) return -5;
+  if (d->pw != d->n + 2 * d->mg || d->mg < Phys<P>::NG || (d->limiter == 4 && (d->mg < 3 || !d->pedge))) return -5;
   if (!d->push || (d->remote && (!d->gmap || !d->blocks))) return -6;
   if (d->xg && (d->remote || d->blocks || !d->gmap || !d->recv || !d->peer_ring || !d->peer_cnt || !d->cnt ||
                 !d->nprod || !d->bmask || !d->epoch || !d->err || d->ring <= 0))
@@ -851,6 +879,9 @@ int launch_t(const StageDesc* d, hipStream_t s) {
     case 1: return launch_l<T, P, BX, BY, 1>(d, s);
     case 2: return launch_l<T, P, BX, BY, 2>(d, s);
     case 3: return launch_l<T, P, BX, BY, 3>(d, s);
+    case 4:   // PPM: the 3-layer window must fit one cell per thread
+      if constexpr ((BX + 6) * (BY + 6) <= Geom<BX, BY>::NT) return launch_l<T, P, BX, BY, 4>(d, s);
+      else return -11;
   }
   return -7;
 }
@@ -944,6 +975,7 @@ int persist_p(int bx, int by, const StageDesc* st, int nstages, int nsteps, unsi
     case 1: return launch_persist<T, P, 16, 16, 1>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
     case 2: return launch_persist<T, P, 16, 16, 2>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
     case 3: return launch_persist<T, P, 16, 16, 3>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
+    case 4: return launch_persist<T, P, 16, 16, 4>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
   }
   return -7;
 }
@@ -957,6 +989,7 @@ extern "C" int stsp_persistent_launch(int phys, int dtype, int bx, int by, const
   for (int k = 0; k < nstages; ++k) {
     const StageDesc* d = &stages[k];
     if (d->blocks || d->remote || !d->push || d->pw != d->n + 2 * d->mg) return -6;
+    if (d->limiter == 4 && (d->mg < 3 || !d->pedge)) return -5;
     if (d->nblocks != stages[0].nblocks) return -9;
   }
   if (dtype == 1) {

@@ -32,7 +32,7 @@ typedef struct StageDesc {
   int remote;           // 1: read remote ghost slots from recv via gmap (boundary blocks)
   double a0, a1, a2, c0, c1, c2, dt;
   double g, omega2;
-  void* stamps;         // diagnostic builds only (-DSTSP_STAMPS): [nblocks][8] s_memtime per phase
+  void* stamps;         // diagnostic builds only (-DSTSP_STAMPS): [nblocks][16 waves][8] s_memtime per phase
   // ---- direct xGMI halo (xg = 1; see ops/xgmi.py) ----------------------------
   // The producing block stores remote ghost cells straight into the consumer
   // rank's receive ring (IPC-mapped, uncached) and bumps that rank's arrival
@@ -49,6 +49,7 @@ typedef struct StageDesc {
   int* epoch;           // [nblocks] stages completed
   int* err;             // set to 1 on a poll timeout (all later polls fall through)
   long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
+  const int* pedge;     // [T] tile sides on a panel edge (bits W, E, S, N); PPM only
 } StageDesc;
 
 int stsp_stage_launch(int phys, int dtype, int bx, int by, const StageDesc* d, hipStream_t stream);

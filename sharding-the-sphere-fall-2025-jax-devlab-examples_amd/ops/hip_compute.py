@@ -58,6 +58,8 @@ class HipCompute:
         assert phys.halo <= plan.ng
         assert t["invA"].shape == (T, n, n)
         assert t["ex"].shape == (T, n, n + 1) and t["ey"].shape == (T, n + 1, n)
+        if "pedge" in t:
+            assert t["pedge"].dtype == torch.int32 and t["pedge"].shape == (T,)
         if self.phys_id == 2:
             assert t["mx"].shape == (T, 3, n + 1) and t["my"].shape == (T, 3, n + 1)
             assert t["cgeo"].shape == (T, n, n, 8)
@@ -102,6 +104,8 @@ class HipCompute:
         d.ey = p(t["ey"])
         if self.phys_id == 2:
             d.mx, d.my, d.cgeo = p(t["mx"]), p(t["my"]), p(t["cgeo"])
+        if "pedge" in t:
+            d.pedge = p(t["pedge"])
         d.ntile = e.plan.T
         d.n = e.plan.n
         d.S = e.plan.S

@@ -19,6 +19,8 @@ PHYS = {
     "adv": lambda: Advection(limiter=2),
     "adv_minmod": lambda: Advection(limiter=1),
     "diff": lambda: Diffusion(),
+    "swe_ppm": lambda: ShallowWater("tc5", limiter=4),
+    "adv_ppm": lambda: Advection(limiter=4),
 }
 
 
@@ -30,11 +32,11 @@ def _relerr(ref, hip):
     return ((a - b).abs().amax(dim=1) / a.abs().amax(dim=1).clamp_min(1e-30)).max().item()
 
 
-def _pair(name, N, t, dtype, integ="ssprk3", ranks=1):
+def _pair(name, N, t, dtype, integ="ssprk3", ranks=1, block=(16, 16)):
     grid = CubedSphereGrid(N)
-    L = TileLayout(N, t, ranks, ng=2)
+    L = TileLayout(N, t, ranks, ng=PHYS[name]().halo)
     ref = Engine(PHYS[name](), L, grid=grid, dtype=torch.float64, device="cuda", backend="torch", integrator=integ)
-    hip = Engine(PHYS[name](), L, grid=grid, dtype=dtype, device="cuda", backend="hip", integrator=integ)
+    hip = Engine(PHYS[name](), L, grid=grid, dtype=dtype, device="cuda", backend="hip", integrator=integ, block=block)
     hip.dt = ref.dt
     return ref, hip
 
@@ -49,7 +51,17 @@ def test_stage_fp64_matches_reference(name, t):
     assert _relerr(ref, hip) < 1e-11
 
 
-@pytest.mark.parametrize("name", ["swe_tc5", "adv", "diff"])
+@pytest.mark.parametrize("block", [(16, 8), (8, 16), (32, 8)])
+@pytest.mark.parametrize("name", ["swe_ppm", "swe_tc5"])
+def test_block_shapes_match_reference(name, block):
+    ref, hip = _pair(name, 48, 1, torch.float64, block=block)
+    ref.step(3)
+    hip.step(3)
+    torch.cuda.synchronize()
+    assert _relerr(ref, hip) < 1e-11
+
+
+@pytest.mark.parametrize("name", ["swe_tc5", "adv", "diff", "swe_ppm"])
 def test_stage_fp32_close_to_fp64_reference(name):
     ref, hip = _pair(name, 24, 2, torch.float32)
     ref.step(3)
