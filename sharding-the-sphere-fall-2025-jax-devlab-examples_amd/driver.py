@@ -36,7 +36,7 @@ from .models.base import limiter_code
 from .models.diffusion import Diffusion
 from .models.geometry import DAY, EARTH_RADIUS, CubedSphereGrid
 from .models.swe import ShallowWater
-from .parallel.comm import TorchDistTransport
+from .parallel.comm import NativeBuffers, TorchDistTransport
 from .parallel.layout import TileLayout
 from .parallel.mesh import setup_sharding
 from .utils import checkpoint as ckpt
@@ -66,7 +66,10 @@ class Solver:
         self.sharding = None
         self.engines: List[Engine] = []
         self.cluster: Optional[VirtualCluster] = None
-        self.runner: Optional[GraphStepper] = None
+        self.runner = None            # NativeStepper (GPU) once stepping starts
+        self.xgmi = None
+        self._nccl = None
+        self.comm = "local"
         self.mode = None
         self.world, self.rank = 1, 0
 
@@ -97,12 +100,17 @@ class Solver:
                 raise ValueError(f"launched with {self.world} processes but num_devices = {nd}")
             self.mode = "spmd"
             import torch.distributed as dist
-            device = torch.device(f"cuda:{local}") if gpu else torch.device("cpu")
+            # STSP_SHARE_GPU=1: every rank on cuda:0 with a gloo group (functional
+            # rehearsal of the multi-GPU paths on a one-GPU machine)
+            share = os.environ.get("STSP_SHARE_GPU") == "1"
+            device = torch.device(f"cuda:{0 if share else local}") if gpu else torch.device("cpu")
             if gpu:
                 torch.cuda.set_device(device)
             if not dist.is_initialized():
-                dist.init_process_group("nccl" if gpu else "gloo",
-                                        device_id=device if gpu else None)
+                if gpu and not share:
+                    dist.init_process_group("nccl", device_id=device)
+                else:
+                    dist.init_process_group("gloo")
         else:
             self.mode = "single" if nd == 1 else "virtual"
             device = torch.device("cuda:0") if gpu else torch.device("cpu")
@@ -115,9 +123,10 @@ class Solver:
                  "fp32": torch.float32}[c.grid.dtype]
         self.dtype = dtype
         N, t = c.grid.N, c.parallelization.tiles_per_edge
-        self.layout = TileLayout(N, t, nd, ng=c.grid.halo, owner=self.sharding.owner)
-        self.grid = CubedSphereGrid(N, c.grid.radius or EARTH_RADIUS)
         phys0 = make_physics(c.physics)
+        # PPM reads three ghost layers: widen the halo if the config asks for fewer
+        self.layout = TileLayout(N, t, nd, ng=max(c.grid.halo, phys0.halo), owner=self.sharding.owner)
+        self.grid = CubedSphereGrid(N, c.grid.radius or EARTH_RADIUS)
         dt = c.time.dt or (phys0.max_dt(self.grid, c.time.cfl) if c.time.cfl else phys0.max_dt(self.grid))
         kw = dict(grid=self.grid, dtype=dtype, device=device, backend=backend, integrator=c.time.integrator, dt=dt)
         if c.runtime.block:
@@ -126,8 +135,18 @@ class Solver:
             self.cluster = VirtualCluster(lambda: make_physics(c.physics), self.layout, **kw)
             self.engines = list(self.cluster.engines)
         elif self.mode == "spmd":
-            tr = TorchDistTransport(self.layout.plan(self.rank), phys0.F, dtype, device,
-                                    staged=(c.runtime.comm == "staged"))
+            comm = c.runtime.comm
+            if comm == "auto":
+                # GPUs: the native runtime with the direct xGMI exchange
+                comm = "xgmi" if (backend == "hip" and c.runtime.graph and not c.runtime.canary) else "torch"
+            if comm in ("xgmi", "rccl") and backend != "hip":
+                raise ValueError(f"runtime.comm = {comm} needs the HIP backend")
+            self.comm = comm
+            if comm in ("xgmi", "rccl"):
+                tr = NativeBuffers(self.layout.plan(self.rank), phys0.F, dtype, device)
+            else:
+                tr = TorchDistTransport(self.layout.plan(self.rank), phys0.F, dtype, device,
+                                        staged=(comm == "staged"))
             self.engines = [Engine(phys0, self.layout, self.rank, transport=tr, **kw)]
         else:
             self.engines = [Engine(phys0, self.layout, 0, **kw)]
@@ -196,22 +215,45 @@ class Solver:
         return self._allreduce(tot)
 
     def all_finite(self) -> bool:
+        if self.runner is not None:
+            self.runner.check()      # direct xGMI exchange: raises on a halo poll timeout
         ok = float(all(bool(torch.isfinite(e.tiles_view()).all()) for e in self.engines))
         return self._allreduce({"ok": ok}, op="min")["ok"] > 0.5
 
     # ---- stepping ---------------------------------------------------------------
-    def _use_graph(self) -> bool:
+    def _use_native(self) -> bool:
+        """Step through the C++ runtime (ops/native_runtime.py): one GPU with
+        graph replay, or SPMD GPUs with the direct xGMI / RCCL exchange."""
         c = self.cfg.runtime
-        return (self.mode == "single" and self.backend == "hip" and c.graph and not c.canary)
+        if self.backend != "hip" or c.canary:
+            return False
+        if self.mode == "single":
+            return c.graph
+        return self.mode == "spmd" and self.comm in ("xgmi", "rccl")
+
+    def _make_runner(self):
+        from .ops.native_runtime import NativeStepper, create_nccl_comm
+        e = self.engines[0]
+        c = self.cfg.runtime
+        xg = nc = None
+        if self.mode == "spmd" and self.comm == "xgmi":
+            from .ops.xgmi import XgmiHalo
+            xg = XgmiHalo(e)
+        elif self.mode == "spmd" and self.comm == "rccl":
+            if self._nccl is None:
+                self._nccl = create_nccl_comm(self.rank, self.world, self.device.index or 0)
+            nc = self._nccl
+        self.xgmi = xg
+        return NativeStepper(e, nccl_comm=nc, use_graph=c.graph, steps_per_graph=c.steps_per_graph, xgmi=xg)
 
     def step(self, nsteps: int = 1) -> None:
         if nsteps <= 0:
             return
         if self.mode == "virtual":
             self.cluster.step(nsteps)
-        elif self._use_graph():
+        elif self._use_native():
             if self.runner is None:
-                self.runner = GraphStepper(self.engines[0], self.cfg.runtime.steps_per_graph)
+                self.runner = self._make_runner()
             self.runner.run(nsteps)
         else:
             self.engines[0].step(nsteps)
@@ -301,7 +343,8 @@ class Solver:
         self.dt = dt
         for e in self.engines:
             e.dt = dt
-        self.runner = None   # graphs bake dt in; recapture lazily
+        if self.runner is not None:
+            self.runner.set_dt(dt)   # graphs bake dt in: the runner re-records
 
     def _barrier(self) -> None:
         if self.mode == "spmd":
@@ -352,6 +395,8 @@ class Solver:
             e.set_state(torch.as_tensor(loc, dtype=self.dtype))
             e.time = float(meta["time"])
             e.step_count = int(meta["step"])
+        if self.xgmi is not None:
+            self.xgmi.prime()      # remote ghosts of the restored state (collective)
         self.set_dt(float(meta["dt"]))
         self._log(f"Restored {path} (step {meta['step']}, t = {meta['time'] / DAY:.4f} days, "
                   f"written by {meta['num_ranks']} rank(s), tiles_per_edge {meta['tiles_per_edge']})")
