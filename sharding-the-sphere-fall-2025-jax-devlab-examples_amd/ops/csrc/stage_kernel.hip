@@ -262,7 +262,6 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   constexpr int NG = (LIM == 4) ? 3 : Phys<P>::NG;   // PPM reads 3 ghost layers
   constexpr int FL = Phys<P>::FL;              // primitive fields (+ sound speed) in LDS
   constexpr bool RECON = (P != 1);             // PLR reconstruction (not for diffusion)
-  constexpr int FC = (P == 2) ? F : 0;         // conserved copy in LDS (SWE only)
   constexpr int NT = Geom<BX, BY>::NT;
   constexpr int NX = Geom<BX, BY>::NX;
   constexpr int NY = Geom<BX, BY>::NY;
@@ -281,7 +280,6 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   constexpr int NFT = NFX + NFY;               // face tasks
   constexpr bool SW = (P == 2);
   __shared__ T s_w[FL][EY][EX + 1];
-  __shared__ T s_c[FC > 0 ? FC : 1][FC > 0 ? EY : 1][FC > 0 ? EX + 1 : 1];
   __shared__ T s_fm[RECON ? F : 1][RECON ? NFT : 1];   // face value on the cell's minus side
   __shared__ T s_fp[RECON ? F : 1][RECON ? NFT : 1];   // ... and plus side
   __shared__ T s_fl[F][NE];                            // edge fluxes
@@ -310,6 +308,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   const unsigned pc = tb + (unsigned)((cy + mg) * pw + (cx + mg));
   const unsigned gc = (unsigned)(gbase + cy * n + cx);
   T xs[F], acs[F];
+  T qo[P == 2 ? F : 1];   // own conserved state (SWE): from global, not kept in LDS
   T iA = T(0), r0 = T(0), r1 = T(0), r2 = T(0);
   T gb[3] = {T(0), T(0), T(0)};
   int pt[4] = {-1, -1, -1, -1};
@@ -325,6 +324,8 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       for (int f = 0; f < F; ++f) acs[f] = ld_state<SYNC>(o32(a.acc_in + f * S, pc));
     }
     if constexpr (P == 2) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) qo[f] = ld_state<SYNC>(o32(a.Q + f * S, pc));
       T rec[8];
       load_rec8<T>(o32(a.cgeo, gc * 8u), rec);
       iA = rec[0]; r0 = rec[1]; r1 = rec[2]; r2 = rec[3];
@@ -399,9 +400,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   // rows are pair-aligned; remote-boundary blocks load cell by cell (a ghost
   // may come from the receive buffer).
   auto put = [&](int ly, int lx, const T (&v)[F]) {
-    if constexpr (P == 2) {  // keep conserved (h, M); primitive (h, v) + sqrt(g h)
-#pragma unroll
-      for (int f = 0; f < 4; ++f) s_c[f][ly][lx] = v[f];
+    if constexpr (P == 2) {  // primitive (h, v) + sqrt(g h)
       const T inv = v[0] != T(0) ? trcp(v[0]) : T(0);
       s_w[0][ly][lx] = v[0];
       s_w[1][ly][lx] = v[1] * inv;
@@ -583,7 +582,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     T qs[F];
     if constexpr (P == 2) {
 #pragma unroll
-      for (int f = 0; f < 4; ++f) qs[f] = s_c[f][NG + oy][NG + ox];
+      for (int f = 0; f < 4; ++f) qs[f] = qo[f];
     } else {
       qs[0] = s_w[0][NG + oy][NG + ox];
     }
