@@ -55,6 +55,11 @@ def main(argv=None):
         for f in history_frames(a.history, a.field, CubedSphereGrid(N), a.outdir, log=a.log):
             print(f)
         return 0
+    from .utils.config import load_config
+    if a.cmd == "run" and load_config(a.config).physics.model == "planar_swe":
+        from .models.planar import run_panel      # single flat panel, no halos
+        print(json.dumps(run_panel(a.config), default=float))
+        return 0
     from .driver import Solver
     s = Solver(a.config)
     if a.cmd == "info":

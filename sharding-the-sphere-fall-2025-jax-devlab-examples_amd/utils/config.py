@@ -46,7 +46,7 @@ class GridConfig:
 
 @dataclass
 class PhysicsConfig:
-    model: str = "swe"            # swe | advection | diffusion
+    model: str = "swe"            # swe | advection | diffusion | planar_swe (single flat panel)
     case: Optional[str] = None    # tc2 | tc5 | tc6 | rest | cosine_bell | gaussian | lima_flag
     limiter: str = "mc"
     alpha: float = 0.0
@@ -140,4 +140,4 @@ def save_config(cfg: Config, path: str) -> None:
 
 
 def default_case(model: str) -> str:
-    return {"swe": "tc5", "advection": "cosine_bell", "diffusion": "lima_flag"}[model]
+    return {"swe": "tc5", "advection": "cosine_bell", "diffusion": "lima_flag", "planar_swe": "gaussian"}[model]
