@@ -50,7 +50,30 @@ def parse():
                          "kernels (graph-captured; default) or RCCL grouped send/recv (eager)")
     ap.add_argument("--partition", default="auto")
     ap.add_argument("--dt", type=float, default=None)
+    ap.add_argument("--no-verify", action="store_true",
+                    help="N > 1: skip the bitwise comparison with a one-GPU run after timing")
     return ap.parse_args()
+
+
+def verify_single(a, phys, grid, dtype, device, dt, layout, tiles_by_rank, runtime, backend):
+    """Max |difference| between the gathered multi-rank state and one rank
+    stepping the same warmup + steps on this GPU (0.0 = bitwise equal)."""
+    import numpy as np
+    from stsphere.engine import Engine, assemble_global
+    from stsphere.parallel.layout import TileLayout
+    L1 = TileLayout(a.N, a.tiles_per_edge, 1, ng=layout.ng)
+    ref = Engine(phys, L1, 0, grid=grid, dtype=dtype, device=device, backend=backend, integrator=a.integrator, dt=dt)
+    total = a.warmup + a.steps
+    if runtime == "native" and backend == "hip":
+        from stsphere.ops.native_runtime import NativeStepper
+        r = NativeStepper(ref, use_graph=True, steps_per_graph=a.steps_per_graph)
+        r.run(total)
+    else:
+        ref.step(total)
+    F = phys.F
+    got = np.stack([assemble_global(layout, {r: t[f] for r, t in enumerate(tiles_by_rank)}) for f in range(F)])
+    want = np.stack([ref.global_field(f) for f in range(F)])
+    return float(np.abs(got - want).max())
 
 
 def main():
@@ -183,6 +206,15 @@ def main():
         dist.all_reduce(t)
         diag["mass"] = float(t.item())
     finite = bool(torch.isfinite(eng.tiles_view()).all().item())
+    verified = None
+    if world > 1 and not a.no_verify:
+        # the multi-GPU result must equal a one-GPU run of the same steps bit for
+        # bit (same kernels, same arithmetic); rank 0 re-runs it after timing
+        tiles = eng.tiles_view().detach().cpu().numpy()
+        allt = [None] * world
+        dist.all_gather_object(allt, tiles)
+        if rank == 0:
+            verified = verify_single(a, phys, grid, dtype, device, eng.dt, layout, allt, runtime, backend)
     cells = 6 * a.N * a.N
     cups = cells * a.steps / elapsed
     sdpd = (a.steps * eng.dt / DAY) / (elapsed / DAY)
@@ -215,6 +247,7 @@ def main():
             },
             "simulated_days_per_day": sdpd,
             "finite": finite,
+            "max_abs_diff_vs_1gpu": verified,
             "mass": diag.get("mass"),
         }
         print(json.dumps(out), flush=True)

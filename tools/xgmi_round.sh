@@ -17,7 +17,7 @@ for n in ${RANKS:-2 4 8}; do
   STSP_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
       --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n --steps 30 --warmup 5 \
       ${BENCH_ARGS:-} > $OUT/rehearse_$n.log 2>&1
-  rc=$?; grep -h '^{' $OUT/rehearse_$n.log | cut -c1-400; grep -h "\[bench\]" $OUT/rehearse_$n.log | head -5
+  rc=$?; grep -h "^{" $OUT/rehearse_$n.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d[\"n_gpus\"], d[\"config\"][\"comm\"], d[\"ms_per_step\"], \"diff_vs_1gpu\", d[\"max_abs_diff_vs_1gpu\"], d[\"finite\"])"; grep -h "\[bench\]" $OUT/rehearse_$n.log | head -5
   if [ $rc -ne 0 ]; then echo "rehearsal rc=$rc"; tail -20 $OUT/rehearse_$n.log; exit $rc; fi
 done
 echo "== done"
