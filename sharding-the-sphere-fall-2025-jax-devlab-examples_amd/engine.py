@@ -63,7 +63,7 @@ class TorchCompute:
 class Engine:
     def __init__(self, physics: Physics, layout: TileLayout, rank: int = 0, grid: Optional[CubedSphereGrid] = None,
                  dtype=torch.float64, device="cpu", transport: Optional[Transport] = None, backend: str = "torch",
-                 integrator: str = "ssprk3", dt: Optional[float] = None, cfl: Optional[float] = None, block=(16, 16)):
+                 integrator: str = "ssprk3", dt: Optional[float] = None, cfl: Optional[float] = None, block=None):
         if physics.halo > layout.ng:
             raise ValueError(f"{physics.name} needs halo {physics.halo} > layout ng {layout.ng}")
         self.physics = physics
@@ -88,7 +88,7 @@ class Engine:
         self.time = 0.0
         self.step_count = 0
         self.backend = backend
-        self.block = tuple(block)
+        self.block = tuple(block) if block is not None else None   # None: ops.hip_compute.choose_block
         if backend == "torch":
             self.compute = TorchCompute(self)
         elif backend == "hip":

@@ -18,16 +18,39 @@ from ..models.integrators import Stage
 BLOCK_SHAPES = ((16, 16), (32, 8), (16, 8), (8, 16), (8, 8))
 
 
-def choose_block(n: int):
-    """Pick the block shape with the least padding waste (ties -> 16x16)."""
-    best, waste = (16, 16), None
+def choose_block(n: int, tiles: int = 0, cus: int = 0):
+    """Block shape for a rank holding ``tiles`` tiles of ``n x n`` cells.
+
+    A block's critical path (about 9k cycles for 16x16 fp64 SWE) is set by
+    its memory round trips plus its VALU issue, and the issue part scales with
+    the waves a block puts on each SIMD.  So when a smaller block still fits
+    the whole grid in one pass over the ``cus`` compute units, the smaller
+    block wins: measured at C96 / t=2 (tools/small_grid_probe.sh,
+    profiles/r1_small_grid_block_shapes.txt), 3 tiles of 48^2 per rank take
+    5.12 us per stage with 16x16 and 4.16 us with 8x8; 12 tiles take 5.38 us
+    with 16x16 and 4.62 us with 16x8.  With more blocks than CUs the larger
+    block is better (24 tiles: 16x16 5.37 us, 8x8 5.66 us), and among the
+    256-cell shapes the one with the least padding waste is taken (ties ->
+    16x16).
+    """
+    def count(bx, by):
+        return tiles * -(-n // bx) * -(-n // by)
+
+    def waste(bx, by):
+        return -(-n // bx) * -(-n // by) * bx * by - n * n
+
+    if tiles and cus:
+        fits = [(bx * by, waste(bx, by), count(bx, by), (bx, by)) for bx, by in BLOCK_SHAPES
+                if count(bx, by) <= cus and bx * by < 256]
+        if fits and count(16, 16) <= cus:
+            return min(fits)[3]
+    best, w0 = (16, 16), None
     for bx, by in BLOCK_SHAPES:
         if bx * by != 256:
             continue
-        nbx, nby = -(-n // bx), -(-n // by)
-        w = nbx * nby * bx * by - n * n
-        if waste is None or w < waste:
-            best, waste = (bx, by), w
+        w = waste(bx, by)
+        if w0 is None or w < w0:
+            best, w0 = (bx, by), w
     return best
 
 
@@ -43,7 +66,11 @@ class HipCompute:
         self.phys_id = phys.kernel_id
         self.dcode = native.dtype_code(e.dtype)
         n, T = plan.n, plan.T
-        bx, by = e.block if e.block != (16, 16) else choose_block(n)
+        if e.block is None:
+            cus = torch.cuda.get_device_properties(e.device).multi_processor_count
+            bx, by = choose_block(n, T, cus)
+        else:
+            bx, by = e.block
         if (bx, by) not in BLOCK_SHAPES:
             raise ValueError(f"unsupported block shape {(bx, by)}")
         self.bx, self.by = bx, by

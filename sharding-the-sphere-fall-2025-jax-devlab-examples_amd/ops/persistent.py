@@ -84,7 +84,12 @@ class PersistentStepper:
         if hc.remote:
             raise RuntimeError("persistent stepping is single-rank (no remote halos)")
         if (hc.bx, hc.by) != (self.BX, self.BY):
-            raise RuntimeError("persistent stepping uses 16x16 blocks")
+            if e.block is not None:
+                raise RuntimeError("persistent stepping uses 16x16 blocks")
+            # the engine picked a smaller block for a small grid: rebuild its
+            # stage tables for the persistent kernel's fixed 16x16 shape
+            e.block = (self.BX, self.BY)
+            e.compute = hc = HipCompute(e)
         if not persistent_safe(e.integ):
             raise RuntimeError(f"integrator {e.integ.name} is not race-free with a one-stage neighbour lag")
         props = torch.cuda.get_device_properties(e.device)
