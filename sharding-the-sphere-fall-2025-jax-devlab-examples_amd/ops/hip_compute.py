@@ -18,7 +18,17 @@ from ..models.integrators import Stage
 BLOCK_SHAPES = ((16, 16), (32, 8), (16, 8), (8, 16), (8, 8))
 
 
-def choose_block(n: int, tiles: int = 0, cus: int = 0):
+def block_threads(bx: int, by: int) -> int:
+    """Threads of a stage block: one per x- and y-edge, rounded to wave64."""
+    return ((bx + 1) * by + bx * (by + 1) + 63) // 64 * 64
+
+
+def block_supports(bx: int, by: int, limiter: int) -> bool:
+    """PPM (limiter 4) loads its 3-layer window one cell per thread."""
+    return limiter != 4 or (bx + 6) * (by + 6) <= block_threads(bx, by)
+
+
+def choose_block(n: int, tiles: int = 0, cus: int = 0, limiter: int = 0):
     """Block shape for a rank holding ``tiles`` tiles of ``n x n`` cells.
 
     A block's critical path (about 9k cycles for 16x16 fp64 SWE) is set by
@@ -31,7 +41,7 @@ def choose_block(n: int, tiles: int = 0, cus: int = 0):
     with 16x16 and 4.62 us with 16x8.  With more blocks than CUs the larger
     block is better (24 tiles: 16x16 5.37 us, 8x8 5.66 us), and among the
     256-cell shapes the one with the least padding waste is taken (ties ->
-    16x16).
+    16x16).  Shapes that cannot run ``limiter`` (8x8 with PPM) are skipped.
     """
     def count(bx, by):
         return tiles * -(-n // bx) * -(-n // by)
@@ -40,10 +50,10 @@ def choose_block(n: int, tiles: int = 0, cus: int = 0):
         return -(-n // bx) * -(-n // by) * bx * by - n * n
 
     if tiles and cus:
-        fits = [(bx * by, waste(bx, by), count(bx, by), (bx, by)) for bx, by in BLOCK_SHAPES
-                if count(bx, by) <= cus and bx * by < 256]
+        fits = [(bx * by, waste(bx, by), count(bx, by), -bx, (bx, by)) for bx, by in BLOCK_SHAPES
+                if count(bx, by) <= cus and bx * by < 256 and block_supports(bx, by, limiter)]
         if fits and count(16, 16) <= cus:
-            return min(fits)[3]
+            return min(fits)[-1]   # ties: the wider (contiguous-row) block
     best, w0 = (16, 16), None
     for bx, by in BLOCK_SHAPES:
         if bx * by != 256:
@@ -68,7 +78,7 @@ class HipCompute:
         n, T = plan.n, plan.T
         if e.block is None:
             cus = torch.cuda.get_device_properties(e.device).multi_processor_count
-            bx, by = choose_block(n, T, cus)
+            bx, by = choose_block(n, T, cus, getattr(phys, "limiter", 0))
         else:
             bx, by = e.block
         if (bx, by) not in BLOCK_SHAPES:

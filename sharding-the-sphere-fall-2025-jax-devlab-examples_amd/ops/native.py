@@ -70,6 +70,7 @@ def load(build_if_missing: bool = True):
         L.stsp_copy_index_launch.argtypes = [ci, vp, vp, vp, vp, ci, ci, cl, cl, vp]
         L.stsp_copy_index_launch.restype = ci
         _declare_runtime(L)
+        _declare_tt(L)
         _LIB = L
         return L
 
@@ -96,6 +97,20 @@ def _declare_runtime(L):
     L.stsp_roctx_push.restype = ci
     L.stsp_roctx_pop.argtypes = []
     L.stsp_roctx_pop.restype = ci
+
+
+def _declare_tt(L):
+    vp, ci, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    L.stsp_tt_gram_blocks.argtypes = [ci]
+    L.stsp_tt_gram_blocks.restype = ci
+    L.stsp_tt_gram.argtypes = [ci, vp, ci, vp, ci, ci, ci, ci, vp, ci, vp, ci, cd, vp]
+    L.stsp_tt_gram.restype = ci
+    L.stsp_tt_mm.argtypes = [ci, vp, ci, vp, ci, vp, ci, ci, ci, ci, cd, cd, vp]
+    L.stsp_tt_mm.restype = ci
+    L.stsp_tt_expand.argtypes = [ci, vp, ci, vp, ci, ci, ci, cd, cd, cd, cd, cd, ci, vp]
+    L.stsp_tt_expand.restype = ci
+    L.stsp_tt_dense_diffusion.argtypes = [ci, vp, vp, ci, ci, cd, vp]
+    L.stsp_tt_dense_diffusion.restype = ci
 
 
 def available() -> bool:

@@ -1,0 +1,111 @@
+"""PyTorch-facing wrappers of the gfx950 low-rank kernels (ops/csrc/tt_kernels.hip).
+
+* ``gram(A, B)``            A^T B for tall-skinny A [N, k], B [N, m] (k, m <= 64), MFMA
+* ``tsmm(A, X, out=...)``   A X (+ beta out) for A [N, k], X [k, m], MFMA
+* ``expand(X, ...)``        [x0 X + x1 D X, y0 X + y1 D X] with D the 1-D second difference
+* ``dense_diffusion(U, c)`` U + c * (5-point Laplacian of U), zero Dirichlet
+
+All of them run on torch's current stream.  Operands must be CUDA tensors of
+one dtype (float64 or float32) whose rows are contiguous (stride(1) == 1); row
+strides are passed through, so column slices of a wider matrix work.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import native
+
+
+def _check(*ts):
+    dt = ts[0].dtype
+    for t in ts:
+        if t.device.type != "cuda":
+            raise ValueError("tt_ops need CUDA tensors")
+        if t.dtype != dt:
+            raise TypeError("operands must share one dtype")
+        if t.dim() != 2 or t.stride(1) != 1:
+            raise ValueError("operands must be 2-D with contiguous rows")
+    return native.dtype_code(dt)
+
+
+def gram_blocks(N: int) -> int:
+    return native.require_native().stsp_tt_gram_blocks(int(N))
+
+
+def _ceil16(x: int) -> int:
+    return (x + 15) // 16 * 16
+
+
+def gram(A: torch.Tensor, B: torch.Tensor, alpha: float = 1.0, out: torch.Tensor = None,
+         work: torch.Tensor = None) -> torch.Tensor:
+    """alpha * A^T B  ([k, m]); the reduction over rows runs in a fixed order
+    (bitwise reproducible)."""
+    L = native.require_native()
+    code = _check(A, B)
+    N, k = A.shape
+    N2, m = B.shape
+    if N2 != N or not (1 <= k <= 64 and 1 <= m <= 64):
+        raise ValueError(f"gram: shapes {tuple(A.shape)} / {tuple(B.shape)}")
+    if out is None:
+        out = torch.empty((k, m), dtype=A.dtype, device=A.device)
+    _check(out)
+    P = L.stsp_tt_gram_blocks(N)
+    need = P * _ceil16(k) * _ceil16(m)
+    if work is None or work.numel() < need or work.dtype != A.dtype:
+        work = torch.empty(need, dtype=A.dtype, device=A.device)
+    rc = L.stsp_tt_gram(code, native.ptr(A), A.stride(0), native.ptr(B), B.stride(0), N, k, m, native.ptr(work), P,
+                        native.ptr(out), out.stride(0), float(alpha), native.current_stream_handle())
+    native.check(rc, "tt_gram")
+    return out
+
+
+def tsmm(A: torch.Tensor, X: torch.Tensor, out: torch.Tensor = None, alpha: float = 1.0,
+         beta: float = 0.0) -> torch.Tensor:
+    """alpha * A X + beta * out  ([N, m])."""
+    L = native.require_native()
+    N, k = A.shape
+    k2, m = X.shape
+    if k2 != k or not (1 <= k <= 64 and 1 <= m <= 64):
+        raise ValueError(f"tsmm: shapes {tuple(A.shape)} x {tuple(X.shape)}")
+    if out is None:
+        if beta != 0.0:
+            raise ValueError("beta != 0 needs out")
+        out = torch.empty((N, m), dtype=A.dtype, device=A.device)
+    code = _check(A, X, out)
+    if out.shape != (N, m):
+        raise ValueError("tsmm: bad out shape")
+    rc = L.stsp_tt_mm(code, native.ptr(A), A.stride(0), native.ptr(X), X.stride(0), native.ptr(out), out.stride(0),
+                      N, k, m, float(alpha), float(beta), native.current_stream_handle())
+    native.check(rc, "tt_mm")
+    return out
+
+
+def expand(X: torch.Tensor, x0: float, x1: float, y0: float, y1: float, ih2: float, periodic: bool = False,
+           out: torch.Tensor = None) -> torch.Tensor:
+    """[N, 2r] = [x0 X + x1 D X, y0 X + y1 D X], (D X)_i = (X_{i-1} - 2 X_i + X_{i+1}) ih2."""
+    L = native.require_native()
+    N, r = X.shape
+    if out is None:
+        out = torch.empty((N, 2 * r), dtype=X.dtype, device=X.device)
+    code = _check(X, out)
+    if out.shape[0] != N or out.shape[1] < 2 * r:
+        raise ValueError("expand: bad out shape")
+    rc = L.stsp_tt_expand(code, native.ptr(X), X.stride(0), native.ptr(out), out.stride(0), N, r, x0, x1, y0, y1, ih2,
+                          int(periodic), native.current_stream_handle())
+    native.check(rc, "tt_expand")
+    return out
+
+
+def dense_diffusion(U: torch.Tensor, c: float, out: torch.Tensor = None) -> torch.Tensor:
+    """U + c (U_{i-1,j} + U_{i+1,j} + U_{i,j-1} + U_{i,j+1} - 4 U_ij), zero outside."""
+    L = native.require_native()
+    if not U.is_contiguous():
+        raise ValueError("dense_diffusion: U must be contiguous")
+    if out is None:
+        out = torch.empty_like(U)
+    code = _check(U, out)
+    N, M = U.shape
+    rc = L.stsp_tt_dense_diffusion(code, native.ptr(U), native.ptr(out), N, M, float(c),
+                                   native.current_stream_handle())
+    native.check(rc, "tt_dense_diffusion")
+    return out

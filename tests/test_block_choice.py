@@ -1,0 +1,25 @@
+"""Stage block-shape choice (ops/hip_compute.choose_block), CPU only."""
+from stsphere.ops.hip_compute import BLOCK_SHAPES, block_supports, choose_block
+
+
+def test_full_c96_grid_keeps_16x16():
+    assert choose_block(48, 24, 256, 2) == (16, 16)      # 216 blocks: one pass over 256 CUs
+
+
+def test_small_rank_grids_take_smaller_blocks():
+    # profiles/r1_small_grid_block_shapes.txt: 12 tiles -> 16x8, 6 / 3 tiles -> 8x8
+    assert choose_block(48, 12, 256, 2) == (16, 8)
+    assert choose_block(48, 6, 256, 2) == (8, 8)
+    assert choose_block(48, 3, 256, 2) == (8, 8)
+
+
+def test_ppm_never_gets_a_block_too_small_for_its_window():
+    assert not block_supports(8, 8, 4) and block_supports(16, 8, 4)
+    for n, t in ((48, 3), (48, 6), (12, 24), (24, 6)):
+        bx, by = choose_block(n, t, 256, 4)
+        assert block_supports(bx, by, 4) and (bx, by) in BLOCK_SHAPES
+
+
+def test_without_device_info_falls_back_to_least_waste():
+    assert choose_block(48) == (16, 16)
+    assert choose_block(40) in ((16, 16), (32, 8))

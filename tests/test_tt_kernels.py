@@ -1,0 +1,123 @@
+"""Low-rank (d = 2 TT) kernels: MFMA Gram / tall-skinny products, the factor
+expansion and the dense five-point step, each against a plain PyTorch fp64
+reference of the same op; the factored diffusion step against dense stepping.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from stsphere.models import tt
+
+
+def _panel(N, dtype=torch.float64, device="cpu"):
+    x = torch.linspace(0, 1, N + 2, dtype=torch.float64)[1:-1]
+    U = torch.sin(math.pi * x)[:, None] * torch.sin(2 * math.pi * x)[None, :] + \
+        0.3 * torch.sin(3 * math.pi * x)[:, None] * torch.sin(math.pi * x)[None, :] + \
+        0.05 * torch.exp(-40 * ((x[:, None] - 0.3) ** 2 + (x[None, :] - 0.6) ** 2))
+    return U.to(dtype=dtype, device=device)
+
+
+def test_gram_core_recompression_matches_qr_path_cpu():
+    """The Gram/eigen route of the hip step, evaluated with torch on the CPU,
+    gives the same rank-2r recompression as the QR route."""
+    N = 96
+    s = tt.LowRankDiffusion(N, kappa=1.0, eps=1e-9, max_rank=24)
+    lr = tt.LowRankField.from_dense(_panel(N), eps=1e-12)
+    c = 0.5 * s.dt_max
+    D = tt.second_difference(N, s.h)
+    Ah = torch.cat([lr.A, c * (D @ lr.A)], 1)
+    Bh = torch.cat([lr.B + c * (D @ lr.B), lr.B], 1)
+    Xa, Xb = s._core(torch.stack([Ah.T @ Ah, Bh.T @ Bh]).numpy())
+    got = (Ah @ torch.from_numpy(Xa)) @ (Bh @ torch.from_numpy(Xb)).T
+    want = s.step(lr, c).dense()
+    assert float((got - want).norm() / want.norm()) < 1e-8
+    dense = s.dense_step(lr.dense(), c)
+    assert float((got - dense).norm() / dense.norm()) < 1e-8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("N,k,m", [(1, 1, 1), (7, 3, 5), (1000, 16, 16), (4099, 20, 37), (20000, 48, 48),
+                                   (513, 64, 64), (300, 33, 17)])
+def test_gram_matches_torch(N, k, m, dtype):
+    from stsphere.ops import tt_ops
+    g = torch.Generator().manual_seed(N + k + m)
+    A = torch.randn(N, k + 3, generator=g, dtype=torch.float64)[:, 1:k + 1]   # strided rows
+    B = torch.randn(N, m, generator=g, dtype=torch.float64)
+    want = A.T @ B
+    got = tt_ops.gram(A.to(dtype).cuda(), B.to(dtype).cuda(), alpha=0.5).double().cpu()
+    tol = 1e-12 if dtype == torch.float64 else 2e-5
+    scale = A.abs().T.matmul(B.abs()).clamp_min(1e-30)
+    assert float(((got - 0.5 * want).abs() / scale).max()) < tol
+
+
+@pytest.mark.gpu
+def test_gram_is_bitwise_reproducible():
+    from stsphere.ops import tt_ops
+    A = torch.randn(123457, 40, dtype=torch.float64, device="cuda")
+    a = tt_ops.gram(A, A)
+    b = tt_ops.gram(A, A)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("N,k,m", [(1, 1, 1), (65, 3, 5), (1000, 16, 16), (4099, 40, 20), (513, 64, 64),
+                                   (300, 33, 17)])
+def test_tsmm_matches_torch(N, k, m, dtype):
+    from stsphere.ops import tt_ops
+    g = torch.Generator().manual_seed(7 * N + k + m)
+    A = torch.randn(N, k, generator=g, dtype=torch.float64)
+    X = torch.randn(k + 2, m, generator=g, dtype=torch.float64)[1:k + 1]
+    C0 = torch.randn(N, m + 4, generator=g, dtype=torch.float64)
+    want = 2.0 * A @ X - 0.5 * C0[:, 2:m + 2]
+    Cd = C0.to(dtype).cuda()
+    tt_ops.tsmm(A.to(dtype).cuda(), X.to(dtype).cuda(), out=Cd[:, 2:m + 2], alpha=2.0, beta=-0.5)
+    got = Cd.double().cpu()
+    tol = 1e-12 if dtype == torch.float64 else 2e-5
+    scale = (2 * A.abs() @ X.abs() + 0.5 * C0[:, 2:m + 2].abs()).clamp_min(1e-30)
+    assert float(((got[:, 2:m + 2] - want).abs() / scale).max()) < tol
+    assert torch.equal(got[:, :2], C0[:, :2].to(dtype).double())          # untouched columns
+    assert torch.equal(got[:, m + 2:], C0[:, m + 2:].to(dtype).double())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bc", ["dirichlet", "periodic"])
+def test_expand_matches_torch(bc):
+    from stsphere.ops import tt_ops
+    N, r = 257, 9
+    X = torch.randn(N, r, dtype=torch.float64)
+    D = tt.second_difference(N, 0.1, bc)
+    want = torch.cat([1.5 * X + 0.25 * (D @ X), -X + 2.0 * (D @ X)], 1)
+    got = tt_ops.expand(X.cuda(), 1.5, 0.25, -1.0, 2.0, 100.0, bc == "periodic").cpu()
+    assert torch.allclose(got, want, rtol=1e-13, atol=1e-11)
+
+
+@pytest.mark.gpu
+def test_dense_diffusion_matches_torch():
+    from stsphere.ops import tt_ops
+    U = torch.randn(130, 75, dtype=torch.float64)
+    P = torch.nn.functional.pad(U, (1, 1, 1, 1))
+    lap = P[:-2, 1:-1] + P[2:, 1:-1] + P[1:-1, :-2] + P[1:-1, 2:] - 4 * U
+    got = tt_ops.dense_diffusion(U.cuda(), 0.2).cpu()
+    assert torch.allclose(got, U + 0.2 * lap, rtol=1e-14, atol=1e-14)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bc", ["dirichlet", "periodic"])
+def test_low_rank_diffusion_hip_matches_dense(bc):
+    N = 512
+    s = tt.LowRankDiffusion(N, kappa=1.0, bc=bc, eps=1e-9, max_rank=24, backend="hip")
+    U = _panel(N)
+    ref = tt.LowRankDiffusion(N, kappa=1.0, bc=bc, eps=1e-9, max_rank=24)
+    lr = tt.LowRankField.from_dense(U.cuda(), eps=1e-12)
+    dt = 0.5 * s.dt_max
+    dense = U.clone()
+    for _ in range(30):
+        lr = s.step(lr, dt)
+        dense = ref.dense_step(dense, dt)
+    got = lr.dense().cpu()
+    assert lr.rank <= 24
+    assert float((got - dense).norm() / dense.norm()) < 1e-7
