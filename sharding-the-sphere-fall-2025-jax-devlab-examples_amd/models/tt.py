@@ -242,51 +242,38 @@ class LowRankDiffusion:
     def _step_hip(self, U: LowRankField, dt: float) -> LowRankField:
         """Same update as ``step`` with the rank-2r form
         U + c (D U + U D^T) = [A, c D A] [B + c D B, B]^T, recompressed through
-        the Gram matrices (MFMA) and a host eigen/SVD of the 2r x 2r core:
+        the Gram matrices (MFMA) and the 2r x 2r core:
         A^ = Qa Ra with Ra = sqrt(La) Va^T from Ga = Va La Va^T (eigenvalues
         below 1e-13 max dropped: exact rank deficiency is fine), then
         Ra Rb^T = W S Z^T and A' = A^ Va La^-1/2 W_r S_r, B' = B^ Vb Lb^-1/2 Z_r.
-        Going through Gram matrices squares the conditioning, so the
-        attainable relative accuracy is ~sqrt(machine eps) (1e-8 in fp64)."""
-        from ..ops import tt_ops
-        c = dt * self.kappa
+        The whole step is one native call (ops/csrc/tt_kernels.hip,
+        stsp_tt_lr_step: 6 kernels, one stream sync for the k x k Gram
+        matrices, the core on the host in C++ Jacobi).  Going through Gram
+        matrices squares the conditioning, so the attainable relative accuracy
+        is ~sqrt(machine eps) (1e-8 in fp64)."""
+        from ..ops import native
+        L = native.require_native()
         N, r = U.A.shape
         if 2 * r > 64:
             raise ValueError(f"hip low-rank step supports rank <= 32 (got {r})")
-        ih2 = 1.0 / (self.h * self.h)
-        per = self.bc == "periodic"
-        A = U.A.contiguous()
-        B = U.B.contiguous()
-        Ah = tt_ops.expand(A, 1.0, 0.0, 0.0, c, ih2, per)     # [A, c D A]
-        Bh = tt_ops.expand(B, 1.0, c, 1.0, 0.0, ih2, per)     # [B + c D B, B]
-        k = 2 * r
-        G = torch.empty((2, k, k), dtype=A.dtype, device=A.device)
-        tt_ops.gram(Ah, Ah, out=G[0])
-        tt_ops.gram(Bh, Bh, out=G[1])
-        hG, hX = self._host_buffers(k, A.dtype)
-        hG.copy_(G, non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-        Xa, Xb = self._core(hG.numpy().astype(np.float64, copy=False))
-        rn = Xa.shape[1]
-        hX[:, :rn] = torch.from_numpy(Xa)
-        hX[:, rn:2 * rn] = torch.from_numpy(Xb)
-        X = hX[:, :2 * rn].to(A.device, non_blocking=True)
-        # hX is reused next step: order its next overwrite after this copy
-        self._copy_done = torch.cuda.Event()
-        self._copy_done.record()
-        return LowRankField(tt_ops.tsmm(Ah, X[:, :rn]), tt_ops.tsmm(Bh, X[:, rn:]))
-
-    def _host_buffers(self, k: int, dtype):
-        """Pinned staging for the k x k Gram matrices and the k x 2r' core maps."""
-        key = (k, dtype)
-        if getattr(self, "_hkey", None) != key:
-            self._hG = torch.empty((2, k, k), dtype=dtype).pin_memory()
-            self._hX = torch.empty((k, 2 * k), dtype=dtype).pin_memory()
-            self._hkey = key
-            self._copy_done = None
-        if self._copy_done is not None:
-            self._copy_done.synchronize()
-        return self._hG, self._hX
+        A = U.A if U.A.stride(1) == 1 else U.A.contiguous()
+        B = U.B if U.B.stride(1) == 1 else U.B.contiguous()
+        dev, dt_ = A.device, A.dtype
+        key = (N, r, dt_, dev)
+        if getattr(self, "_wkey", None) != key:
+            self._ws = torch.empty(L.stsp_tt_step_workspace(N, r), dtype=dt_, device=dev)
+            self._hbuf = torch.empty(4 * (2 * r) ** 2, dtype=torch.float64).pin_memory()
+            self._wkey = key
+        rmax = 2 * r if self.max_rank is None else min(2 * r, self.max_rank)
+        out = torch.empty((2, N, rmax), dtype=dt_, device=dev)
+        rn = L.stsp_tt_lr_step(native.dtype_code(dt_), native.ptr(A), A.stride(0), native.ptr(B), B.stride(0), N, r,
+                               dt * self.kappa,
+                               1.0 / (self.h * self.h), int(self.bc == "periodic"), self.eps,
+                               self.max_rank or 0, native.ptr(self._ws), native.ptr(self._hbuf),
+                               native.ptr(out[0]), native.ptr(out[1]), rmax, native.current_stream_handle())
+        if rn <= 0:
+            raise RuntimeError(f"stsp_tt_lr_step failed ({rn})")
+        return LowRankField(out[0, :, :rn], out[1, :, :rn])
 
     def _core(self, G: np.ndarray):
         def half(g):

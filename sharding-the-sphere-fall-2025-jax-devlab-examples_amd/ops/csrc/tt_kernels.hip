@@ -26,6 +26,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
 namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -291,6 +295,166 @@ int tsmm_t(const void* A, int lda, const void* X, int ldx, void* C, int ldc, int
   return -2;
 }
 
+// ---------------------------------------------------------------------------
+// Host side of the factored step: the 2r x 2r "core" (microseconds of scalar
+// work; a BLAS call or a Python round trip costs more than the arithmetic).
+// ---------------------------------------------------------------------------
+
+// Cyclic Jacobi eigen-decomposition of the symmetric n x n matrix a (row-major,
+// destroyed): eigenvalues w[j], eigenvectors in the columns of v.
+void jacobi_eigh(int n, double* a, double* w, double* v) {
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) v[i * n + j] = i == j ? 1.0 : 0.0;
+  double nrm = 0;
+  for (int i = 0; i < n * n; ++i) nrm += a[i] * a[i];
+  // entries below 1e-15 |a|_F only move eigenvalues far under the 1e-13 max
+  // cut of gram_factor; rotating them would chase rounding noise forever
+  const double tiny = 1e-15 * std::sqrt(nrm);
+  for (int sweep = 0; sweep < 64; ++sweep) {
+    bool rotated = false;
+    for (int p = 0; p < n; ++p)
+      for (int q = p + 1; q < n; ++q) {
+        const double apq = a[p * n + q];
+        if (std::fabs(apq) <= tiny ||
+            std::fabs(apq) <= 1e-16 * std::sqrt(std::fabs(a[p * n + p] * a[q * n + q]))) {
+          a[p * n + q] = a[q * n + p] = 0.0;
+          continue;
+        }
+        rotated = true;
+        const double th = (a[q * n + q] - a[p * n + p]) / (2.0 * apq);
+        const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1.0));
+        const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < n; ++k) {
+          const double kp = a[k * n + p], kq = a[k * n + q];
+          a[k * n + p] = c * kp - s * kq;
+          a[k * n + q] = s * kp + c * kq;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double pk = a[p * n + k], qk = a[q * n + k];
+          a[p * n + k] = c * pk - s * qk;
+          a[q * n + k] = s * pk + c * qk;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double kp = v[k * n + p], kq = v[k * n + q];
+          v[k * n + p] = c * kp - s * kq;
+          v[k * n + q] = s * kp + c * kq;
+        }
+      }
+    if (!rotated) break;
+  }
+  for (int i = 0; i < n; ++i) w[i] = a[i * n + i];
+}
+
+// One-sided (Hestenes) Jacobi SVD of m (rows x cols, row-major, overwritten by
+// U Sigma): on return the columns of m are mutually orthogonal, sig[j] = |col j|
+// and m = (m_out) W^T with W (cols x cols) in w.
+void jacobi_svd(int rows, int cols, double* m, double* sig, double* w) {
+  for (int i = 0; i < cols; ++i)
+    for (int j = 0; j < cols; ++j) w[i * cols + j] = i == j ? 1.0 : 0.0;
+  double tot = 0;
+  for (int i = 0; i < rows * cols; ++i) tot += m[i] * m[i];
+  const double tiny = 1e-30 * tot;   // columns this small are rounding noise
+  for (int sweep = 0; sweep < 64; ++sweep) {
+    bool rotated = false;
+    for (int p = 0; p < cols; ++p)
+      for (int q = p + 1; q < cols; ++q) {
+        double al = 0, be = 0, ga = 0;
+        for (int k = 0; k < rows; ++k) {
+          const double x = m[k * cols + p], y = m[k * cols + q];
+          al += x * x;
+          be += y * y;
+          ga += x * y;
+        }
+        if (al <= tiny || be <= tiny || std::fabs(ga) <= 1e-15 * std::sqrt(al * be)) continue;
+        rotated = true;
+        const double ze = (be - al) / (2.0 * ga);
+        const double t = (ze >= 0 ? 1.0 : -1.0) / (std::fabs(ze) + std::sqrt(1.0 + ze * ze));
+        const double c = 1.0 / std::sqrt(1.0 + t * t), s = c * t;
+        for (int k = 0; k < rows; ++k) {
+          const double x = m[k * cols + p], y = m[k * cols + q];
+          m[k * cols + p] = c * x - s * y;
+          m[k * cols + q] = s * x + c * y;
+        }
+        for (int k = 0; k < cols; ++k) {
+          const double x = w[k * cols + p], y = w[k * cols + q];
+          w[k * cols + p] = c * x - s * y;
+          w[k * cols + q] = s * x + c * y;
+        }
+      }
+    if (!rotated) break;
+  }
+  for (int j = 0; j < cols; ++j) {
+    double s2 = 0;
+    for (int k = 0; k < rows; ++k) s2 += m[k * cols + j] * m[k * cols + j];
+    sig[j] = std::sqrt(s2);
+  }
+}
+
+// Factor G = R^T R of a PSD Gram matrix through its eigenvectors, dropping
+// eigenvalues below 1e-13 max: R = sqrt(L) V^T (rho x k) and I = V L^-1/2 (k x rho).
+int gram_factor(int k, const double* g, double* R, double* I) {
+  std::vector<double> a(k * k), w(k), v(k * k);
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) a[i * k + j] = 0.5 * (g[i * k + j] + g[j * k + i]);
+  jacobi_eigh(k, a.data(), w.data(), v.data());
+  double wmax = 0;
+  for (int i = 0; i < k; ++i) wmax = std::max(wmax, w[i]);
+  int rho = 0;
+  for (int j = 0; j < k; ++j) {
+    if (!(w[j] > 1e-13 * std::max(wmax, 1e-300))) continue;
+    const double sq = std::sqrt(w[j]);
+    for (int i = 0; i < k; ++i) {
+      R[rho * k + i] = sq * v[i * k + j];
+      I[i * k + rho] = v[i * k + j] / sq;   // I has row stride k
+    }
+    ++rho;
+  }
+  return rho;
+}
+
+// Core maps of the recompression: Xa (k x rn), Xb (k x rn), written as
+// X[i * ldx + j] and X[i * ldx + rn + j].  Returns rn (0 on a zero field).
+int lr_core(int k, const double* Ga, const double* Gb, double eps, int max_rank, double* X, int ldx) {
+  std::vector<double> Ra(k * k), Ia(k * k), Rb(k * k), Ib(k * k);
+  const int ra = gram_factor(k, Ga, Ra.data(), Ia.data());
+  const int rb = gram_factor(k, Gb, Rb.data(), Ib.data());
+  if (ra == 0 || rb == 0) return 0;
+  std::vector<double> M(ra * rb), sig(rb), W(rb * rb);
+  for (int i = 0; i < ra; ++i)
+    for (int j = 0; j < rb; ++j) {
+      double t = 0;
+      for (int l = 0; l < k; ++l) t += Ra[i * k + l] * Rb[j * k + l];
+      M[i * rb + j] = t;
+    }
+  jacobi_svd(ra, rb, M.data(), sig.data(), W.data());
+  std::vector<int> ord(rb);
+  for (int j = 0; j < rb; ++j) ord[j] = j;
+  std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return sig[x] > sig[y]; });
+  double tot = 0;
+  for (int j = 0; j < rb; ++j) tot += sig[j] * sig[j];
+  int rn = std::min(ra, rb);
+  double tail = 0;   // smallest rank whose discarded tail is <= eps^2 * total
+  for (int j = std::min(ra, rb) - 1; j >= 1; --j) {
+    tail += sig[ord[j]] * sig[ord[j]];
+    if (tail <= eps * eps * tot) rn = j;
+    else break;
+  }
+  if (max_rank > 0) rn = std::min(rn, max_rank);
+  rn = std::max(rn, 1);
+  // Xa = Ia (U Sigma)_r, where U Sigma = M's columns (ra x rb after rotation);
+  // Xb = Ib W_r
+  for (int i = 0; i < k; ++i)
+    for (int jj = 0; jj < rn; ++jj) {
+      const int j = ord[jj];
+      double ta = 0, tb = 0;
+      for (int l = 0; l < ra; ++l) ta += Ia[i * k + l] * M[l * rb + j];
+      for (int l = 0; l < rb; ++l) tb += Ib[i * k + l] * W[l * rb + j];
+      X[i * ldx + jj] = ta;
+      X[i * ldx + rn + jj] = tb;
+    }
+  return rn;
+}
+
 }  // namespace
 
 extern "C" {
@@ -349,6 +513,65 @@ int stsp_tt_dense_diffusion(int dtype, const void* U, void* V, int N, int M, dou
   else
     return -4;
   return (int)hipGetLastError();
+}
+
+// Host only: core maps of the factored step from the two k x k Gram matrices
+// (G = [Ga, Gb], doubles).  X (k x ldx, ldx >= 2 k) receives [Xa | Xb].
+int stsp_tt_core(int k, const double* G, double eps, int max_rank, double* X, int ldx) {
+  if (k < 1 || k > 64 || ldx < 2 * k) return -1;
+  return lr_core(k, G, G + k * k, eps, max_rank, X, ldx);
+}
+
+// One explicit factored diffusion step U' = U + c (D U + U D^T) for U = A B^T
+// (A, B: N x r, row strides lda / ldb), recompressed to rank rn <= max_rank:
+// expand (2 launches) -> MFMA Gram (2 x 2 launches) -> Gram to pinned host ->
+// host core -> maps to the device -> MFMA products into Aout / Bout (N x rn,
+// row stride ldo).  ws = device workspace (stsp_tt_step_workspace elements),
+// hbuf = pinned host buffer of 2 k^2 + 2 k^2 doubles.  Returns rn (> 0) or an
+// error (< 0).  The stream is synchronised once (for the Gram matrices).
+size_t stsp_tt_step_workspace(int N, int r) {
+  const int k = 2 * r, kp = (k + 15) / 16 * 16;
+  return (size_t)2 * N * k + 2 * (size_t)k * k + (size_t)stsp_tt_gram_blocks(N) * kp * kp + (size_t)k * 2 * k;
+}
+
+int stsp_tt_lr_step(int dtype, const void* A, int lda, const void* B, int ldb, int N, int r, double c, double ih2,
+                    int periodic,
+                    double eps, int max_rank, void* ws, double* hbuf, void* Aout, void* Bout, int ldo,
+                    hipStream_t st) {
+  const int k = 2 * r;
+  if (N < 1 || r < 1 || k > 64) return -1;
+  const size_t es = dtype == 1 ? 8 : 4;
+  char* w = (char*)ws;
+  void* Ah = w;
+  void* Bh = w + es * (size_t)N * k;
+  void* G = w + es * 2 * (size_t)N * k;
+  void* part = (char*)G + es * 2 * (size_t)k * k;
+  const int P = stsp_tt_gram_blocks(N);
+  const int kp = (k + 15) / 16 * 16;
+  void* dX = (char*)part + es * (size_t)P * kp * kp;
+  int rc;
+  if ((rc = stsp_tt_expand(dtype, A, lda, Ah, k, N, r, 1.0, 0.0, 0.0, c, ih2, periodic, st))) return rc;
+  if ((rc = stsp_tt_expand(dtype, B, ldb, Bh, k, N, r, 1.0, c, 1.0, 0.0, ih2, periodic, st))) return rc;
+  if ((rc = stsp_tt_gram(dtype, Ah, k, Ah, k, N, k, k, part, P, G, k, 1.0, st))) return rc;
+  if ((rc = stsp_tt_gram(dtype, Bh, k, Bh, k, N, k, k, part, P, (char*)G + es * k * k, k, 1.0, st))) return rc;
+  double* hG = hbuf;
+  double* hX = hbuf + 2 * k * k;
+  if (hipMemcpyAsync(hG, G, es * 2 * k * k, hipMemcpyDeviceToHost, st) != hipSuccess) return -20;
+  if (hipStreamSynchronize(st) != hipSuccess) return -21;
+  if (dtype == 0) {   // widen in place (back to front)
+    const float* f = (const float*)hG;
+    for (int i = 2 * k * k - 1; i >= 0; --i) hG[i] = (double)f[i];
+  }
+  const int rn = lr_core(k, hG, hG + k * k, eps, max_rank, hX, 2 * k);
+  if (rn <= 0) return -22;
+  if (dtype == 0) {   // narrow in place (front to back)
+    float* f = (float*)hX;
+    for (int i = 0; i < 2 * k * k; ++i) f[i] = (float)hX[i];
+  }
+  if (hipMemcpyAsync(dX, hX, es * 2 * k * k, hipMemcpyHostToDevice, st) != hipSuccess) return -23;
+  if ((rc = stsp_tt_mm(dtype, Ah, k, dX, 2 * k, Aout, ldo, N, k, rn, 1.0, 0.0, st))) return rc;
+  if ((rc = stsp_tt_mm(dtype, Bh, k, (char*)dX + es * rn, 2 * k, Bout, ldo, N, k, rn, 1.0, 0.0, st))) return rc;
+  return rn;
 }
 
 }  // extern "C"

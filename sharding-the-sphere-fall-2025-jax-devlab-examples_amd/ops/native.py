@@ -111,6 +111,12 @@ def _declare_tt(L):
     L.stsp_tt_expand.restype = ci
     L.stsp_tt_dense_diffusion.argtypes = [ci, vp, vp, ci, ci, cd, vp]
     L.stsp_tt_dense_diffusion.restype = ci
+    L.stsp_tt_core.argtypes = [ci, vp, cd, ci, vp, ci]
+    L.stsp_tt_core.restype = ci
+    L.stsp_tt_step_workspace.argtypes = [ci, ci]
+    L.stsp_tt_step_workspace.restype = ctypes.c_size_t
+    L.stsp_tt_lr_step.argtypes = [ci, vp, ci, vp, ci, ci, ci, cd, cd, ci, cd, ci, vp, vp, vp, vp, ci, vp]
+    L.stsp_tt_lr_step.restype = ci
 
 
 def available() -> bool:

@@ -121,3 +121,24 @@ def test_low_rank_diffusion_hip_matches_dense(bc):
     got = lr.dense().cpu()
     assert lr.rank <= 24
     assert float((got - dense).norm() / dense.norm()) < 1e-7
+
+
+@pytest.mark.parametrize("k", [2, 6, 16, 40])
+def test_native_core_matches_numpy_core_cpu(k):
+    """Host C++ core of the fused step (Jacobi eigen + one-sided Jacobi SVD)
+    reproduces the numpy route, including exactly rank-deficient Grams."""
+    from stsphere.ops import native
+    L = native.require_native()
+    rng = np.random.default_rng(k)
+    A = rng.standard_normal((300, k))
+    B = rng.standard_normal((300, k))
+    A[:, -1] = 2.0 * A[:, 0]
+    s = tt.LowRankDiffusion(64, eps=1e-9, max_rank=24)
+    G = np.ascontiguousarray(np.stack([A.T @ A, B.T @ B]))
+    X = np.zeros((k, 2 * k))
+    rn = L.stsp_tt_core(k, G.ctypes.data, 1e-9, 24, X.ctypes.data, 2 * k)
+    Xa, Xb = s._core(G)
+    assert rn == Xa.shape[1] == min(k - 1, 24)
+    got = (A @ X[:, :rn]) @ (B @ X[:, rn:2 * rn]).T
+    want = (A @ Xa) @ (B @ Xb).T
+    assert np.linalg.norm(got - want) / np.linalg.norm(want) < 1e-12
