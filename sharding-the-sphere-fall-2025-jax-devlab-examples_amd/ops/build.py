@@ -47,20 +47,53 @@ def needs_build(variant: str = "") -> bool:
     return False
 
 
+def _obj_dir(variant: str) -> str:
+    return os.path.join(HERE, "_obj", variant or "prod")
+
+
 def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
+    """Compile each source to an object (in parallel; an object is rebuilt
+    only when its source or a header is newer), then link the library."""
     lib = lib_for(variant)
     if not force and not needs_build(variant):
         return lib
-    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-Wno-unused-result", "-I", CSRC, "-I", "/opt/rocm/include", *VARIANT_FLAGS[variant],
-           *srcs, "-o", lib + ".tmp", "-L/opt/rocm/lib", "-l:librccl.so.1", "-lrocprofiler-sdk-roctx"]
+    odir = _obj_dir(variant)
+    os.makedirs(odir, exist_ok=True)
+    hdr_t = max([os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS if os.path.exists(os.path.join(CSRC, h))]
+                + [0.0])
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-I", CSRC,
+             "-I", "/opt/rocm/include", *VARIANT_FLAGS[variant]]
+    objs, procs = [], []
+    for src in SOURCES:
+        sp = os.path.join(CSRC, src)
+        if not os.path.exists(sp):
+            continue
+        op = os.path.join(odir, src + ".o")
+        objs.append(op)
+        if not force and os.path.exists(op) and os.path.getmtime(op) >= max(os.path.getmtime(sp), hdr_t):
+            continue
+        cmd = [_hipcc(), *flags, "-c", sp, "-o", op + ".tmp"]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((op, cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
+    failed = False
+    for op, cmd, pr in procs:
+        out, _ = pr.communicate()
+        if pr.returncode != 0:
+            sys.stderr.write(out)
+            failed = True
+        else:
+            os.replace(op + ".tmp", op)
+    if failed:
+        raise RuntimeError("hipcc failed")
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib + ".tmp", "-L/opt/rocm/lib",
+           "-l:librccl.so.1", "-lrocprofiler-sdk-roctx"]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
-        raise RuntimeError(f"hipcc failed ({r.returncode})")
+        raise RuntimeError(f"link failed ({r.returncode})")
     os.replace(lib + ".tmp", lib)
     return lib
 
