@@ -20,8 +20,9 @@ LIB = os.path.join(HERE, "libstsp.so")
 SOURCES = ["stage_kernel.hip", "tt_kernels.hip", "runtime.cpp"]
 HEADERS = ["stsp_kernels.h", "runtime.h"]
 ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
-# library variants: "" = production; "diag" = in-kernel phase stamps (-DSTSP_STAMPS)
-VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"]}
+# library variants: "" = production; "diag" = in-kernel phase stamps (-DSTSP_STAMPS);
+# "xgf0" / "xgf2" = xGMI publish-protocol probes (stage_kernel.hip, STSP_XG_FENCE)
+VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgf0": ["-DSTSP_XG_FENCE=0"], "xgf2": ["-DSTSP_XG_FENCE=2"]}
 
 
 def lib_for(variant: str = "") -> str:

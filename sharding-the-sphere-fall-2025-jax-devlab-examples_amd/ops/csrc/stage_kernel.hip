@@ -28,6 +28,17 @@
 // (PDF s.12), 2 = shallow water with Cartesian momentum (PY:2).
 #include "stsp_kernels.h"
 
+// Publish protocol of the direct xGMI halo (probe variants, tools/xg_fence_probe.py,
+// profiles/r1_xg_fence_probe.jsonl; loopback C96 µs/step, plain step 17.1):
+//   0 = __threadfence_system() + release add: 117.5 (the fence is seq_cst, so
+//       every wave also invalidates L2 and the whole grid re-reads from HBM)
+//   1 = release add only (one L2 write-back per producing block): 28.6  <- default
+//   2 = relaxed add after the storing waves drain: 26.8 (relies on the ring
+//       stores being system-scope write-through; not a release in the model)
+#ifndef STSP_XG_FENCE
+#define STSP_XG_FENCE 1
+#endif
+
 #include <cstdlib>
 #include <type_traits>
 
@@ -660,11 +671,17 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   }
   if constexpr (XG) {
     if (feed) {   // publish: every storing wave drains, then one lane per peer counts
+#if STSP_XG_FENCE == 0
       __threadfence_system();
+#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid < 32 && ((feed >> tid) & 1))
+#if STSP_XG_FENCE == 2
+        __hip_atomic_fetch_add((gu64*)a.peer_cnt[tid], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
         __hip_atomic_fetch_add((gu64*)a.peer_cnt[tid], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
     }
     if (tid == 0) a.epoch[bid] = xe + 1;
   }
