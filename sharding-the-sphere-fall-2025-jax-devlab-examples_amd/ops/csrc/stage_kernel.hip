@@ -310,6 +310,34 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   const unsigned tb = (unsigned)(tile * pw * pw);   // padded tile base
   const int gbase = tile * nn;                 // compact geometry base
   STAMP(0);
+  // direct xGMI: the block's epoch and peer masks are issued before every other
+  // load, so waiting for them (vmcnt counts in issue order) never waits for the
+  // prefetch below and the poll can start one round trip into the kernel
+  int xe = 0, need = 0, feed = 0;
+  if constexpr (XG) {
+    xe = a.epoch[bid];
+    need = a.bmask[2 * bid];
+    feed = a.bmask[2 * bid + 1];
+  }
+  // ghost-map entry of this thread's window cell when it lies in a ghost strip
+  // (the map is static: issued now, it is back by the time the poll is done
+  // instead of costing its own round trip in the window phase)
+  int wgm = 0;
+  if constexpr (REMOTE || XG) {
+    if (tid < EX * EY) {
+      const int ly = tid / EX, lx = tid - ly * EX;
+      const int x = x0 + lx - NG, y = y0 + ly - NG;
+      const bool oxx = (x < 0) | (x >= n), oyy = (y < 0) | (y >= n);
+      if (x < n + NG && y < n + NG && oxx != oyy) {
+        int side, layer, pos;
+        if (x < 0) { side = 0; layer = -1 - x; pos = y; }
+        else if (x >= n) { side = 1; layer = x - n; pos = y; }
+        else if (y < 0) { side = 2; layer = -1 - y; pos = x; }
+        else { side = 3; layer = y - n; pos = x; }
+        wgm = a.gmap[((tile * 4 + side) * mg + layer) * n + pos];
+      }
+    }
+  }
 
   // ---- 0. issue every per-thread operand load up front ------------------------
   // (a) own cell (threads < BX*BY)
@@ -380,13 +408,9 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   STAMP(1);
 
   // ---- 0b. direct xGMI: wait for the peers whose ghosts this block reads ------
-  int xe = 0, feed = 0;
   bool rblk = REMOTE;
   const T* rring = a.recv;
   if constexpr (XG) {
-    xe = a.epoch[bid];
-    const int need = a.bmask[2 * bid];
-    feed = a.bmask[2 * bid + 1];
     rblk = need != 0;
     rring = a.recv + (long)(xe % 3) * a.ring;
     if (rblk) {
@@ -458,14 +482,8 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       const unsigned pa = tb + (unsigned)((y + mg) * pw + (x + mg));
       bool from_recv = false;
       if constexpr (REMOTE || XG) {
-        const bool oxx = (x < 0) | (x >= n), oyy = (y < 0) | (y >= n);
-        if (rblk && oxx != oyy) {
-          int side, layer, pos;
-          if (x < 0) { side = 0; layer = -1 - x; pos = y; }
-          else if (x >= n) { side = 1; layer = x - n; pos = y; }
-          else if (y < 0) { side = 2; layer = -1 - y; pos = x; }
-          else { side = 3; layer = y - n; pos = x; }
-          const int m = a.gmap[((tile * 4 + side) * mg + layer) * n + pos];
+        if (rblk) {
+          const int m = wgm;   // < 0: remote slot -1 - m (0 outside the ghost strips)
           if (m < 0) {
             from_recv = true;
             const T* rp = rring + (long)(-1 - m) * F;
