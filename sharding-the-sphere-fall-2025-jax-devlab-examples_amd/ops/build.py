@@ -21,8 +21,10 @@ SOURCES = ["stage_kernel.hip", "tt_kernels.hip", "runtime.cpp"]
 HEADERS = ["stsp_kernels.h", "runtime.h"]
 ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
 # library variants: "" = production; "diag" = in-kernel phase stamps (-DSTSP_STAMPS);
-# "xgf0" / "xgf2" = xGMI publish-protocol probes (stage_kernel.hip, STSP_XG_FENCE)
-VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgf0": ["-DSTSP_XG_FENCE=0"], "xgf2": ["-DSTSP_XG_FENCE=2"]}
+# "xgc" = the arrival-counter hand-off of the xGMI halo instead of tagged granules
+# (STSP_XG_TAG=0), "xgf0" / "xgf2" = its publish-protocol probes (STSP_XG_FENCE)
+VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgc": ["-DSTSP_XG_TAG=0"],
+                 "xgf0": ["-DSTSP_XG_TAG=0", "-DSTSP_XG_FENCE=0"], "xgf2": ["-DSTSP_XG_TAG=0", "-DSTSP_XG_FENCE=2"]}
 
 
 def lib_for(variant: str = "") -> str:

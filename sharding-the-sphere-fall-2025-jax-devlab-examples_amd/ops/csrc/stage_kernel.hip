@@ -28,8 +28,9 @@
 // (PDF s.12), 2 = shallow water with Cartesian momentum (PY:2).
 #include "stsp_kernels.h"
 
-// Publish protocol of the direct xGMI halo (probe variants, tools/xg_fence_probe.py,
-// profiles/r1_xg_fence_probe.jsonl; loopback C96 µs/step, plain step 17.1):
+// Publish protocol of the arrival-counter hand-off (STSP_XG_TAG=0 below; probe
+// variants, tools/xg_fence_probe.py, profiles/r1_xg_fence_probe.jsonl; loopback
+// C96 µs/step, plain step 17.1):
 //   0 = __threadfence_system() + release add: 117.5 (the fence is seq_cst, so
 //       every wave also invalidates L2 and the whole grid re-reads from HBM)
 //   1 = release add only (one L2 write-back per producing block): 28.6  <- default
@@ -38,6 +39,27 @@
 #ifndef STSP_XG_FENCE
 #define STSP_XG_FENCE 1
 #endif
+// Halo hand-off form (stsp_kernels.h, xg fields):
+//   0 = arrival counters (drain + release add per producing block, block-level poll)
+//   1 = tagged granules: the data is the flag.  Each 32-bit word of a ghost cell
+//       travels as ONE 8-byte {tag = stage epoch + 1, payload} relaxed system-scope
+//       atomic store (single-copy atomic, so never torn); the consumer thread
+//       re-reads its cell's granules until every tag matches.  The producer
+//       neither drains nor signals, and the consumer skips the separate poll
+//       round trip (cdna_hip_programming.md Guideline 16, R2).
+//   Measured (tools/xg_tag_round.sh, profiles/r1_xg_tag_probe.jsonl, C96 fp64 µs/step):
+//   loopback 28.9 (counters) -> 24.9 (tags); two ranks sharing one GPU 26.9 -> 21.8.
+#ifndef STSP_XG_TAG
+#define STSP_XG_TAG 1
+#endif
+// Ring slots.  A rank reads slot e % S during its stage e while a peer writes
+// slot (e_p + 1) % S during its stage e_p.  A peer can have STARTED at most two
+// stages past us: its stage e + 2 needs its stage e + 1 complete, which waited
+// for our stage-e output, i.e. our stage e started and e - 1 completed.  So the
+// peer writes slot (e + 1 .. e + 3) % S, never e % S, iff S does not divide 1,
+// 2 or 3: S = 4 (three slots left a window where a peer two stages ahead
+// overwrote the slot a slow block of ours was still reading).
+#define STSP_XG_SLOTS 4
 
 #include <cstdlib>
 #include <type_traits>
@@ -257,16 +279,11 @@ __device__ __forceinline__ void st_state(T* p, T v) {
 // One RK stage of one BX x BY block (all phases).  SYNC = persistent-kernel
 // mode: every access to state written by other workgroups in this launch is an
 // agent-scope sc1 access (L1 bypass, write-through), see persistent_kernel.
-// XG = direct xGMI halo: a block that reads remote ghosts first waits for the
-// arrival counters of those peers, reads the ghosts from this rank's receive
-// ring (slot epoch % 3), and every block stores the cells its peers need into
-// their rings (slot (epoch + 1) % 3) before bumping their counters.
-//
-// Why three ring slots and no reset: a rank can run at most one stage ahead of
-// a peer it exchanges with (it waits for that peer's previous stage), so a
-// write into slot (e + 1) % 3 never lands on the slot (e % 3) the peer may still
-// be reading, nor on the one before it; counters only grow (stage e of a peer
-// is complete once its counter reaches (e + 1) * nprod).
+// XG = direct xGMI halo: a block reads its remote ghosts from this rank's
+// receive ring (slot epoch % STSP_XG_SLOTS) once they have arrived (tags match,
+// or the peers' arrival counters are complete), and every block stores the cells
+// its peers need into their rings (slot (epoch + 1) % STSP_XG_SLOTS).  Why four
+// slots and no reset: see STSP_XG_SLOTS; tags and counters only grow.
 template <typename T, int P, int BX, int BY, int LIM, bool REMOTE, bool SYNC, bool XG = false>
 __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   constexpr int F = Phys<P>::F;
@@ -412,8 +429,8 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   const T* rring = a.recv;
   if constexpr (XG) {
     rblk = need != 0;
-    rring = a.recv + (long)(xe % 3) * a.ring;
-    if (rblk) {
+    rring = a.recv + (long)(xe % STSP_XG_SLOTS) * a.ring;   // tags: a.ring counts 8-byte granules, see below
+    if (!STSP_XG_TAG && rblk) {
       if (tid < 32 && ((need >> tid) & 1)) {
         const unsigned long long want = (unsigned long long)xe * a.nprod[tid];
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -486,11 +503,42 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
           const int m = wgm;   // < 0: remote slot -1 - m (0 outside the ghost strips)
           if (m < 0) {
             from_recv = true;
-            const T* rp = rring + (long)(-1 - m) * F;
-            if constexpr (XG) {
+            if constexpr (XG && STSP_XG_TAG) {
+              // spin on this cell's granules until all carry this stage's tag
+              constexpr int G = sizeof(T) / 4;
+              const gu64* rp = ((const gu64*)(a.recv)) + (long)(xe % STSP_XG_SLOTS) * a.ring +
+                               (long)(-1 - m) * (F * G);
+              const unsigned want = (unsigned)xe + 1u;
+              unsigned long long gr[F * G];
+              const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+              for (;;) {
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < F * G; ++k) {
+                  gr[k] = __hip_atomic_load(rp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                  ok &= (unsigned)(gr[k] >> 32) == want;
+                }
+                if (ok) break;
+                if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+                if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
+                  __hip_atomic_store((gu32*)a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+              }
+#pragma unroll
+              for (int f = 0; f < F; ++f) {
+                if constexpr (G == 2)
+                  v[f] = __builtin_bit_cast(T, (gr[2 * f + 1] << 32) | (gr[2 * f] & 0xFFFFFFFFull));
+                else
+                  v[f] = __builtin_bit_cast(T, (unsigned)gr[f]);
+              }
+            } else if constexpr (XG) {
+              const T* rp = rring + (long)(-1 - m) * F;
 #pragma unroll
               for (int f = 0; f < F; ++f) v[f] = ld_sys(rp + f);
             } else {
+              const T* rp = rring + (long)(-1 - m) * F;
 #pragma unroll
               for (int f = 0; f < F; ++f) v[f] = ld_state<SYNC>(rp + f);
             }
@@ -680,15 +728,33 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       for (int k = 0; k < 4; ++k) {
         if (pt[k] < -1) {
           const int code = -2 - pt[k];
-          T* dst = a.peer_ring[code >> 24] + (long)((xe + 1) % 3) * a.ring + (long)(code & 0xFFFFFF) * F;
+          if constexpr (STSP_XG_TAG) {
+            constexpr int G = sizeof(T) / 4;
+            gu64* dst = ((gu64*)(a.peer_ring[code >> 24])) + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring +
+                        (long)(code & 0xFFFFFF) * (F * G);
+            const unsigned long long tag = (unsigned long long)((unsigned)xe + 2u) << 32;
 #pragma unroll
-          for (int f = 0; f < F; ++f) st_sys(dst + f, o[f]);
+            for (int f = 0; f < F; ++f) {
+              if constexpr (G == 2) {
+                const unsigned long long b = __builtin_bit_cast(unsigned long long, o[f]);
+                __hip_atomic_store(dst + 2 * f, tag | (b & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(dst + 2 * f + 1, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              } else {
+                __hip_atomic_store(dst + f, tag | __builtin_bit_cast(unsigned, o[f]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+              }
+            }
+          } else {
+            T* dst = a.peer_ring[code >> 24] + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring + (long)(code & 0xFFFFFF) * F;
+#pragma unroll
+            for (int f = 0; f < F; ++f) st_sys(dst + f, o[f]);
+          }
         }
       }
     }
   }
   if constexpr (XG) {
-    if (feed) {   // publish: every storing wave drains, then one lane per peer counts
+    if (!STSP_XG_TAG && feed) {   // publish: every storing wave drains, then one lane per peer counts
 #if STSP_XG_FENCE == 0
       __threadfence_system();
 #endif
@@ -951,15 +1017,34 @@ __global__ __launch_bounds__(256) void pack_kernel(const T* __restrict__ q, int 
 }
 
 // ---- direct xGMI halo: initial ghost delivery (no counter bump) -------------
+// Writes the ghosts of stage `epoch`'s input: slot epoch % SLOTS, tag epoch + 1.
 template <typename T>
 __global__ __launch_bounds__(256) void xg_prime_kernel(const T* __restrict__ q, int S, int F,
                                                        const int* __restrict__ src, const int* __restrict__ code,
-                                                       int nent, T* const* peer_ring, int ring, int slot_ring) {
+                                                       int nent, T* const* peer_ring, int ring, int epoch) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int slot = epoch % STSP_XG_SLOTS;
   if (i < nent) {
     const int c = code[i];
-    T* dst = peer_ring[c >> 24] + (long)slot_ring * ring + (long)(c & 0xFFFFFF) * F;
-    for (int f = 0; f < F; ++f) st_sys(dst + f, q[(long)f * S + src[i]]);
+    if constexpr (STSP_XG_TAG) {
+      constexpr int G = sizeof(T) / 4;
+      gu64* dst = ((gu64*)(peer_ring[c >> 24])) + (long)slot * ring + (long)(c & 0xFFFFFF) * F * G;
+      const unsigned long long tag = (unsigned long long)((unsigned)epoch + 1u) << 32;
+      for (int f = 0; f < F; ++f) {
+        const T v = q[(long)f * S + src[i]];
+        if constexpr (G == 2) {
+          const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+          __hip_atomic_store(dst + 2 * f, tag | (b & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(dst + 2 * f + 1, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+          __hip_atomic_store(dst + f, tag | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    } else {
+      T* dst = peer_ring[c >> 24] + (long)slot * ring + (long)(c & 0xFFFFFF) * F;
+      for (int f = 0; f < F; ++f) st_sys(dst + f, q[(long)f * S + src[i]]);
+    }
   }
   __threadfence_system();
 }
@@ -1075,15 +1160,18 @@ extern "C" int stsp_copy_index_launch(int dtype, const void* src, const int* sid
 }
 
 extern "C" int stsp_xg_prime_launch(int dtype, const void* q, int S, int F, const int* src, const int* code, int nent,
-                                    void* const* peer_ring, int ring, int slot_ring, hipStream_t stream) {
+                                    void* const* peer_ring, int ring, int epoch, hipStream_t stream) {
   if (nent <= 0) return 0;
-  if (slot_ring < 0 || slot_ring > 2 || ring <= 0) return -6;
+  if (epoch < 0 || ring <= 0) return -6;
   const int nb = (nent + 255) / 256;
   if (dtype == 1)
     hipLaunchKernelGGL(xg_prime_kernel<double>, dim3(nb), dim3(256), 0, stream, (const double*)q, S, F, src, code,
-                       nent, (double* const*)peer_ring, ring, slot_ring);
+                       nent, (double* const*)peer_ring, ring, epoch);
   else
     hipLaunchKernelGGL(xg_prime_kernel<float>, dim3(nb), dim3(256), 0, stream, (const float*)q, S, F, src, code,
-                       nent, (float* const*)peer_ring, ring, slot_ring);
+                       nent, (float* const*)peer_ring, ring, epoch);
   return (int)hipGetLastError();
 }
+
+extern "C" int stsp_xg_protocol(void) { return STSP_XG_TAG; }
+extern "C" int stsp_xg_slots(void) { return STSP_XG_SLOTS; }

@@ -35,12 +35,16 @@ typedef struct StageDesc {
   void* stamps;         // diagnostic builds only (-DSTSP_STAMPS): [nblocks][16 waves][8] s_memtime per phase
   // ---- direct xGMI halo (xg = 1; see ops/xgmi.py) ----------------------------
   // The producing block stores remote ghost cells straight into the consumer
-  // rank's receive ring (IPC-mapped, uncached) and bumps that rank's arrival
-  // counter; a consumer block polls only the counters of the peers it reads.
+  // rank's receive ring (IPC-mapped, uncached, STSP_XG_SLOTS slots).  Protocol
+  // (stsp_xg_protocol()): 1 = tagged granules, every ghost word travels as an
+  // 8-byte {epoch tag, 32-bit payload} atomic store and the consumer re-reads
+  // its granules until every tag matches (no counters, no drain); 0 = arrival
+  // counters (the producer drains its stores and bumps a counter per peer; a
+  // consumer block polls the counters of the peers it reads).
   // `recv` is then this rank's ring base; `push` entries < -1 encode
   // -2 - (peer << 24 | slot).
   int xg;
-  int ring;             // elements per ring slot (= max receive slots over ranks * F)
+  int ring;             // per ring slot: elements (counters) or 8-byte granules (tags)
   void* const* peer_ring;                  // [world] ring base of rank p (device array)
   unsigned long long* const* peer_cnt;     // [world] &counter[my rank] on rank p
   const unsigned long long* cnt;           // [world] arrival counters on this rank
@@ -62,7 +66,10 @@ int stsp_pack_launch(int dtype, const void* q, int S, int F, const int* idx, int
 int stsp_copy_index_launch(int dtype, const void* src, const int* sidx, void* dst, const int* didx, int k,
                            int batch, long src_stride, long dst_stride, hipStream_t stream);
 // Direct xGMI halo: write the remote ghost cells of state q (entries src[i] ->
-// code[i] = peer << 24 | slot) into ring slot `slot_ring` of every peer.
+// code[i] = peer << 24 | slot) into every peer's ring slot of stage `epoch`.
 int stsp_xg_prime_launch(int dtype, const void* q, int S, int F, const int* src, const int* code, int nent,
-                         void* const* peer_ring, int ring, int slot_ring, hipStream_t stream);
+                         void* const* peer_ring, int ring, int epoch, hipStream_t stream);
+// Direct xGMI halo build constants: protocol (0 counters, 1 tagged granules), ring slots.
+int stsp_xg_protocol(void);
+int stsp_xg_slots(void);
 }

@@ -11,23 +11,32 @@ therefore becomes part of the stage kernel itself (ops/csrc/stage_kernel.hip,
 XG variant):
 
 * Every rank owns one uncached allocation holding ``[world]`` u64 arrival
-  counters and a 3-slot receive ring (``ring = max receive slots x F``
-  elements per slot).  Peers map it with ``hipIpcOpenMemHandle``.
+  counters and a 4-slot receive ring (``ring_slots x F`` values per slot).
+  Peers map it with ``hipIpcOpenMemHandle``.
 * A block whose cells are ghosts of another rank stores them into that rank's
-  ring slot ``(epoch + 1) % 3``.  Its waves drain their stores, then one lane
-  per peer adds 1 to that peer's counter (system-scope release).  The push map
-  carries the destination: ``-2 - (peer << 24 | slot)``.
-* A block that reads remote ghosts polls the counters of those peers until
-  ``counter[p] >= epoch * nprod[p]``.  ``nprod[p]`` is the number of producer
-  blocks on p that feed this rank.  The poll is bounded by a timeout that sets
-  ``err``; after that every poll falls through.  The block then reads ring
-  slot ``epoch % 3``.
-* ``epoch`` is a per-block count of completed stages.  Counters never reset.
+  ring slot ``(epoch + 1) % 4``.  The push map carries the destination:
+  ``-2 - (peer << 24 | slot)``.
+* Hand-off (``stsp_xg_protocol()``, compile-time):
 
-Three slots are enough because a rank waits for its peers' previous stage, so
-it can run at most one stage ahead of any peer it exchanges with (the proof is
-in the kernel comment).  The whole step is plain kernels, so multi-GPU steps
-are captured in a hipGraph like single-GPU ones.
+  - tagged granules (1): every 32-bit word of a ghost travels as one 8-byte
+    ``{tag = epoch + 1, payload}`` atomic store; the consumer thread re-reads
+    its granules until every tag matches.  The data is the flag: no drain, no
+    counter, no separate poll round trip.
+  - arrival counters (0): the producer's waves drain their stores, then one
+    lane per peer adds 1 to that peer's counter (system-scope release).  A
+    block that reads remote ghosts polls the counters of those peers until
+    ``counter[p] >= epoch * nprod[p]``.  ``nprod[p]`` is the number of producer
+    blocks on p that feed this rank.
+
+  Either wait is bounded by a timeout that sets ``err``; after that every wait
+  falls through.
+* ``epoch`` is a per-block count of completed stages.  Tags and counters never
+  reset.
+
+Four slots make the ring race-free: a peer can have started at most two stages
+past a rank's current stage (the proof is at STSP_XG_SLOTS in the kernel), so
+it never writes the slot that rank still reads.  The whole step is plain
+kernels, so multi-GPU steps are captured in a hipGraph like single-GPU ones.
 
 ``XgmiPlan`` is the host-side index math (numpy only, tested on CPU).
 ``XgmiHalo`` owns the memory, the IPC mappings and the initial delivery.
@@ -192,8 +201,14 @@ class XgmiHalo:
         dev = e.device
         F = e.physics.F
         self.esize = torch.tensor([], dtype=e.dtype).element_size()
-        self.ring = self.xp.ring_slots * F
-        nbytes = CNT_BYTES + 3 * self.ring * self.esize
+        self.protocol = int(L.stsp_xg_protocol())
+        self.slots = int(L.stsp_xg_slots())
+        if self.protocol == 1:   # 8-byte granules, one per 32-bit word
+            self.ring = self.xp.ring_slots * F * (self.esize // 4)
+            nbytes = CNT_BYTES + self.slots * self.ring * 8
+        else:
+            self.ring = self.xp.ring_slots * F
+            nbytes = CNT_BYTES + self.slots * self.ring * self.esize
         base = ctypes.c_void_p()
         rc = L.stsp_xg_alloc(ctypes.c_size_t(nbytes), ctypes.byref(base))
         if rc != 0:
@@ -292,7 +307,7 @@ class XgmiHalo:
         rc = self._lib.stsp_xg_prime_launch(native.dtype_code(e.dtype), native.ptr(e.pool[0]), e.plan.S,
                                             e.physics.F, native.ptr(self.prime_src), native.ptr(self.prime_code),
                                             int(self.prime_src.numel()), native.ptr(self.peer_ring), self.ring,
-                                            e0 % 3, native.current_stream_handle())
+                                            e0, native.current_stream_handle())
         native.check(rc, "xGMI prime")
         torch.cuda.synchronize(e.device)
         if dist.is_available() and dist.is_initialized() and self.world > 1:
@@ -337,4 +352,8 @@ def _declare(L):
     L.stsp_enable_peers.restype = ci
     L.stsp_xg_prime_launch.argtypes = [ci, vp, ci, ci, vp, vp, ci, vp, ci, ci, vp]
     L.stsp_xg_prime_launch.restype = ci
+    L.stsp_xg_protocol.argtypes = []
+    L.stsp_xg_protocol.restype = ci
+    L.stsp_xg_slots.argtypes = []
+    L.stsp_xg_slots.restype = ci
     return L
