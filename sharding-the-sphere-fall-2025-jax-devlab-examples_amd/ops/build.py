@@ -24,7 +24,9 @@ ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
 # "xgc" = the arrival-counter hand-off of the xGMI halo instead of tagged granules
 # (STSP_XG_TAG=0), "xgf0" / "xgf2" = its publish-protocol probes (STSP_XG_FENCE)
 VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgc": ["-DSTSP_XG_TAG=0"],
-                 "xgf0": ["-DSTSP_XG_TAG=0", "-DSTSP_XG_FENCE=0"], "xgf2": ["-DSTSP_XG_TAG=0", "-DSTSP_XG_FENCE=2"]}
+                 "xgf0": ["-DSTSP_XG_TAG=0", "-DSTSP_XG_FENCE=0"], "xgf2": ["-DSTSP_XG_TAG=0", "-DSTSP_XG_FENCE=2"],
+                 "unfused": ["-DSTSP_FUSE_FACES=0"],
+                 "ownw0": ["-DSTSP_OWN_SKIP0=0"]}
 
 
 def lib_for(variant: str = "") -> str:

@@ -60,6 +60,16 @@
 // 2 or 3: S = 4 (three slots left a window where a peer two stages ahead
 // overwrote the slot a slow block of ours was still reading).
 #define STSP_XG_SLOTS 4
+// Own-cell waves: 1 = the first waves not on SIMD 0, 0 = waves 0 .. n-1.
+#ifndef STSP_OWN_SKIP0
+#define STSP_OWN_SKIP0 1
+#endif
+// Face reconstruction fused into the flux phase for PLR (stage_body phase 2):
+// 1 = each edge thread computes its two faces from the window; 0 = separate
+// face phase through LDS (always for PPM).
+#ifndef STSP_FUSE_FACES
+#define STSP_FUSE_FACES 1
+#endif
 
 #include <cstdlib>
 #include <type_traits>
@@ -290,6 +300,10 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   constexpr int NG = (LIM == 4) ? 3 : Phys<P>::NG;   // PPM reads 3 ghost layers
   constexpr int FL = Phys<P>::FL;              // primitive fields (+ sound speed) in LDS
   constexpr bool RECON = (P != 1);             // PLR reconstruction (not for diffusion)
+  // FUSED: each edge thread reconstructs the two faces it needs straight from
+  // the window (PLR only; PPM keeps the separate face phase, its stencil is wider)
+  constexpr bool FUSED = RECON && (LIM != 4) && STSP_FUSE_FACES;
+  constexpr bool FACES = RECON && !FUSED;
   constexpr int NT = Geom<BX, BY>::NT;
   constexpr int NX = Geom<BX, BY>::NX;
   constexpr int NY = Geom<BX, BY>::NY;
@@ -308,8 +322,8 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   constexpr int NFT = NFX + NFY;               // face tasks
   constexpr bool SW = (P == 2);
   __shared__ T s_w[FL][EY][EX + 1];
-  __shared__ T s_fm[RECON ? F : 1][RECON ? NFT : 1];   // face value on the cell's minus side
-  __shared__ T s_fp[RECON ? F : 1][RECON ? NFT : 1];   // ... and plus side
+  __shared__ T s_fm[FACES ? F : 1][FACES ? NFT : 1];   // face value on the cell's minus side
+  __shared__ T s_fp[FACES ? F : 1][FACES ? NFT : 1];   // ... and plus side
   __shared__ T s_fl[F][NE];                            // edge fluxes
   __shared__ T s_nrm[SW ? 3 : 1][SW ? BX + BY + 2 : 1];  // edge normals: x columns, then y rows
   __shared__ T s_len[SW ? NE : 1];                     // edge lengths (for the curvature balance)
@@ -336,13 +350,49 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     need = a.bmask[2 * bid];
     feed = a.bmask[2 * bid + 1];
   }
+  // Thread roles.  Waves run on SIMD (wave % 4), and SIMD 0 also carries the
+  // ninth (partial) flux wave of a 16x16 block, so the own-cell waves (prefetch,
+  // sources, update, stores) are the first BX*BY/64 waves NOT on SIMD 0:
+  // 1, 2, 3, 5 for 256 cells.  An own-cell thread puts its own cell's state
+  // (which it loads anyway) into the window; every other thread loads at most
+  // one cell of the NG-wide ring around the block.  Measured on C96 fp64
+  // (profiles/r1_c96_stage_ab.txt): splitting the window this way instead of
+  // row-major 16-byte pairs in waves 0-3 took the stage from 5.52 to 5.22 us.
+  constexpr int NIN = BX * BY, RING = EX * EY - NIN, NOWN = NIN / 64;
+  static_assert(NIN % 64 == 0, "own cells fill whole waves");
+  static_assert(NOWN <= NT / 64 - (NT / 64 + 3) / 4, "enough waves off SIMD 0");
+  const int wv = tid >> 6;
+#if STSP_OWN_SKIP0
+  const int below = wv - (wv + 3) / 4;          // waves < wv that are not on SIMD 0
+  const int oid = ((wv & 3) != 0 && below < NOWN) ? below * 64 + (tid & 63) : -1;
+#else
+  const int below = wv;                         // own cells in waves 0 .. NOWN-1
+  const int oid = wv < NOWN ? tid : -1;
+#endif
+  int wly = -1, wlx = 0;
+  if (oid >= 0) {
+    wly = NG + oid / BX;
+    wlx = NG + oid % BX;
+  } else {
+    const int r = tid - 64 * (below < NOWN ? below : NOWN);
+    static_assert(RING <= NT - NIN, "one ring cell per thread without an own cell");
+    if (r < 2 * NG * EX) {          // NG rows above and below
+      const int rr = r / EX;
+      wlx = r - rr * EX;
+      wly = rr < NG ? rr : EY - 2 * NG + rr;
+    } else if (r < RING) {          // NG columns left and right
+      const int r2 = r - 2 * NG * EX, rr = r2 / (2 * NG), c = r2 - rr * (2 * NG);
+      wly = NG + rr;
+      wlx = c < NG ? c : EX - 2 * NG + c;
+    }
+  }
   // ghost-map entry of this thread's window cell when it lies in a ghost strip
   // (the map is static: issued now, it is back by the time the poll is done
   // instead of costing its own round trip in the window phase)
   int wgm = 0;
   if constexpr (REMOTE || XG) {
-    if (tid < EX * EY) {
-      const int ly = tid / EX, lx = tid - ly * EX;
+    if (wly >= 0) {
+      const int ly = wly, lx = wlx;
       const int x = x0 + lx - NG, y = y0 + ly - NG;
       const bool oxx = (x < 0) | (x >= n), oyy = (y < 0) | (y >= n);
       if (x < n + NG && y < n + NG && oxx != oyy) {
@@ -358,13 +408,13 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 
   // ---- 0. issue every per-thread operand load up front ------------------------
   // (a) own cell (threads < BX*BY)
-  const int ox = tid % BX, oy = tid / BX;
+  const int ox = oid % BX, oy = oid / BX;
   const int cx = x0 + ox, cy = y0 + oy;
-  const bool own = (tid < BX * BY) && (cx < n) && (cy < n);
+  const bool own = (oid >= 0) && (cx < n) && (cy < n);
   const unsigned pc = tb + (unsigned)((cy + mg) * pw + (cx + mg));
   const unsigned gc = (unsigned)(gbase + cy * n + cx);
   T xs[F], acs[F];
-  T qo[P == 2 ? F : 1];   // own conserved state (SWE): from global, not kept in LDS
+  T qo[F];                // own conserved state: from global, not kept in LDS
   T iA = T(0), r0 = T(0), r1 = T(0), r2 = T(0);
   T gb[3] = {T(0), T(0), T(0)};
   int pt[4] = {-1, -1, -1, -1};
@@ -375,13 +425,13 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 #pragma unroll
       for (int f = 0; f < F; ++f) xs[f] = ld_state<SYNC>(o32(a.X + f * S, pc));
     }
+#pragma unroll
+    for (int f = 0; f < F; ++f) qo[f] = ld_state<SYNC>(o32(a.Q + f * S, pc));
     if (need_acc) {
 #pragma unroll
       for (int f = 0; f < F; ++f) acs[f] = ld_state<SYNC>(o32(a.acc_in + f * S, pc));
     }
     if constexpr (P == 2) {
-#pragma unroll
-      for (int f = 0; f < F; ++f) qo[f] = ld_state<SYNC>(o32(a.Q + f * S, pc));
       T rec[8];
       load_rec8<T>(o32(a.cgeo, gc * 8u), rec);
       iA = rec[0]; r0 = rec[1]; r1 = rec[2]; r2 = rec[3];
@@ -448,9 +498,8 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   }
 
   // ---- 1. window (block + NG halo) -> LDS --------------------------------------
-  // Same-rank blocks load cell PAIRS with 16-byte (fp64) loads when the padded
-  // rows are pair-aligned; remote-boundary blocks load cell by cell (a ghost
-  // may come from the receive buffer).
+  // Own-cell threads store the state they prefetched, the ring threads load one
+  // cell each (a remote ghost from the receive ring).
   auto put = [&](int ly, int lx, const T (&v)[F]) {
     if constexpr (P == 2) {  // primitive (h, v) + sqrt(g h)
       const T inv = v[0] != T(0) ? trcp(v[0]) : T(0);
@@ -463,36 +512,10 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       s_w[0][ly][lx] = v[0];
     }
   };
-  const bool pairs = !rblk && !SYNC && ((EX & 1) == 0) && (((mg - NG) & 1) == 0) && ((pw & 1) == 0);
-  if (pairs) {
-    constexpr int HX = EX / 2;
-    if (tid < HX * EY) {
-      const int ly = tid / HX, lx = 2 * (tid - ly * HX);
-      const int x = x0 + lx - NG, y = y0 + ly - NG;
-      T v0[F], v1[F];
-#pragma unroll
-      for (int f = 0; f < F; ++f) { v0[f] = T(0); v1[f] = T(0); }
-      if (y < n + NG && x < n + NG) {
-        const unsigned pa = tb + (unsigned)((y + mg) * pw + (x + mg));
-        if (x + 1 < n + NG) {
-          using V2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
-#pragma unroll
-          for (int f = 0; f < F; ++f) {
-            const V2 w = *reinterpret_cast<const V2*>(o32(a.Q + f * S, pa));
-            v0[f] = w.x; v1[f] = w.y;
-          }
-        } else {
-#pragma unroll
-          for (int f = 0; f < F; ++f) v0[f] = ld_state<SYNC>(o32(a.Q + f * S, pa));
-        }
-      }
-      put(ly, lx, v0);
-      put(ly, lx + 1, v1);
-    }
-  } else if (tid < EX * EY) {
-    const int ly = tid / EX, lx = tid - ly * EX;
+  // one window cell: zero past a partial block, a remote ghost from the
+  // receive ring, anything else from the padded state
+  auto load_win = [&](int ly, int lx, T (&v)[F]) {
     const int x = x0 + lx - NG, y = y0 + ly - NG;
-    T v[F];
 #pragma unroll
     for (int f = 0; f < F; ++f) v[f] = T(0);
     if (x < n + NG && y < n + NG) {          // false only past a partial block
@@ -550,7 +573,16 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
         for (int f = 0; f < F; ++f) v[f] = ld_state<SYNC>(o32(a.Q + f * S, pa));
       }
     }
-    put(ly, lx, v);
+  };
+  if (wly >= 0) {
+    T v[F];
+    if (own) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) v[f] = qo[f];
+    } else {
+      load_win(wly, wlx, v);
+    }
+    put(wly, wlx, v);
   }
   if constexpr (P == 2) {
     if (tid < 3 * (BX + 1)) {
@@ -561,6 +593,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       const int k = u / (BY + 1), c = u - k * (BY + 1);
       s_nrm[k][BX + 1 + c] = nrm;
     }
+    if (edge_ok) s_len[tid] = coef;   // edge lengths for the curvature balance (phase 2b)
   }
   STAMP(2);
   __syncthreads();
@@ -569,7 +602,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   // ---- 1b. PLR face values, one (cell, direction) per thread -------------------
   // task t < NFX: x-direction, cell (x0 + c - 1, y0 + r), t = r (BX + 2) + c;
   // else y-direction, cell (x0 + c, y0 + r - 1), t - NFX = r BX + c.
-  if constexpr (RECON) {
+  if constexpr (FACES) {
     const T* w0 = &s_w[0][0][0];
     // PPM: tile sides on a cube (panel) edge; cells whose 5-cell stencil
     // crosses one use MC-limited PLR faces (models/base.py::ppm_faces)
@@ -632,42 +665,52 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     if constexpr (P == 1) {
       s_fl[0][tid] = -coef * (w0[cl_ + cst] - w0[cl_]);
     } else if constexpr (P == 0) {
-      const T wl = s_fp[0][fl_], wr = s_fm[0][fl_ + fst];
+      T wl, wr;
+      if constexpr (FUSED) {
+        const T m1 = w0[cl_ - cst], c0 = w0[cl_], p1 = w0[cl_ + cst], p2 = w0[cl_ + 2 * cst];
+        wl = c0 + T(0.5) * slope<LIM>(c0 - m1, p1 - c0);
+        wr = p1 - T(0.5) * slope<LIM>(p1 - c0, p2 - p1);
+      } else {
+        wl = s_fp[0][fl_];
+        wr = s_fm[0][fl_ + fst];
+      }
       s_fl[0][tid] = coef * (coef > T(0) ? wl : wr);
     } else {
       T wl[4], wr[4], cl[5], cr[5];
 #pragma unroll
-      for (int f = 0; f < 4; ++f) { wl[f] = s_fp[f][fl_]; wr[f] = s_fm[f][fl_ + fst]; }
-#pragma unroll
       for (int f = 0; f < 5; ++f) { cl[f] = w0[f * WF + cl_]; cr[f] = w0[f * WF + cl_ + cst]; }
+      if constexpr (FUSED) {
+        // + face of the left cell and - face of the right cell (same arithmetic
+        // as the face phase: c0 +- 0.5 slope)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const T m1 = w0[f * WF + cl_ - cst], p2 = w0[f * WF + cl_ + 2 * cst];
+          wl[f] = cl[f] + T(0.5) * slope<LIM>(cl[f] - m1, cr[f] - cl[f]);
+          wr[f] = cr[f] - T(0.5) * slope<LIM>(cr[f] - cl[f], p2 - cr[f]);
+        }
+      } else {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) { wl[f] = s_fp[f][fl_]; wr[f] = s_fm[f][fl_ + fst]; }
+      }
       const int ni = is_x ? e_c : BX + 1 + e_r;
       T fl[4];
       swe_flux<T>(wl, wr, cl, cr, s_nrm[0][ni], s_nrm[1][ni], s_nrm[2][ni], coef, a.g, fl);
 #pragma unroll
       for (int f = 0; f < 4; ++f) s_fl[f][tid] = fl[f];
-      s_len[tid] = coef;
     }
   }
-  STAMP(5);
-  __syncthreads();
-  STAMP(7);
-
-  // ---- 3. divergence + sources + RK combination + push -------------------------
+  // ---- 2b. own-cell terms that need no flux: sources and the RK base ----------
+  // Done before the barrier: the own-cell waves finish their edges well before
+  // the SIMD that runs the ninth (partial) flux wave, so this is off the
+  // critical path instead of in front of the stores.
+  const int ew = oy * (BX + 1) + ox;            // west x-edge of the cell
+  const int es = NX + oy * BX + ox;             // south y-edge
+  T qs[F], base[F];
+  T src[3] = {T(0), T(0), T(0)};
   if (own) {
-    const int ew = oy * (BX + 1) + ox;          // west x-edge of the cell
-    const int es = NX + oy * BX + ox;           // south y-edge
-    T qs[F];
     if constexpr (P == 2) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) qs[f] = qo[f];
-    } else {
-      qs[0] = s_w[0][NG + oy][NG + ox];
-    }
-    T dq[F];
-#pragma unroll
-    for (int f = 0; f < F; ++f)
-      dq[f] = -((s_fl[f][ew + 1] - s_fl[f][ew]) + (s_fl[f][es + BX] - s_fl[f][es])) * iA;
-    if constexpr (P == 2) {
       const T fc = a.omega2 * r2;
       const T h = qs[0];
       const T cor[3] = {r1 * qs[3] - r2 * qs[2], r2 * qs[1] - r0 * qs[3], r0 * qs[2] - r1 * qs[1]};
@@ -677,20 +720,35 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const T Sk = Le * s_nrm[k][ox + 1] - Lw * s_nrm[k][ox] + Ln * s_nrm[k][BX + 2 + oy] - Ls * s_nrm[k][BX + 1 + oy];
-        dq[1 + k] += -fc * cor[k] + pb * Sk - gh * gb[k];
+        src[k] = -fc * cor[k] + pb * Sk - gh * gb[k];
       }
+    } else {
+      qs[0] = s_w[0][NG + oy][NG + ox];
+    }
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      base[f] = T(0);
+      if (a.a1 != T(0)) base[f] = a.a1 * qs[f];
+      if (a.a0 != T(0)) base[f] += a.a0 * xs[f];
+    }
+  }
+  STAMP(5);
+  __syncthreads();
+  STAMP(7);
+
+  // ---- 3. divergence + RK combination + push -----------------------------------
+  if (own) {
+    T dq[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+      dq[f] = -((s_fl[f][ew + 1] - s_fl[f][ew]) + (s_fl[f][es + BX] - s_fl[f][es])) * iA;
+    if constexpr (P == 2) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dq[1 + k] += src[k];
     }
     T o[F];
 #pragma unroll
-    for (int f = 0; f < F; ++f) o[f] = a.a2 * a.dt * dq[f];
-    if (a.a1 != T(0)) {
-#pragma unroll
-      for (int f = 0; f < F; ++f) o[f] += a.a1 * qs[f];
-    }
-    if (a.a0 != T(0)) {
-#pragma unroll
-      for (int f = 0; f < F; ++f) o[f] += a.a0 * xs[f];
-    }
+    for (int f = 0; f < F; ++f) o[f] = a.a2 * a.dt * dq[f] + base[f];
     if constexpr (P == 2) {
       const T d = o[1] * r0 + o[2] * r1 + o[3] * r2;
       o[1] -= d * r0; o[2] -= d * r1; o[3] -= d * r2;

@@ -51,7 +51,7 @@ def test_stage_fp64_matches_reference(name, t):
     assert _relerr(ref, hip) < 1e-11
 
 
-@pytest.mark.parametrize("block", [(16, 8), (8, 16), (32, 8)])
+@pytest.mark.parametrize("block", [(16, 16), (16, 8), (8, 16), (32, 8)])
 @pytest.mark.parametrize("name", ["swe_ppm", "swe_tc5"])
 def test_block_shapes_match_reference(name, block):
     ref, hip = _pair(name, 48, 1, torch.float64, block=block)

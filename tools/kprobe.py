@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--blocks", default="16x16,16x8,8x16,32x8,8x8")
     ap.add_argument("--limit", type=int, default=0, help="launch only this many blocks (latency probe)")
     a = ap.parse_args()
-    if a.stamps:
+    if a.stamps and not os.environ.get("STSP_VARIANT", "").startswith("diag"):
         os.environ["STSP_VARIANT"] = "diag"
     import torch
     from stsphere.engine import Engine
