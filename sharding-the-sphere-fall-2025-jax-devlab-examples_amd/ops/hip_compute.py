@@ -36,10 +36,10 @@ def choose_block(n: int, tiles: int = 0, cus: int = 0, limiter: int = 0):
     the waves a block puts on each SIMD.  So when a smaller block still fits
     the whole grid in one pass over the ``cus`` compute units, the smaller
     block wins: measured at C96 / t=2 (tools/small_grid_probe.sh,
-    profiles/r1_small_grid_block_shapes.txt), 3 tiles of 48^2 per rank take
-    5.12 us per stage with 16x16 and 4.16 us with 8x8; 12 tiles take 5.38 us
-    with 16x16 and 4.62 us with 16x8.  With more blocks than CUs the larger
-    block is better (24 tiles: 16x16 5.37 us, 8x8 5.66 us), and among the
+    profiles/r1_small_grid_block_shapes_v4.txt), 3 tiles of 48^2 per rank
+    take 4.40 us per stage with 16x16 and 3.67 us with 8x8; 12 tiles take
+    4.67 us with 16x16 and 4.05 us with 16x8.  With more blocks than CUs the
+    larger block is better (24 tiles: 16x16 4.72 us, 8x8 5.03 us), and among the
     256-cell shapes the one with the least padding waste is taken (ties ->
     16x16).  Shapes that cannot run ``limiter`` (8x8 with PPM) are skipped.
     """
