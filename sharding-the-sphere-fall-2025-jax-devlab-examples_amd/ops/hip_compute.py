@@ -28,20 +28,27 @@ def block_supports(bx: int, by: int, limiter: int) -> bool:
     return limiter != 4 or (bx + 6) * (by + 6) <= block_threads(bx, by)
 
 
-def choose_block(n: int, tiles: int = 0, cus: int = 0, limiter: int = 0):
-    """Block shape for a rank holding ``tiles`` tiles of ``n x n`` cells.
+def choose_block(n: int, tiles: int = 0, cus: int = 0, limiter: int = 0, esize: int = 8):
+    """Block shape for a rank holding ``tiles`` tiles of ``n x n`` cells
+    (``esize``: bytes per value, 8 = fp64, 4 = fp32).
 
-    A block's critical path (about 9k cycles for 16x16 fp64 SWE) is set by
-    its memory round trips plus its VALU issue, and the issue part scales with
-    the waves a block puts on each SIMD.  So when a smaller block still fits
-    the whole grid in one pass over the ``cus`` compute units, the smaller
-    block wins: measured at C96 / t=2 (tools/small_grid_probe.sh,
-    profiles/r1_small_grid_block_shapes_v4.txt), 3 tiles of 48^2 per rank
-    take 4.40 us per stage with 16x16 and 3.67 us with 8x8; 12 tiles take
-    4.67 us with 16x16 and 4.05 us with 16x8.  With more blocks than CUs the
-    larger block is better (24 tiles: 16x16 4.72 us, 8x8 5.03 us), and among the
-    256-cell shapes the one with the least padding waste is taken (ties ->
-    16x16).  Shapes that cannot run ``limiter`` (8x8 with PPM) are skipped.
+    One pass (the 16x16 grid fits the ``cus`` compute units): a block's
+    critical path is its memory round trips plus its flux and update chains,
+    and the issue part scales with the waves a block puts on each SIMD, so the
+    smallest shape that still fits in one pass wins.  Measured at C96 / t=2
+    (tools/small_grid_probe.sh, profiles/r1_small_grid_block_shapes_v4.txt):
+    3 tiles of 48^2 take 4.40 us per stage with 16x16 and 3.67 us with 8x8;
+    12 tiles 4.67 us with 16x16 and 4.05 us with 16x8; the full 24 tiles
+    (216 blocks) 4.86 us with 16x16 and 5.02-5.12 us with the smaller shapes.
+
+    Several passes: the CU hides one block's round trips and barriers behind
+    other resident blocks, and small blocks (16x8: 5 waves, 8x8: 3 waves) keep
+    more of them in flight than 16x16 (9 waves, 3 blocks = 27 of 32 wave
+    slots).  Measured per stage (profiles/r1_block_shapes_by_size.txt):
+    fp32 16x8 is best from C128 up (C720: 83.6 us vs 103.7 for 16x16);
+    fp64 16x8 up to about 8 blocks of 16x8 per CU (C180: 12.4 vs 13.8 us),
+    8x8 beyond (C256: 20.2 vs 23.8, C720: 141 vs 196 us).  Shapes that cannot
+    run ``limiter`` (8x8 with PPM) are skipped.
     """
     def count(bx, by):
         return tiles * -(-n // bx) * -(-n // by)
@@ -50,10 +57,15 @@ def choose_block(n: int, tiles: int = 0, cus: int = 0, limiter: int = 0):
         return -(-n // bx) * -(-n // by) * bx * by - n * n
 
     if tiles and cus:
-        fits = [(bx * by, waste(bx, by), count(bx, by), -bx, (bx, by)) for bx, by in BLOCK_SHAPES
-                if count(bx, by) <= cus and bx * by < 256 and block_supports(bx, by, limiter)]
-        if fits and count(16, 16) <= cus:
-            return min(fits)[-1]   # ties: the wider (contiguous-row) block
+        if count(16, 16) <= cus:
+            fits = [(bx * by, waste(bx, by), count(bx, by), -bx, (bx, by)) for bx, by in BLOCK_SHAPES
+                    if count(bx, by) <= cus and bx * by < 256 and block_supports(bx, by, limiter)]
+            if fits:
+                return min(fits)[-1]   # ties: the wider (contiguous-row) block
+            return (16, 16)
+        if esize >= 8 and count(16, 8) > 8 * cus and block_supports(8, 8, limiter):
+            return (8, 8)
+        return (16, 8)
     best, w0 = (16, 16), None
     for bx, by in BLOCK_SHAPES:
         if bx * by != 256:
@@ -78,7 +90,7 @@ class HipCompute:
         n, T = plan.n, plan.T
         if e.block is None:
             cus = torch.cuda.get_device_properties(e.device).multi_processor_count
-            bx, by = choose_block(n, T, cus, getattr(phys, "limiter", 0))
+            bx, by = choose_block(n, T, cus, getattr(phys, "limiter", 0), torch.tensor([], dtype=e.dtype).element_size())
         else:
             bx, by = e.block
         if (bx, by) not in BLOCK_SHAPES:

@@ -13,6 +13,17 @@ def test_small_rank_grids_take_smaller_blocks():
     assert choose_block(48, 3, 256, 2) == (8, 8)
 
 
+def test_multi_pass_grids_take_small_blocks():
+    # profiles/r1_block_shapes_by_size.txt: several blocks per CU -> 16x8 (fp32,
+    # mid-size fp64), 8x8 for large fp64 grids; PPM never gets 8x8
+    assert choose_block(64, 24, 256, 2, esize=4) == (16, 8)      # C128 fp32
+    assert choose_block(90, 24, 256, 2, esize=8) == (16, 8)      # C180 fp64
+    assert choose_block(128, 24, 256, 2, esize=8) == (8, 8)      # C256 fp64
+    assert choose_block(360, 24, 256, 2, esize=8) == (8, 8)      # C720 fp64
+    assert choose_block(360, 24, 256, 2, esize=4) == (16, 8)     # C720 fp32
+    assert choose_block(360, 24, 256, 4, esize=8) == (16, 8)     # PPM
+
+
 def test_ppm_never_gets_a_block_too_small_for_its_window():
     assert not block_supports(8, 8, 4) and block_supports(16, 8, 4)
     for n, t in ((48, 3), (48, 6), (12, 24), (24, 6)):
