@@ -214,6 +214,20 @@ class Solver:
                 tot[k] = tot.get(k, 0.0) + v
         return self._allreduce(tot)
 
+    def error_norms(self) -> Optional[Dict[str, float]]:
+        """Williamson l1 / l2 / linf of field 0 against the case's true
+        solution at the current time (TC1, TC2, lake at rest), on rank 0;
+        None where the case has no closed form (and on other ranks)."""
+        from .models.errors import williamson_norms
+        exact = getattr(self.physics, "exact", None)
+        h = self.global_field(0)
+        if exact is None or h is None:
+            return None
+        ht = exact(self.grid, self.time)
+        if ht is None:
+            return None
+        return williamson_norms(h, ht, self.grid.areas())
+
     def all_finite(self) -> bool:
         if self.runner is not None:
             self.runner.check()      # direct xGMI exchange: raises on a halo poll timeout
@@ -335,6 +349,9 @@ class Solver:
                    "cell_updates_per_s": 6 * self.layout.N ** 2 * nsteps / max(wall, 1e-12),
                    "sim_days_per_day": (nsteps * self.dt / DAY) / max(wall / DAY, 1e-30)}
         summary.update(self.diagnostics())
+        norms = self.error_norms()
+        if norms is not None:
+            summary.update({f"err_{k}": v for k, v in norms.items()})
         self._log(f"Run complete: {nsteps} steps, {summary['sim_days']:.3f} days, "
                   f"{summary['cell_updates_per_s']:.3e} cell-updates/s")
         return summary

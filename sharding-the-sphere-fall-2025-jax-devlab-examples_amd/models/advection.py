@@ -55,7 +55,11 @@ class Advection(Physics):
     def initial_state(self, geo: RankGeometry) -> np.ndarray:
         return geo.gather_global(self.initial_global(geo.grid))[None]
 
-    def exact(self, grid: CubedSphereGrid, t: float) -> np.ndarray:
+    def exact(self, grid: CubedSphereGrid, t: float):
+        """TC1: the bell rotated rigidly about the tilted axis; None for
+        cases without a closed form."""
+        if self.case != "cosine_bell":
+            return None
         return ic.cosine_bell_exact(grid.centers(), t, self.alpha, radius=grid.radius, u0=self._u0(grid))
 
     def setup(self, geo: RankGeometry, dtype, device) -> Dict[str, torch.Tensor]:

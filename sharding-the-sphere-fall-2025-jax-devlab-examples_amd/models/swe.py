@@ -64,6 +64,13 @@ class ShallowWater(Physics):
             raise ValueError(f"unknown SWE case {self.case!r}")
         return h, wind, b
 
+    def exact(self, grid: CubedSphereGrid, t: float):
+        """True depth h(t) where the case has one: TC2 (steady geostrophic
+        flow) and the lake at rest keep their initial depth; else None."""
+        if self.case in ("tc2", "rest"):
+            return self.global_fields(grid)[0]
+        return None
+
     def initial_state(self, geo: RankGeometry) -> np.ndarray:
         h, wind, b = self.global_fields(geo.grid)
         hl = geo.gather_global(h)

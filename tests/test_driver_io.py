@@ -88,3 +88,15 @@ def test_watchdog_recovers_from_checkpoint(tmp_path):
     s.set_dt(dt0 * 8)              # unstable from here on
     s.run(nsteps=40)               # watchdog: restore step 2, halve dt, until stable
     assert s.all_finite() and s.dt <= dt0
+
+
+def test_run_summary_reports_williamson_norms(tmp_path):
+    """TC2 has a closed-form solution (steady state): the run summary carries
+    its l1 / l2 / linf errors; TC5 has none and reports no norms."""
+    s = S.Solver(S.load_config(_cfg(tmp_path)), verbose=False)
+    out = s.run(nsteps=4)
+    assert 0 < out["err_l2"] < 1e-2 and 0 < out["err_linf"] < 1e-2 and out["err_l1"] > 0
+    c = _cfg(tmp_path)
+    c["physics"]["case"] = "tc5"
+    s5 = S.Solver(S.load_config(c), verbose=False)
+    assert "err_l2" not in s5.run(nsteps=2) and s5.error_norms() is None
