@@ -189,6 +189,7 @@ struct Args {
   unsigned long long* stamps;
   unsigned mdiv_t, mdiv_r;   // ceil(2^32 / (nbx nby)), ceil(2^32 / nbx); 0 = divide
   int diag_repeat;           // diag build only: run the block body this many extra times
+  int wt;                    // write-through output stores (st_out)
   // direct xGMI halo (XG kernels only, see stsp_kernels.h)
   int ring;
   T* const* peer_ring;
@@ -273,6 +274,19 @@ __device__ __forceinline__ void st_sys(T* p, T v) {
     __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   else
     __hip_atomic_store((gu32*)p, __builtin_bit_cast(unsigned int, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Stage output stores.  wt (block-uniform): write-through (agent-scope relaxed
+// atomic store, global_store ... sc1), so the kernel-end release has no dirty
+// L2 lines of the state to write back.  That shortens the kernel boundary on
+// latency-bound grids (C96: 15.2 -> 14.9 us/step) but costs HBM efficiency on
+// grids that stream (C360: 120 -> 221 us/step); launch_l decides per launch.
+template <bool SYNC, typename T>
+__device__ __forceinline__ void st_state(T* p, T v);
+template <bool SYNC, typename T>
+__device__ __forceinline__ void st_out(int wt, T* p, T v) {
+  if (wt) st_state<true>(p, v);
+  else st_state<SYNC>(p, v);
 }
 
 template <bool SYNC, typename T>
@@ -770,15 +784,15 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
         p[1] -= d * r0; p[2] -= d * r1; p[3] -= d * r2;
       }
 #pragma unroll
-      for (int f = 0; f < F; ++f) st_state<SYNC>(o32(a.acc_out + f * S, pc), p[f]);
+      for (int f = 0; f < F; ++f) st_out<SYNC>(a.wt, o32(a.acc_out + f * S, pc), p[f]);
     }
 #pragma unroll
-    for (int f = 0; f < F; ++f) st_state<SYNC>(o32(a.out + f * S, pc), o[f]);
+    for (int f = 0; f < F; ++f) st_out<SYNC>(a.wt, o32(a.out + f * S, pc), o[f]);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (pt[k] >= 0) {
 #pragma unroll
-        for (int f = 0; f < F; ++f) st_state<SYNC>(o32(a.out + f * S, (unsigned)pt[k]), o[f]);
+        for (int f = 0; f < F; ++f) st_out<SYNC>(a.wt, o32(a.out + f * S, (unsigned)pt[k]), o[f]);
       }
     }
     if constexpr (XG) {   // remote ghosts: straight into the consumer's ring
@@ -974,6 +988,7 @@ Args<T> make_args(const StageDesc* d) {
   a.dt = (T)d->dt; a.g = (T)d->g; a.omega2 = (T)d->omega2;
   a.stamps = (unsigned long long*)d->stamps;
   a.diag_repeat = 0;
+  a.wt = 0;
   a.ring = d->ring;
   a.peer_ring = (T* const*)d->peer_ring;
   a.peer_cnt = d->peer_cnt;
@@ -1002,10 +1017,29 @@ void set_magic(Args<T>& a) {
   a.mdiv_r = magic_div(nbx, (unsigned long long)nbx * nby);
 }
 
+// Write-through output stores pay off while the launch is latency-bound: up to
+// about 1024 cells per CU (C180 on one GPU, every multi-GPU C96 rank).
+// STSP_WT_STORES=0/1 overrides (A/B runs).
+inline bool want_wt(long cells) {
+  static const int cus = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      c = 256;
+    return c > 0 ? c : 256;
+  }();
+  static const int force = [] {
+    const char* e = std::getenv("STSP_WT_STORES");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (force >= 0) return force != 0;
+  return cells <= 1024L * cus;
+}
+
 template <typename T, int P, int BX, int BY, int LIM>
 int launch_l(const StageDesc* d, hipStream_t s) {
   Args<T> a = make_args<T>(d);
   set_magic<T, BX, BY>(a);
+  a.wt = want_wt((long)d->nblocks * BX * BY) ? 1 : 0;
 #ifdef STSP_STAMPS
   const char* rp = std::getenv("STSP_DIAG_REPEAT");
   a.diag_repeat = rp ? std::atoi(rp) : 0;
