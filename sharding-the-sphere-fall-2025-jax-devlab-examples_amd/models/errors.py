@@ -1,6 +1,8 @@
 """Williamson et al. (1992) normalised error norms (the survey's test plan,
 SURVEY.md section 4: "l1/l2/l-inf error norms versus the analytic/reference
-solution; convergence order ~2 for PLR").
+solution; convergence order ~2 for PLR").  The reference itself shows its
+advection result only as a picture (PDF s.13 / s.18: "Cosine Bell Advection,
+Initial vs Final"); these norms put a number on that comparison.
 
 For a field h and the true solution h_T on the same cells, with I(.) the
 area-weighted global integral:

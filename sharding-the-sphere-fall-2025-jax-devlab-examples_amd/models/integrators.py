@@ -2,6 +2,8 @@
 
 The reference never names its time integrator; the
 framework offers forward Euler, SSP-RK2, SSP-RK3 (default) and classical RK4.
+The slide-19 cost model counts work "per rhs eval." (PDF s.19); here every
+rhs evaluation is one stage launch.
 
 Every stage is one fused kernel launch (HIP path) computing
 

@@ -1,6 +1,7 @@
 """Single-panel shallow water on a doubly periodic f-plane (BASELINE.json
 config 1: "Single-panel 32x32 shallow-water RK4 on CPU (plumbing, no GPU, no
-halos)").
+halos)"), the "FV Cubed-Sphere Shallow Water Solver" of PY:2 reduced to one
+panel.
 
 This is the smallest end-to-end plumbing path, with the same numerics as the
 cubed-sphere solver (models/swe.py):

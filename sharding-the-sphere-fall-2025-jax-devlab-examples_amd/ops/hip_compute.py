@@ -1,6 +1,8 @@
 """HIP stage computation for ``Engine(backend='hip')``: one fused gfx950 kernel
 launch per RK stage (two when the rank has remote neighbours: interior blocks
-while the halo messages fly, boundary blocks after).
+while the halo messages fly, boundary blocks after).  The launch replaces the
+reference's XLA-generated halo ops (extract / reverse / ``.at[].set``,
+PY:166-197) and its numerics (PDF s.4, s.19: FV-PLR, 870 flops per cell).
 
 All shape contracts the kernel relies on are checked here, on the host, once,
 before anything is launched (a bad index in a hand-written kernel can reset a

@@ -5,7 +5,10 @@ list (stage kernels; for ranks with remote neighbours also pack + RCCL grouped
 send/recv on a high-priority comm stream + interior/boundary split) and hands
 stepping to C++: eager, or captured once into a hipGraph and replayed.  The
 RCCL communicator is created here (``create_nccl_comm``) and owned natively;
-torch.distributed is used only to broadcast the unique id.
+torch.distributed is used only to broadcast the unique id.  The captured graph
+plays the role of the reference's second ``jax.jit`` around the composed halo
+program (PY:238-246, PDF s.10 "Why two JITs?"): the whole step is recorded
+once and replayed without per-op host work.
 """
 from __future__ import annotations
 

@@ -9,7 +9,9 @@ workgroup keeps its block for every stage, and a stage boundary is a
 neighbour-only hand-off (sc1 write-through stores + per-block epoch flag,
 bounded polls) instead of a kernel boundary.  Single rank, SSP-RK3 (the
 stage/buffer sequence must be race-free with neighbours one stage apart,
-``integrators.persistent_safe``).
+``integrators.persistent_safe``).  Race freedom is argued per neighbour pair,
+the same structural argument as the reference's "no device appears twice in
+the same communication stage" (PDF s.9).
 """
 from __future__ import annotations
 

@@ -8,6 +8,8 @@
 All of them run on torch's current stream.  Operands must be CUDA tensors of
 one dtype (float64 or float32) whose rows are contiguous (stride(1) == 1); row
 strides are passed through, so column slices of a wider matrix work.
+These are the "r x r x r multiplies" of the slide-19 TT cost model
+(PDF s.19, s.5: TT numerics turn the memory-bound FV update compute-bound).
 """
 from __future__ import annotations
 

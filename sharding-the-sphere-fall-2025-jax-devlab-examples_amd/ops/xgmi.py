@@ -8,7 +8,9 @@ this image cannot be captured into a hipGraph (ops/native_runtime.py).
 MI355X GPUs in a node are fully connected by xGMI, and a GPU can store
 directly into a peer's HBM through a dmabuf IPC mapping.  The exchange
 therefore becomes part of the stage kernel itself (ops/csrc/stage_kernel.hip,
-XG variant):
+XG variant).  It is the explicit form of the cross-device transfer the
+reference leaves to XLA when ``exchange_edge_pair`` (PY:166-197) reads one
+sharded face and writes another:
 
 * Every rank owns one uncached allocation holding ``[world]`` u64 arrival
   counters and a 4-slot receive ring (``ring_slots x F`` values per slot).

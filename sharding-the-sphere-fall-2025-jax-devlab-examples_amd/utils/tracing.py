@@ -7,7 +7,8 @@
 
 Kernel-level evidence is collected with rocprofv3 (see tools/*.sh):
 ``rocprofv3 --kernel-trace --stats`` for per-kernel time and ``--pmc`` for
-counters (in separate runs).
+counters (in separate runs).  The reference's only performance artefact is
+the analytic roofline of PDF s.19 (utils/roofline.py).
 """
 from __future__ import annotations
 
