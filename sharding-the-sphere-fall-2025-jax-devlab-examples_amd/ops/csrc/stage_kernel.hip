@@ -167,6 +167,48 @@ __device__ __forceinline__ void load_rec8(const T* __restrict__ p, T (&r)[8]) {
   }
 }
 
+// Raw buffer access to the state and geometry arrays: one uniform resource per
+// array (4 SGPRs), the per-lane byte offset in one VGPR and the field offset
+// f * S in an SGPR (soffset).  A field costs no VALU address arithmetic: with
+// plain global pointers the compiler materialised a 64-bit VGPR address per
+// field (v_lshl_add_u64 chains, 42 in the SWE kernel) in front of every load
+// and store.  Stores take the cache policy as aux (16 = sc1, write-through).
+typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, -1, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ T bld(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  if constexpr (sizeof(T) == 8)
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
+  else
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+}
+template <int AUX, typename T>
+__device__ __forceinline__ void bst(T v, __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  if constexpr (sizeof(T) == 8)
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, v), r, (int)voff, (int)soff, AUX);
+  else
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)voff, (int)soff, AUX);
+}
+// 8-value cell record (64 B fp64 / 32 B fp32) as 16-byte buffer loads
+template <typename T>
+__device__ __forceinline__ void bld_rec8(__amdgpu_buffer_rsrc_t r, unsigned voff, T (&out)[8]) {
+  constexpr int W = 16 / sizeof(T);
+#pragma unroll
+  for (int k = 0; k < 8 / W; ++k) {
+    const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(voff + 16u * k), 0, 0);
+    if constexpr (W == 2) {
+      const double2 d = __builtin_bit_cast(double2, v);
+      out[2 * k] = (T)d.x; out[2 * k + 1] = (T)d.y;
+    } else {
+      const float4 f = __builtin_bit_cast(float4, v);
+      out[4 * k] = (T)f.x; out[4 * k + 1] = (T)f.y; out[4 * k + 2] = (T)f.z; out[4 * k + 3] = (T)f.w;
+    }
+  }
+}
+
 template <typename T>
 struct Args {
   const T* X;
@@ -353,6 +395,14 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   const int x0 = xb * BX, y0 = yb * BY;
   const int tid = threadIdx.x;
   const unsigned tb = (unsigned)(tile * pw * pw);   // padded tile base
+  // buffer resources of the state / geometry arrays (plain launches only; the
+  // persistent kernel keeps its agent-scope atomic accesses)
+  // Measured (profiles/r1_buffer_ops_ab.txt): a win for the 5- and 3-wave blocks
+  // (16x8 4.76 -> 4.62 us, 8x8 4.84 -> 4.78 us per C96 stage), a 1-2 % loss for
+  // 16x16 (4.64 -> 4.72 us), which keeps its global loads.
+  constexpr bool BUF = !SYNC && (BX * BY < 256);
+  const __amdgpu_buffer_rsrc_t rX = brsrc(a.X), rQ = brsrc(a.Q), rO = brsrc(a.out), rG = brsrc(a.cgeo);
+  constexpr unsigned ES = sizeof(T);
   const int gbase = tile * nn;                 // compact geometry base
   STAMP(0);
   // direct xGMI: the block's epoch and peer masks are issued before every other
@@ -437,17 +487,24 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   if (own) {
     if (need_x) {
 #pragma unroll
-      for (int f = 0; f < F; ++f) xs[f] = ld_state<SYNC>(o32(a.X + f * S, pc));
+      for (int f = 0; f < F; ++f) {
+        if constexpr (!BUF) xs[f] = ld_state<SYNC>(o32(a.X + f * S, pc));
+        else xs[f] = bld<T>(rX, pc * ES, (unsigned)(f * S) * ES);
+      }
     }
 #pragma unroll
-    for (int f = 0; f < F; ++f) qo[f] = ld_state<SYNC>(o32(a.Q + f * S, pc));
+    for (int f = 0; f < F; ++f) {
+      if constexpr (!BUF) qo[f] = ld_state<SYNC>(o32(a.Q + f * S, pc));
+      else qo[f] = bld<T>(rQ, pc * ES, (unsigned)(f * S) * ES);
+    }
     if (need_acc) {
 #pragma unroll
       for (int f = 0; f < F; ++f) acs[f] = ld_state<SYNC>(o32(a.acc_in + f * S, pc));
     }
     if constexpr (P == 2) {
       T rec[8];
-      load_rec8<T>(o32(a.cgeo, gc * 8u), rec);
+      if constexpr (BUF) bld_rec8<T>(rG, gc * 8u * ES, rec);
+      else load_rec8<T>(o32(a.cgeo, gc * 8u), rec);
       iA = rec[0]; r0 = rec[1]; r1 = rec[2]; r2 = rec[3];
       gb[0] = rec[4]; gb[1] = rec[5]; gb[2] = rec[6];
     } else {
@@ -584,7 +641,10 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       }
       if (!from_recv) {
 #pragma unroll
-        for (int f = 0; f < F; ++f) v[f] = ld_state<SYNC>(o32(a.Q + f * S, pa));
+        for (int f = 0; f < F; ++f) {
+          if constexpr (!BUF) v[f] = ld_state<SYNC>(o32(a.Q + f * S, pa));
+          else v[f] = bld<T>(rQ, pa * ES, (unsigned)(f * S) * ES);
+        }
       }
     }
   };
@@ -786,14 +846,23 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 #pragma unroll
       for (int f = 0; f < F; ++f) st_out<SYNC>(a.wt, o32(a.acc_out + f * S, pc), p[f]);
     }
+    // state stores (write-through when a.wt, see st_out)
+    auto put_out = [&](unsigned idx, const T (&v)[F]) {
+      if constexpr (!BUF) {
 #pragma unroll
-    for (int f = 0; f < F; ++f) st_out<SYNC>(a.wt, o32(a.out + f * S, pc), o[f]);
+        for (int f = 0; f < F; ++f) st_out<SYNC>(a.wt, o32(a.out + f * S, idx), v[f]);
+      } else if (a.wt) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) bst<16>(v[f], rO, idx * ES, (unsigned)(f * S) * ES);
+      } else {
+#pragma unroll
+        for (int f = 0; f < F; ++f) bst<0>(v[f], rO, idx * ES, (unsigned)(f * S) * ES);
+      }
+    };
+    put_out(pc, o);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (pt[k] >= 0) {
-#pragma unroll
-        for (int f = 0; f < F; ++f) st_out<SYNC>(a.wt, o32(a.out + f * S, (unsigned)pt[k]), o[f]);
-      }
+      if (pt[k] >= 0) put_out((unsigned)pt[k], o);
     }
     if constexpr (XG) {   // remote ghosts: straight into the consumer's ring
 #pragma unroll

@@ -109,3 +109,15 @@ def test_graph_replay_matches_eager():
     torch.cuda.synchronize()
     assert torch.equal(a.tiles_view(), b.tiles_view())
     assert b.step_count == 13 and math.isclose(b.time, a.time)
+
+
+@pytest.mark.parametrize("name", ["swe_tc5", "adv", "diff"])
+def test_8x8_blocks_match_reference(name):
+    """The 3-wave block (small multi-GPU rank grids, large fp64 grids) with its
+    raw-buffer state accesses, full and partial blocks (N = 48 and 20)."""
+    for N in (48, 20):
+        ref, hip = _pair(name, N, 1, torch.float64, block=(8, 8))
+        ref.step(3)
+        hip.step(3)
+        torch.cuda.synchronize()
+        assert _relerr(ref, hip) < 1e-11, N
