@@ -81,10 +81,27 @@ template <> struct Phys<0> { static constexpr int F = 1, NG = 2, FL = 1; };
 template <> struct Phys<1> { static constexpr int F = 1, NG = 1, FL = 1; };
 template <> struct Phys<2> { static constexpr int F = 4, NG = 2, FL = 5; };  // + sound speed
 
+// Ten-wave role map for 256-cell blocks (STSP_W10): SIMD s runs waves
+// {s, s+4, s+8}.  Nine waves (one per edge) left SIMD 1 with two own-cell waves
+// that also carried full flux waves, while SIMD 0 had three flux waves: the
+// slowest SIMD set both barriers.  With a tenth wave:
+//   SIMD 0: W0 flux+ring, W4 flux+ring, W8 flux
+//   SIMD 1: W1 own+flux,  W5 own,       W9 32 edges
+//   SIMD 2: W2 own+flux,  W6 flux+ring
+//   SIMD 3: W3 own+flux,  W7 flux
+// (ring = the window cells around the block, 144 for 16x16).
+// Tables: one nibble per wave (wave w at bits 4w), 0xF = no role.
+#ifndef STSP_W10
+#define STSP_W10 1
+#endif
 template <int BX, int BY> struct Geom {
   static constexpr int NX = (BX + 1) * BY;   // x-edges
   static constexpr int NY = BX * (BY + 1);   // y-edges
-  static constexpr int NT = ((NX + NY + 63) / 64) * 64;
+  static constexpr bool W10 = STSP_W10 && (BX * BY == 256) && (NX + NY <= 9 * 64 - 32);
+  static constexpr int NT = W10 ? 640 : ((NX + NY + 63) / 64) * 64;
+  static constexpr unsigned long long OWN_TAB = 0xffff1f320fULL;    // own-cell slot
+  static constexpr unsigned long long FLUX_TAB = 0x8275f16430ULL;   // flux slot: edges slot*64 + lane
+  static constexpr unsigned long long RING_TAB = 0x5432f1fff0ULL;   // ring slot (non-own waves)
 };
 
 // Hardware min/max/abs/copysign (v_max_f64, |x| source modifier, v_bfi):
@@ -414,32 +431,46 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     need = a.bmask[2 * bid];
     feed = a.bmask[2 * bid + 1];
   }
-  // Thread roles.  Waves run on SIMD (wave % 4), and SIMD 0 also carries the
-  // ninth (partial) flux wave of a 16x16 block, so the own-cell waves (prefetch,
-  // sources, update, stores) are the first BX*BY/64 waves NOT on SIMD 0:
-  // 1, 2, 3, 5 for 256 cells.  An own-cell thread puts its own cell's state
+  // Thread roles.  Waves run on SIMD (wave % 4).  256-cell blocks use the
+  // ten-wave map of Geom (STSP_W10).  Otherwise edge e is thread e, and since
+  // SIMD 0 carries the extra waves, the own-cell waves (prefetch, sources,
+  // update, stores) are the first BX*BY/64 waves NOT on SIMD 0.  An own-cell thread puts its own cell's state
   // (which it loads anyway) into the window; every other thread loads at most
   // one cell of the NG-wide ring around the block.  Measured on C96 fp64
   // (profiles/r1_c96_stage_ab.txt): splitting the window this way instead of
   // row-major 16-byte pairs in waves 0-3 took the stage from 5.52 to 5.22 us.
   constexpr int NIN = BX * BY, RING = EX * EY - NIN, NOWN = NIN / 64;
+  constexpr int NE_ = Geom<BX, BY>::NX + Geom<BX, BY>::NY;
   static_assert(NIN % 64 == 0, "own cells fill whole waves");
-  static_assert(NOWN <= NT / 64 - (NT / 64 + 3) / 4, "enough waves off SIMD 0");
+  static_assert(RING <= NT - NIN, "one ring cell per thread without an own cell");
   const int wv = tid >> 6;
+  int oid, rid, eid;    // own-cell slot, ring slot (RING: none), edge (NE_: none)
+  if constexpr (Geom<BX, BY>::W10) {
+    const int lane = tid & 63;
+    const unsigned os = (unsigned)(Geom<BX, BY>::OWN_TAB >> (4 * wv)) & 15u;
+    const unsigned fs = (unsigned)(Geom<BX, BY>::FLUX_TAB >> (4 * wv)) & 15u;
+    const unsigned rs = (unsigned)(Geom<BX, BY>::RING_TAB >> (4 * wv)) & 15u;
+    oid = os != 15u ? (int)os * 64 + lane : -1;
+    eid = fs != 15u ? (int)fs * 64 + lane : NE_;
+    rid = rs != 15u ? (int)rs * 64 + lane : RING;
+  } else {
+    static_assert(Geom<BX, BY>::W10 || NOWN <= NT / 64 - (NT / 64 + 3) / 4, "enough waves off SIMD 0");
 #if STSP_OWN_SKIP0
-  const int below = wv - (wv + 3) / 4;          // waves < wv that are not on SIMD 0
-  const int oid = ((wv & 3) != 0 && below < NOWN) ? below * 64 + (tid & 63) : -1;
+    const int below = wv - (wv + 3) / 4;          // waves < wv that are not on SIMD 0
+    oid = ((wv & 3) != 0 && below < NOWN) ? below * 64 + (tid & 63) : -1;
 #else
-  const int below = wv;                         // own cells in waves 0 .. NOWN-1
-  const int oid = wv < NOWN ? tid : -1;
+    const int below = wv;                         // own cells in waves 0 .. NOWN-1
+    oid = wv < NOWN ? tid : -1;
 #endif
+    rid = oid >= 0 ? RING : tid - 64 * (below < NOWN ? below : NOWN);
+    eid = tid;
+  }
   int wly = -1, wlx = 0;
   if (oid >= 0) {
     wly = NG + oid / BX;
     wlx = NG + oid % BX;
   } else {
-    const int r = tid - 64 * (below < NOWN ? below : NOWN);
-    static_assert(RING <= NT - NIN, "one ring cell per thread without an own cell");
+    const int r = rid;
     if (r < 2 * NG * EX) {          // NG rows above and below
       const int rr = r / EX;
       wlx = r - rr * EX;
@@ -532,12 +563,12 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     }
   }
   // (b) this thread's edge (threads < NX: x-edge, NX <= tid < NX+NY: y-edge)
-  const bool is_x = tid < NX;
-  const int ete = is_x ? tid : tid - NX;
+  const bool is_x = eid < NX;
+  const int ete = is_x ? eid : eid - NX;
   const int e_r = is_x ? ete / (BX + 1) : ete / BX;       // edge row (x) / row index (y)
   const int e_c = is_x ? ete - e_r * (BX + 1) : ete - e_r * BX;
   const int ex_ = x0 + e_c, ey_ = y0 + e_r;
-  const bool edge_ok = is_x ? (ex_ <= n && ey_ < n) : (tid < NX + NY && ex_ < n && ey_ <= n);
+  const bool edge_ok = is_x ? (ex_ <= n && ey_ < n) : (eid < NX + NY && ex_ < n && ey_ <= n);
   T coef = T(0);
   if (edge_ok) {
     coef = is_x ? *o32(a.ex, (unsigned)(tile * n * (n + 1) + ey_ * (n + 1) + ex_))
@@ -667,7 +698,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       const int k = u / (BY + 1), c = u - k * (BY + 1);
       s_nrm[k][BX + 1 + c] = nrm;
     }
-    if (edge_ok) s_len[tid] = coef;   // edge lengths for the curvature balance (phase 2b)
+    if (edge_ok) s_len[eid] = coef;   // edge lengths for the curvature balance (phase 2b)
   }
   STAMP(2);
   __syncthreads();
@@ -726,7 +757,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   }
   STAMP(4);
 
-  // ---- 2. one edge flux per thread (edge id = tid: x-edges, then y-edges) -------
+  // ---- 2. one edge flux per thread (edge id eid: x-edges, then y-edges) --------
   // x-edge (e_r, e_c) lies between cells e_c - 1 and e_c of row e_r (face tasks
   // e_r (BX + 2) + e_c and + 1); y-edge (e_r, e_c) between rows e_r - 1 and e_r
   // (face tasks NFX + e_r BX + e_c and + BX).
@@ -737,7 +768,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     const int cst = is_x ? 1 : WS;
     const T* w0 = &s_w[0][0][0];
     if constexpr (P == 1) {
-      s_fl[0][tid] = -coef * (w0[cl_ + cst] - w0[cl_]);
+      s_fl[0][eid] = -coef * (w0[cl_ + cst] - w0[cl_]);
     } else if constexpr (P == 0) {
       T wl, wr;
       if constexpr (FUSED) {
@@ -748,7 +779,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
         wl = s_fp[0][fl_];
         wr = s_fm[0][fl_ + fst];
       }
-      s_fl[0][tid] = coef * (coef > T(0) ? wl : wr);
+      s_fl[0][eid] = coef * (coef > T(0) ? wl : wr);
     } else {
       T wl[4], wr[4], cl[5], cr[5];
 #pragma unroll
@@ -770,7 +801,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       T fl[4];
       swe_flux<T>(wl, wr, cl, cr, s_nrm[0][ni], s_nrm[1][ni], s_nrm[2][ni], coef, a.g, fl);
 #pragma unroll
-      for (int f = 0; f < 4; ++f) s_fl[f][tid] = fl[f];
+      for (int f = 0; f < 4; ++f) s_fl[f][eid] = fl[f];
     }
   }
   // ---- 2b. own-cell terms that need no flux: sources and the RK base ----------
