@@ -1,0 +1,42 @@
+"""Host-side contracts of the gfx950 stage kernel that can be checked without a
+GPU: the ten-wave role tables of 256-cell blocks (ops/csrc/stage_kernel.hip,
+Geom::OWN_TAB / FLUX_TAB / RING_TAB) must give every own cell, every edge and
+every window-ring cell exactly one thread."""
+import os
+import re
+
+import pytest
+
+SRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "sharding-the-sphere-fall-2025-jax-devlab-examples_amd", "ops", "csrc", "stage_kernel.hip")
+
+
+def _tables():
+    s = open(SRC).read()
+    out = {}
+    for name in ("OWN_TAB", "FLUX_TAB", "RING_TAB"):
+        v = int(re.search(name + r" = (0x[0-9a-f]+)ULL", s).group(1), 16)
+        out[name] = [(v >> (4 * w)) & 15 for w in range(10)]
+    return out
+
+
+@pytest.mark.parametrize("bx,by,ng", [(16, 16, 2), (16, 16, 3)])
+def test_ten_wave_role_tables_cover_block(bx, by, ng):
+    t = _tables()
+    own, flux, ring = t["OWN_TAB"], t["FLUX_TAB"], t["RING_TAB"]
+    nin, ne = bx * by, (bx + 1) * by + bx * (by + 1)
+    ring_cells = (bx + 2 * ng) * (by + 2 * ng) - nin
+    lanes = range(64)
+    own_ids = sorted(o * 64 + l for o in own if o != 15 for l in lanes)
+    assert own_ids == list(range(nin))                       # every own cell once
+    edge_ids = sorted(f * 64 + l for f in flux if f != 15 for l in lanes if f * 64 + l < ne)
+    assert edge_ids == list(range(ne))                       # every edge once
+    ring_ids = sorted(r * 64 + l for w, r in enumerate(ring) if r != 15 for l in lanes)
+    assert ring_ids[:ring_cells] == list(range(ring_cells))  # every ring cell once
+    assert all(own[w] == 15 for w, r in enumerate(ring) if r != 15)   # ring only on waves without own cells
+    # SIMD balance (wave w runs on SIMD w % 4): nine flux iterations, no own-cell
+    # wave on the SIMD that runs three of them
+    iters = [sum(1 for w in range(10) if w % 4 == s and flux[w] != 15) for s in range(4)]
+    owns = [sum(1 for w in range(10) if w % 4 == s and own[w] != 15) for s in range(4)]
+    assert sum(iters) == -(-ne // 64) and max(iters) == 3
+    assert all(owns[s] == 0 for s in range(4) if iters[s] == 3)
