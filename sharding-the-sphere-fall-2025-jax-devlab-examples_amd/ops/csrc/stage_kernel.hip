@@ -94,6 +94,10 @@ template <> struct Phys<2> { static constexpr int F = 4, NG = 2, FL = 5; };  // 
 #ifndef STSP_W10
 #define STSP_W10 1
 #endif
+// Branch-free minmod / MC slopes through a sign factor (slope()).
+#ifndef STSP_SIGN_SLOPE
+#define STSP_SIGN_SLOPE 1
+#endif
 template <int BX, int BY> struct Geom {
   static constexpr int NX = (BX + 1) * BY;   // x-edges
   static constexpr int NY = BX * (BY + 1);   // y-edges
@@ -137,6 +141,14 @@ template <int LIM, typename T>
 __device__ __forceinline__ T slope(T dl, T dr) {
   if constexpr (LIM == 0) {
     return T(0.5) * (dl + dr);
+  } else if constexpr ((LIM == 1 || LIM == 2) && STSP_SIGN_SLOPE) {
+    // sign factor instead of the dl * dr > 0 test and two selects: sg is +-1
+    // when dl and dr agree in sign and 0 otherwise; the magnitude is 0 when
+    // either difference is 0, so the result equals the select form
+    const T sg = tsign(T(0.5), dl) + tsign(T(0.5), dr);
+    T m = tmin(tabs(dl), tabs(dr));
+    if constexpr (LIM == 2) m = tmin(T(2) * m, tabs(T(0.5) * (dl + dr)));
+    return sg * m;
   } else {
     const bool same = dl * dr > T(0);
     T s;
