@@ -26,7 +26,7 @@ ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
 VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgc": ["-DSTSP_XG_TAG=0"],
                  "xgf0": ["-DSTSP_XG_TAG=0", "-DSTSP_XG_FENCE=0"], "xgf2": ["-DSTSP_XG_TAG=0", "-DSTSP_XG_FENCE=2"],
                  "unfused": ["-DSTSP_FUSE_FACES=0"],
-                 "ownw0": ["-DSTSP_OWN_SKIP0=0"], "w9": ["-DSTSP_W10=0"],
+                 "ownw0": ["-DSTSP_OWN_SKIP0=0"], "w9": ["-DSTSP_W10=0"], "swsqrt": ["-DSTSP_HW_SQRT=0"],
                  "selslope": ["-DSTSP_SIGN_SLOPE=0"]}
 
 

@@ -119,8 +119,30 @@ __device__ __forceinline__ double tmax(double a, double b) { return __builtin_fm
 __device__ __forceinline__ float tmax(float a, float b) { return __builtin_fmaxf(a, b); }
 __device__ __forceinline__ double tsign(double m, double s) { return __builtin_copysign(m, s); }
 __device__ __forceinline__ float tsign(float m, float s) { return __builtin_copysignf(m, s); }
+// Sound speed sqrt(g h) for g h in [0, ~1e7]: v_rsq_f64 + one Goldschmidt
+// step + a final correction (~1 ulp, like the library expansion) without the
+// library's range scaling for denormal / huge arguments (~15 VALU ops -> ~9).
+// The bare v_sqrt_f64 is not enough: 3.6e-9 relative error in the state after
+// a few steps against the fp64 reference.
+#ifndef STSP_HW_SQRT
+#define STSP_HW_SQRT 1
+#endif
+#if STSP_HW_SQRT
+__device__ __forceinline__ double tsqrt(double x) {
+  const double r = __builtin_amdgcn_rsq(x);
+  double g = x * r, h = 0.5 * r;
+  const double e = __builtin_fma(-g, h, 0.5);
+  g = __builtin_fma(g, e, g);
+  h = __builtin_fma(h, e, h);
+  const double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  return x > 0.0 ? g : 0.0;
+}
+__device__ __forceinline__ float tsqrt(float x) { return sqrtf(x); }
+#else
 __device__ __forceinline__ double tsqrt(double x) { return sqrt(x); }
 __device__ __forceinline__ float tsqrt(float x) { return sqrtf(x); }
+#endif
 // 1/x: hardware reciprocal + two Newton steps (within an ulp of IEEE division,
 // 5 VALU ops instead of the 12-op div_scale/div_fmas/div_fixup sequence)
 __device__ __forceinline__ double trcp(double x) {
