@@ -187,6 +187,25 @@ __device__ __forceinline__ T slope(T dl, T dr) {
   }
 }
 
+// Half slope 0.5 * slope<LIM>(dl, dr), the offset from a cell average to its
+// face value, with the powers of two folded into the sign factor and the
+// limiter bound (exact: every folded factor is a power of two), so a face value
+// is one fma on top: c0 +- half_slope.
+template <int LIM, typename T>
+__device__ __forceinline__ T half_slope(T dl, T dr) {
+  if constexpr (LIM == 1 && STSP_SIGN_SLOPE) {
+    const T sg = tsign(T(0.25), dl) + tsign(T(0.25), dr);   // +-0.5 or 0
+    return sg * tmin(tabs(dl), tabs(dr));
+  } else if constexpr (LIM == 2 && STSP_SIGN_SLOPE) {
+    const T sg = tsign(T(0.5), dl) + tsign(T(0.5), dr);     // +-1 or 0
+    return sg * tmin(tmin(tabs(dl), tabs(dr)), T(0.25) * tabs(dl + dr));
+  } else if constexpr (LIM == 0) {
+    return T(0.25) * (dl + dr);
+  } else {
+    return T(0.5) * slope<LIM>(dl, dr);
+  }
+}
+
 // 16-byte vector loads (the CU's load path moves 16 B/lane at about twice the
 // byte rate of 8 B/lane).
 template <typename T> struct V16;
@@ -807,8 +826,8 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       T wl, wr;
       if constexpr (FUSED) {
         const T m1 = w0[cl_ - cst], c0 = w0[cl_], p1 = w0[cl_ + cst], p2 = w0[cl_ + 2 * cst];
-        wl = c0 + T(0.5) * slope<LIM>(c0 - m1, p1 - c0);
-        wr = p1 - T(0.5) * slope<LIM>(p1 - c0, p2 - p1);
+        wl = c0 + half_slope<LIM>(c0 - m1, p1 - c0);
+        wr = p1 - half_slope<LIM>(p1 - c0, p2 - p1);
       } else {
         wl = s_fp[0][fl_];
         wr = s_fm[0][fl_ + fst];
@@ -824,8 +843,9 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
           const T m1 = w0[f * WF + cl_ - cst], p2 = w0[f * WF + cl_ + 2 * cst];
-          wl[f] = cl[f] + T(0.5) * slope<LIM>(cl[f] - m1, cr[f] - cl[f]);
-          wr[f] = cr[f] - T(0.5) * slope<LIM>(cr[f] - cl[f], p2 - cr[f]);
+          const T d1 = cr[f] - cl[f];
+          wl[f] = cl[f] + half_slope<LIM>(cl[f] - m1, d1);
+          wr[f] = cr[f] - half_slope<LIM>(d1, p2 - cr[f]);
         }
       } else {
 #pragma unroll
