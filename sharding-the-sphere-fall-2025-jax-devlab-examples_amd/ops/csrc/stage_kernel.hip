@@ -317,13 +317,13 @@ struct Args {
 
 #ifdef STSP_STAMPS
 // Diagnostic build: lane 0 of every wave records the shader clock at phase
-// boundaries into stamps[block][wave < 16][8] (shares only; never quote a
+// boundaries into stamps[block][wave < 16][16] (shares only; never quote a
 // stamped build's run time).
 #define STAMP(k)                                                                        \
   do {                                                                                  \
     __builtin_amdgcn_sched_barrier(0);                                                  \
     if ((threadIdx.x & 63) == 0 && a.stamps)                                            \
-      a.stamps[((long)blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+      a.stamps[((long)blockIdx.x * 16 + (threadIdx.x >> 6)) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0);                                                  \
   } while (0)
 #else
@@ -944,11 +944,14 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
         for (int f = 0; f < F; ++f) bst<0>(v[f], rO, idx * ES, (unsigned)(f * S) * ES);
       }
     };
+    STAMP(8);
     put_out(pc, o);
+    STAMP(9);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (pt[k] >= 0) put_out((unsigned)pt[k], o);
     }
+    STAMP(10);
     if constexpr (XG) {   // remote ghosts: straight into the consumer's ring
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -1121,9 +1124,9 @@ __global__ __launch_bounds__((Geom<BX, BY>::NT)) void persistent_kernel(PArgs<T>
   }
 #ifdef STSP_STAMPS
   if (tid == 0 && pa.st[0].stamps) {
-    pa.st[0].stamps[(long)blockIdx.x * 128 + 0] = acc_body;
-    pa.st[0].stamps[(long)blockIdx.x * 128 + 1] = acc_drain;
-    pa.st[0].stamps[(long)blockIdx.x * 128 + 2] = acc_wait;
+    pa.st[0].stamps[(long)blockIdx.x * 256 + 0] = acc_body;
+    pa.st[0].stamps[(long)blockIdx.x * 256 + 1] = acc_drain;
+    pa.st[0].stamps[(long)blockIdx.x * 256 + 2] = acc_wait;
   }
 #endif
 }

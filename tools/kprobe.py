@@ -55,7 +55,7 @@ def main():
             d = hc.desc(st, e.dt, lst, a.limit)
         stamps = None
         if a.stamps:
-            stamps = torch.zeros(hc.nblocks * 16 * 8, dtype=torch.int64, device="cuda")
+            stamps = torch.zeros(hc.nblocks * 16 * 16, dtype=torch.int64, device="cuda")
             d.stamps = native.ptr(stamps)
         s = torch.cuda.Stream()
         with torch.cuda.stream(s):
@@ -81,13 +81,14 @@ def main():
             import numpy as np
             ne = (bx + 1) * by + bx * (by + 1)
             nw = 10 if (bx * by == 256 and ne <= 544 and os.environ.get("STSP_W9") != "1") else -(-ne // 64)   # waves per block
-            st_ = stamps.view(-1, 16, 8).cpu().numpy().astype("float64")[:, :nw]   # [block, wave, k]
+            st_ = stamps.view(-1, 16, 16).cpu().numpy().astype("float64")[:, :nw]   # [block, wave, k]
             t0_ = st_[:, :, 0].min(axis=1)                         # block start (first wave)
             rel = st_ - t0_[:, None, None]
-            names = ["start", "prefetch", "window", "barrier1", "faces+barrier", "flux", "end", "barrier2"]
+            names = ["start", "prefetch", "window", "barrier1", "faces+barrier", "flux", "end", "barrier2",
+                     "update_computed", "out_stored", "pushes_stored"]
             # median over blocks of each wave's time at each stamp, relative to block start
             r["wave_stamp_cycles_median"] = {names[k]: [float(np.median(rel[:, w, k])) for w in range(nw)]
-                                             for k in range(8)}
+                                             for k in range(len(names))}
             tot = st_[:, :, 6].max(axis=1) - t0_
             r["block_cycles_median"] = float(np.median(tot))
             r["block_cycles_max"] = float(tot.max())

@@ -15,7 +15,7 @@ from stsphere.parallel.layout import TileLayout
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 96
 e = Engine(ShallowWater("tc5"), TileLayout(N, 2, 1, ng=2), grid=CubedSphereGrid(N), device="cuda", backend="hip")
 ps = PersistentStepper(e)
-stamps = torch.zeros(e.compute.nblocks * 128, dtype=torch.int64, device="cuda")
+stamps = torch.zeros(e.compute.nblocks * 256, dtype=torch.int64, device="cuda")   # [block][16 waves][16] per-wave stamps; [block][0..2] sums
 ps._descs[0].stamps = native.ptr(stamps)
 steps = 100
 ps.run(5)
@@ -23,7 +23,7 @@ torch.cuda.synchronize()
 t0 = torch.cuda.Event(enable_timing=True); t1 = torch.cuda.Event(enable_timing=True)
 t0.record(); ps.run(steps); t1.record(); torch.cuda.synchronize()
 ps.check()
-st = stamps.view(-1, 128)[:, :8].cpu().numpy().astype(float)
+st = stamps.view(-1, 256)[:, :8].cpu().numpy().astype(float)
 nst = steps * 3
 print(json.dumps({"us_per_step": t0.elapsed_time(t1) * 1e3 / steps,
                   "cycles_per_stage_median": {"body": float(np.median(st[:, 0]) / nst),
