@@ -21,8 +21,13 @@ BLOCK_SHAPES = ((16, 16), (32, 8), (16, 8), (8, 16), (8, 8))
 
 
 def block_threads(bx: int, by: int) -> int:
-    """Threads of a stage block: one per x- and y-edge, rounded to wave64."""
-    return ((bx + 1) * by + bx * (by + 1) + 63) // 64 * 64
+    """Threads of a stage block: one per x- and y-edge, rounded to wave64;
+    256-cell blocks with at most 544 edges run the ten-wave role map
+    (stage_kernel.hip, Geom::W10)."""
+    ne = (bx + 1) * by + bx * (by + 1)
+    if bx * by == 256 and ne <= 544:
+        return 640
+    return (ne + 63) // 64 * 64
 
 
 def block_supports(bx: int, by: int, limiter: int) -> bool:
@@ -45,7 +50,7 @@ def choose_block(n: int, tiles: int = 0, cus: int = 0, limiter: int = 0, esize: 
 
     Several passes: the CU hides one block's round trips and barriers behind
     other resident blocks, and small blocks (16x8: 5 waves, 8x8: 3 waves) keep
-    more of them in flight than 16x16 (9 waves, 3 blocks = 27 of 32 wave
+    more of them in flight than 16x16 (10 waves, 3 blocks = 30 of 32 wave
     slots).  Measured per stage (profiles/r1_block_shapes_by_size.txt):
     fp32 16x8 is best from C128 up (C720: 83.6 us vs 103.7 for 16x16);
     fp64 16x8 up to about 8 blocks of 16x8 per CU (C180: 12.4 vs 13.8 us),
