@@ -195,9 +195,23 @@ class GraphStepper:
             engine.step(self.k)
         engine.pool = pool0
         engine.time, engine.step_count = t0, c0
+        self._pool0 = list(pool0)
+
+    def _sync_pool(self) -> None:
+        """The graph holds the construction-order buffer pointers; after an
+        eager remainder rotated ``e.pool`` (period > 1), copy the buffers back
+        into that order."""
+        e = self.e
+        if all(a is b for a, b in zip(e.pool, self._pool0)):
+            return
+        vals = [b.clone() for b in e.pool]
+        for b, v in zip(self._pool0, vals):
+            b.copy_(v)
+        e.pool = list(self._pool0)
 
     def run(self, nsteps: int) -> None:
         e = self.e
+        self._sync_pool()
         full, rem = divmod(nsteps, self.k)
         for _ in range(full):
             self.graph.replay()
@@ -205,6 +219,7 @@ class GraphStepper:
         e.step_count += full * self.k
         if rem:
             e.step(rem)
+            self._sync_pool()
 
 
 def assemble_global(layout: TileLayout, tiles_by_rank: Dict[int, np.ndarray]) -> np.ndarray:

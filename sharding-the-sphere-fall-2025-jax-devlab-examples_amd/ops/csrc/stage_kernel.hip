@@ -1424,3 +1424,15 @@ extern "C" int stsp_xg_prime_launch(int dtype, const void* q, int S, int F, cons
 
 extern "C" int stsp_xg_protocol(void) { return STSP_XG_TAG; }
 extern "C" int stsp_xg_slots(void) { return STSP_XG_SLOTS; }
+
+// Threads per stage block as compiled (Geom<BX, BY>::NT; depends on the
+// STSP_W10 build flag), so the host's block_threads() / PPM window check
+// describe the kernel that actually runs.  -1: unsupported shape.
+extern "C" int stsp_block_threads(int bx, int by) {
+  if (bx == 16 && by == 16) return Geom<16, 16>::NT;
+  if (bx == 32 && by == 8) return Geom<32, 8>::NT;
+  if (bx == 16 && by == 8) return Geom<16, 8>::NT;
+  if (bx == 8 && by == 16) return Geom<8, 16>::NT;
+  if (bx == 8 && by == 8) return Geom<8, 8>::NT;
+  return -1;
+}

@@ -10,6 +10,7 @@ whole node).
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional
 
 import torch
@@ -20,14 +21,38 @@ from ..models.integrators import Stage
 BLOCK_SHAPES = ((16, 16), (32, 8), (16, 8), (8, 16), (8, 8))
 
 
-def block_threads(bx: int, by: int) -> int:
+def block_threads_formula(bx: int, by: int, w10: bool = True) -> int:
     """Threads of a stage block: one per x- and y-edge, rounded to wave64;
     256-cell blocks with at most 544 edges run the ten-wave role map
-    (stage_kernel.hip, Geom::W10)."""
+    (stage_kernel.hip, Geom::W10; off in the ``w9`` library variant)."""
     ne = (bx + 1) * by + bx * (by + 1)
-    if bx * by == 256 and ne <= 544:
+    if w10 and bx * by == 256 and ne <= 544:
         return 640
     return (ne + 63) // 64 * 64
+
+
+_NT_CACHE = {}
+
+
+def block_threads(bx: int, by: int) -> int:
+    """Threads per stage block of the library that is (or would be) loaded:
+    ``stsp_block_threads`` (Geom<BX, BY>::NT as compiled) when the library is
+    present, else the formula for the selected build variant."""
+    key = (bx, by)
+    if key not in _NT_CACHE:
+        nt = -1
+        try:
+            L = native.load(build_if_missing=False)
+            L.stsp_block_threads.argtypes = [ctypes.c_int, ctypes.c_int]
+            L.stsp_block_threads.restype = ctypes.c_int
+            nt = int(L.stsp_block_threads(bx, by))
+        except (OSError, AttributeError):
+            nt = -1
+        if nt <= 0:
+            import os
+            nt = block_threads_formula(bx, by, w10=os.environ.get("STSP_VARIANT", "") != "w9")
+        _NT_CACHE[key] = nt
+    return _NT_CACHE[key]
 
 
 def block_supports(bx: int, by: int, limiter: int) -> bool:

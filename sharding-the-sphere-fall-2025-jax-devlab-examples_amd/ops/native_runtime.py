@@ -195,7 +195,10 @@ class NativeStepper:
         d.use_graph = 1 if self._cxx_graph else 0
         self.graph_periods = max(1, steps_per_graph // period)
         d.graph_periods = self.graph_periods
-        self._tg = None
+        self._graphs = {}          # periods -> torch.cuda.CUDAGraph
+        self._primed = set()       # graph lengths replayed at least once
+        self._pool0 = list(e.pool)  # construction order = the op list's buffer pointers
+        self.stats = {"graph_steps": 0, "eager_steps": 0, "replays": 0}
         self._warmed = False
         d.stream = int(self.stream.cuda_stream)
         d.nccl_comm = nccl_comm or 0
@@ -246,33 +249,105 @@ class NativeStepper:
             self.stream.wait_stream(cur)
             self._check(self.L.stsp_rt_run(self.h, nsteps), "run")
             cur.wait_stream(self.stream)
+            self.stats["eager_steps"] += nsteps
+
+    def _warm(self) -> None:
+        """Lazy one-time setup (RCCL, streams, code objects) must not happen
+        under capture: run one period eagerly on a scratch copy of the state
+        (the state, time and step count are left unchanged)."""
+        if self._warmed:
+            return
+        saved = self._save()
+        self._run_native(self.period)
+        self.stats["eager_steps"] -= self.period     # not a step of the run
+        torch.cuda.synchronize(self.e.device)
+        self._restore(saved)
+        self._warmed = True
+
+    def _save(self):
+        return [b.clone() for b in self._pool0]
+
+    def _restore(self, saved) -> None:
+        for b, s in zip(self._pool0, saved):
+            b.copy_(s)
+        torch.cuda.synchronize(self.e.device)
+        if self.xgmi is not None:
+            self.xgmi.prime()          # re-deliver the remote ghosts of the restored state (collective)
+
+    def _graph(self, periods: int):
+        """hipGraph of exactly ``periods`` integrator periods (recorded once,
+        cached by length; recorded launches carry the current dt)."""
+        g = self._graphs.get(periods)
+        if g is None:
+            self._warm()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self.stream):
+                self._check(self.L.stsp_rt_run(self.h, periods * self.period), "capture")   # recorded, not executed
+            self._graphs[periods] = g
+            self._primed.discard(periods)
+        return g
+
+    def plan(self, nsteps: int) -> List[int]:
+        """Graph lengths (in periods) that ``run(nsteps)`` replays: full
+        ``steps_per_graph`` chunks, then one graph for the remainder, so every
+        step of a run is a graph replay whatever ``nsteps`` is."""
+        periods = nsteps // self.period
+        k = self.graph_periods
+        chunks = [k] * (periods // k)
+        if periods % k:
+            chunks.append(periods % k)
+        return chunks
+
+    def prepare(self, nsteps: int, prime: bool = True) -> None:
+        """Record every graph ``run(nsteps)`` will replay and (prime=True)
+        replay each once on a scratch copy of the state, so the first timed
+        replay pays neither capture, instantiation nor upload.  The state,
+        time and step count are unchanged.  With the direct xGMI exchange this
+        is collective (the restore re-primes the rings)."""
+        if not self.use_graph or self._cxx_graph:
+            return
+        todo = []
+        for c in self.plan(nsteps):
+            self._graph(c)
+            if c not in self._primed:
+                todo.append(c)
+        if prime and todo:
+            saved = self._save()
+            for c in todo:
+                self._graphs[c].replay()
+                self._primed.add(c)
+            torch.cuda.synchronize(self.e.device)
+            self._restore(saved)
 
     def _run(self, nsteps: int) -> None:
         """nsteps (a multiple of the period)."""
         if not self.use_graph or self._cxx_graph:
             self._run_native(nsteps)
             return
-        k = self.graph_periods * self.period
-        if not self._warmed:
-            # lazy one-time setup (RCCL, streams) must not happen under capture:
-            # the first period runs eagerly and counts
-            self._run_native(self.period)
-            nsteps -= self.period
-            torch.cuda.synchronize(self.e.device)
-            self._warmed = True
-        if self._tg is None:          # record once, up front (after a set_dt: again)
-            self._tg = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._tg, stream=self.stream):
-                self._check(self.L.stsp_rt_run(self.h, k), "capture")   # recorded, not executed
-        full = nsteps // k if self._tg is not None else 0
         # replay on torch's current stream: measured 17.2 us/step at C96 there
         # against 20-21 us/step when the same graph is launched on a side stream
-        for _ in range(full):
-            self._tg.replay()
-        self._run_native(nsteps - full * k)
+        for c in self.plan(nsteps):
+            self._graph(c).replay()
+            self._primed.add(c)
+            self.stats["graph_steps"] += c * self.period
+            self.stats["replays"] += 1
+
+    def _sync_pool(self) -> None:
+        """The op list holds the buffer pointers of the construction-order
+        pool.  Engine.step rotates ``e.pool`` (period > 1 integrators), so after
+        a partial period copy the rotated buffers back into construction order
+        (a rotated pool made the next native run read stale state)."""
+        e = self.e
+        if all(a is b for a, b in zip(e.pool, self._pool0)):
+            return
+        vals = [b.clone() for b in e.pool]
+        for b, v in zip(self._pool0, vals):
+            b.copy_(v)
+        e.pool = list(self._pool0)
 
     def run(self, nsteps: int) -> None:
         e = self.e
+        self._sync_pool()
         full = (nsteps // self.period) * self.period
         if full:
             self._run(full)
@@ -280,14 +355,17 @@ class NativeStepper:
             e.step_count += full
         if nsteps - full:
             e.step(nsteps - full)
+            self.stats["eager_steps"] += nsteps - full
+            self._sync_pool()
 
     def set_dt(self, dt: float) -> None:
         self.e.dt = dt
         self._check(self.L.stsp_rt_set_dt(self.h, dt), "set_dt")
-        self._tg = None       # recorded launches carry the old dt
+        self._graphs = {}     # recorded launches carry the old dt
+        self._primed = set()
 
     def close(self) -> None:
-        self._tg = None
+        self._graphs = {}
         if getattr(self, "h", None):
             self.L.stsp_rt_destroy(self.h)
             self.h = None

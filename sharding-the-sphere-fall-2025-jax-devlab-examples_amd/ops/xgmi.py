@@ -211,35 +211,51 @@ class XgmiHalo:
         else:
             self.ring = self.xp.ring_slots * F
             nbytes = CNT_BYTES + self.slots * self.ring * self.esize
-        base = ctypes.c_void_p()
-        rc = L.stsp_xg_alloc(ctypes.c_size_t(nbytes), ctypes.byref(base))
-        if rc != 0:
-            raise RuntimeError(f"uncached allocation for the xGMI ring failed ({rc})")
-        self.base = base.value
+        self.base = None
         self.opened: List[int] = []
         peers = sorted(set(self.xp.plan.send_peers) | set(self.xp.plan.recv_peers))
-        bases = {self.rank: self.base}
+        bases = {self.rank: 0}
         distributed = dist.is_available() and dist.is_initialized() and world > 1
-        if distributed:
-            L.stsp_enable_peers(dev.index if dev.index is not None else torch.cuda.current_device())
-            hb = L.stsp_ipc_handle_bytes()
-            h = (ctypes.c_char * hb)()
-            rc = L.stsp_ipc_get(ctypes.c_void_p(self.base), h)
+        if not distributed and any(p != self.rank for p in peers):
+            raise RuntimeError("remote peers but no initialised torch.distributed group to exchange IPC handles")
+        # Every step that can fail on one rank is followed by an all-ranks
+        # agreement, so all ranks leave through the same collective sequence
+        # (a rank that raised between collectives left its peers
+        # inside a different one).
+        err = None
+        hb = L.stsp_ipc_handle_bytes()
+        h = (ctypes.c_char * hb)()
+        try:
+            base = ctypes.c_void_p()
+            rc = L.stsp_xg_alloc(ctypes.c_size_t(nbytes), ctypes.byref(base))
             if rc != 0:
-                raise RuntimeError(f"hipIpcGetMemHandle failed ({rc})")
+                raise RuntimeError(f"uncached allocation for the xGMI ring failed ({rc})")
+            self.base = base.value
+            bases[self.rank] = self.base
+            if distributed:
+                L.stsp_enable_peers(dev.index if dev.index is not None else torch.cuda.current_device())
+                rc = L.stsp_ipc_get(ctypes.c_void_p(self.base), h)
+                if rc != 0:
+                    raise RuntimeError(f"hipIpcGetMemHandle failed ({rc})")
+        except RuntimeError as exc:
+            err = exc
+        self._agreed(err, distributed)
+        if distributed:
             allh = [None] * world
             dist.all_gather_object(allh, bytes(h), group=group)
-            for p in peers:
-                if p == self.rank:
-                    continue
-                ptr = ctypes.c_void_p()
-                rc = L.stsp_ipc_open((ctypes.c_char * hb).from_buffer_copy(allh[p]), ctypes.byref(ptr))
-                if rc != 0:
-                    raise RuntimeError(f"hipIpcOpenMemHandle of rank {p} failed ({rc})")
-                self.opened.append(ptr.value)
-                bases[p] = ptr.value
-        elif any(p != self.rank for p in peers):
-            raise RuntimeError("remote peers but no initialised torch.distributed group to exchange IPC handles")
+            try:
+                for p in peers:
+                    if p == self.rank:
+                        continue
+                    ptr = ctypes.c_void_p()
+                    rc = L.stsp_ipc_open((ctypes.c_char * hb).from_buffer_copy(allh[p]), ctypes.byref(ptr))
+                    if rc != 0:
+                        raise RuntimeError(f"hipIpcOpenMemHandle of rank {p} failed ({rc})")
+                    self.opened.append(ptr.value)
+                    bases[p] = ptr.value
+            except RuntimeError as exc:
+                err = exc
+            self._agreed(err, distributed)
         pr = np.zeros(MAX_WORLD, dtype=np.int64)
         pc = np.zeros(MAX_WORLD, dtype=np.int64)
         for p, b in bases.items():
@@ -257,7 +273,22 @@ class XgmiHalo:
         assert int(self.xp.push.max(initial=-1)) < e.plan.S
         assert self.prime_src.numel() == 0 or int(self.xp.prime_src.max()) < e.plan.S
         self.timeout_ticks = int(timeout_s * 1e8)
+        self._distributed = distributed
         self.prime()
+
+    def _agreed(self, err, distributed: bool) -> None:
+        """All-ranks agreement after a local step that may have failed: every
+        rank raises (after releasing what it holds) if any rank failed."""
+        ok = err is None
+        if distributed:
+            import torch.distributed as dist
+            dev = self.e.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+            ok = bool(t.item())
+        if not ok:
+            self.close()
+            raise err if err is not None else RuntimeError("xGMI setup failed on another rank")
 
     @staticmethod
     def _check_chain(integ) -> None:
@@ -310,8 +341,9 @@ class XgmiHalo:
                                             e.physics.F, native.ptr(self.prime_src), native.ptr(self.prime_code),
                                             int(self.prime_src.numel()), native.ptr(self.peer_ring), self.ring,
                                             e0, native.current_stream_handle())
-        native.check(rc, "xGMI prime")
         torch.cuda.synchronize(e.device)
+        self._agreed(None if rc == 0 else RuntimeError(f"xGMI prime launch failed ({rc})"),
+                     dist.is_available() and dist.is_initialized() and self.world > 1)
         if dist.is_available() and dist.is_initialized() and self.world > 1:
             dist.barrier(group=self.group)
 

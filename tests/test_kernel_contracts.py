@@ -40,3 +40,20 @@ def test_ten_wave_role_tables_cover_block(bx, by, ng):
     owns = [sum(1 for w in range(10) if w % 4 == s and own[w] != 15) for s in range(4)]
     assert sum(iters) == -(-ne // 64) and max(iters) == 3
     assert all(owns[s] == 0 for s in range(4) if iters[s] == 3)
+
+
+def test_block_threads_matches_library():
+    """The host's thread count (used by the PPM window check and the launch
+    geometry) equals Geom<BX, BY>::NT of the library as built (ADVICE r1)."""
+    import ctypes
+    from stsphere.ops import build as b
+    from stsphere.ops.hip_compute import BLOCK_SHAPES, block_threads, block_threads_formula
+    if not os.path.exists(b.lib_for("")):
+        pytest.skip("library not built")
+    L = ctypes.CDLL(b.lib_for(""), mode=ctypes.RTLD_GLOBAL)
+    L.stsp_block_threads.argtypes = [ctypes.c_int, ctypes.c_int]
+    for bx, by in BLOCK_SHAPES:
+        nt = L.stsp_block_threads(bx, by)
+        assert nt == block_threads(bx, by) == block_threads_formula(bx, by)
+    assert L.stsp_block_threads(7, 7) == -1
+    assert block_threads_formula(16, 16, w10=False) == 576

@@ -39,6 +39,52 @@ def test_native_stepper_matches_engine(use_graph, integ):
     ns.close()
 
 
+@pytest.mark.parametrize("integ", ["euler", "ssprk3"])
+def test_odd_chunks_keep_runner_and_pool_in_sync(integ):
+    """run(3); run(3) == Engine.step(6) even when a chunk is not a multiple of
+    the integrator period (euler ping-pongs its buffers: ADVICE r1)."""
+    from stsphere.engine import GraphStepper
+    from stsphere.ops.native_runtime import NativeStepper
+    _, a = _single(integ=integ)
+    _, b = _single(integ=integ)
+    _, c = _single(integ=integ)
+    ns = NativeStepper(b, use_graph=True, steps_per_graph=4)
+    gs = GraphStepper(c, steps_per_graph=2)
+    a.step(6)
+    for _ in range(2):
+        ns.run(3)
+        gs.run(3)
+    torch.cuda.synchronize()
+    assert torch.equal(a.tiles_view(), b.tiles_view())
+    assert torch.equal(a.tiles_view(), c.tiles_view())
+    assert b.step_count == 6 and c.step_count == 6
+    ns.close()
+
+
+def test_short_run_replays_a_graph():
+    """run(20) with the default 30-step graph length replays recorded graphs
+    only (r1: 20 // 30 = 0 graphs, so every step ran eagerly)."""
+    from stsphere.ops.native_runtime import NativeStepper
+    _, a = _single()
+    _, b = _single()
+    ns = NativeStepper(b, use_graph=True, steps_per_graph=30)
+    ns.prepare(20)
+    assert b.step_count == 0 and torch.equal(a.tiles_view(), b.tiles_view())   # prepare leaves the state alone
+    s0 = dict(ns.stats)
+    ns.run(20)
+    a.step(20)
+    torch.cuda.synchronize()
+    assert ns.stats["eager_steps"] == s0["eager_steps"]
+    assert ns.stats["graph_steps"] - s0["graph_steps"] == 20 and ns.stats["replays"] - s0["replays"] == 1
+    assert torch.equal(a.tiles_view(), b.tiles_view())
+    ns.run(35)      # one 30-step graph + a 5-step graph
+    a.step(35)
+    torch.cuda.synchronize()
+    assert ns.stats["eager_steps"] == s0["eager_steps"]
+    assert torch.equal(a.tiles_view(), b.tiles_view())
+    ns.close()
+
+
 @pytest.fixture(scope="module")
 def nccl_comm():
     import torch.distributed as dist
