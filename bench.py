@@ -64,6 +64,7 @@ def parse(argv=None):
                          "kernels (graph-captured; default) or RCCL grouped send/recv (eager)")
     ap.add_argument("--partition", default="auto")
     ap.add_argument("--dt", type=float, default=None)
+    ap.add_argument("--block", default=None, help="stage block shape BXxBY (default: chosen per grid)")
     ap.add_argument("--no-verify", action="store_true",
                     help="N > 1: skip the bitwise comparisons with a one-GPU run")
     return ap.parse_args(argv)
@@ -180,12 +181,13 @@ def main():
                 transport = NativeBuffers(layout.plan(rank), phys.F, dtype, device)
             else:
                 transport = TorchDistTransport(layout.plan(rank), phys.F, dtype, device)
+        blk = tuple(int(v) for v in a.block.lower().split("x")) if a.block else None
         eng = Engine(phys_factory(), layout, rank, grid=grid, dtype=dtype, device=device, transport=transport,
-                     backend=backend, integrator=a.integrator, dt=a.dt)
+                     backend=backend, integrator=a.integrator, dt=a.dt, block=blk)
         runner, xg = None, None
         if runtime == "persistent":
             from stsphere.ops.persistent import PersistentStepper
-            runner = PersistentStepper(eng, timeout_s=5.0, max_steps_per_launch=max(a.steps, a.warmup, 1))
+            runner = PersistentStepper(eng, timeout_s=2.0, max_steps_per_launch=max(a.steps, a.warmup, 1))
         elif runtime == "native":
             # C++ runtime, hipGraph replay; between GPUs either direct xGMI
             # stores from the stage kernels (graph-captured) or RCCL grouped
@@ -330,7 +332,9 @@ def main():
                 "backend": backend,
                 "runtime": runtime,
                 "comm": comm,
+                "block": list((eng.compute.bx, eng.compute.by)) if hasattr(eng.compute, "bx") else None,
                 "graph_replayed_steps": timed.get("graph_steps"),
+                "persistent_steps": timed.get("persistent_steps"),
                 "eager_steps": timed.get("eager_steps"),
             },
             "simulated_days_per_day": sdpd,

@@ -92,17 +92,18 @@ def get_integrator(name: str) -> Integrator:
         raise ValueError(f"unknown integrator {name!r}; choose from {sorted(INTEGRATORS)}")
 
 
-def persistent_safe(integ: Integrator) -> bool:
-    """True if the stage sequence can run in the persistent kernel, where
-    neighbouring blocks may be one stage apart: the buffer a stage writes must
-    never be the halo-read input of the previous stage (cyclically), and the
-    step must be buffer-invariant (period 1)."""
-    if integ.period != 1:
-        return False
+def step_kernel_compatible(integ: Integrator) -> bool:
+    """True if the persistent step kernel (ops/csrc/step_kernel.hip) can run
+    the integrator with its state in registers: period 1, no accumulator,
+    at most 4 stages, every stage combines the step-start state (buffer 0)
+    with the previous stage's output (the first stage's input is buffer 0),
+    and the last stage writes buffer 0 (SSP-RK2, SSP-RK3)."""
     st = integ.stages
-    n = len(st)
-    for k in range(n):
-        nxt = st[(k + 1) % n]
-        if nxt.out == st[k].Q:
+    if integ.period != 1 or not 1 <= len(st) <= 4 or st[-1].out != 0 or st[0].Q != 0:
+        return False
+    for k, s in enumerate(st):
+        if s.X != 0 or s.acc_in >= 0 or s.acc_out >= 0:
+            return False
+        if k and s.Q != st[k - 1].out:
             return False
     return True

@@ -17,8 +17,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libstsp.so")
-SOURCES = ["stage_kernel.hip", "tt_kernels.hip", "runtime.cpp"]
-HEADERS = ["stsp_kernels.h", "runtime.h"]
+SOURCES = ["stage_kernel.hip", "step_kernel.hip", "tt_kernels.hip", "runtime.cpp"]
+HEADERS = ["stsp_kernels.h", "stage_common.h", "runtime.h"]
 ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
 # library variants: "" = production; "diag" = in-kernel phase stamps (-DSTSP_STAMPS);
 # "xgc" = the arrival-counter hand-off of the xGMI halo instead of tagged granules
@@ -27,7 +27,8 @@ VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgc": ["-DSTSP_XG_TAG=0"],
                  "xgf0": ["-DSTSP_XG_TAG=0", "-DSTSP_XG_FENCE=0"], "xgf2": ["-DSTSP_XG_TAG=0", "-DSTSP_XG_FENCE=2"],
                  "unfused": ["-DSTSP_FUSE_FACES=0"],
                  "ownw0": ["-DSTSP_OWN_SKIP0=0"], "w9": ["-DSTSP_W10=0"], "swsqrt": ["-DSTSP_HW_SQRT=0"],
-                 "selslope": ["-DSTSP_SIGN_SLOPE=0"]}
+                 "selslope": ["-DSTSP_SIGN_SLOPE=0"], "stepdbg": ["-DSTSP_STEP_DEBUG"],
+                 "stepdbg_bp": ["-DSTSP_STEP_DEBUG", "-DSTSP_STEP_BAND_PLAIN=1"]}
 
 
 def lib_for(variant: str = "") -> str:
@@ -67,7 +68,13 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     os.makedirs(odir, exist_ok=True)
     hdr_t = max([os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS if os.path.exists(os.path.join(CSRC, h))]
                 + [0.0])
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-I", CSRC,
+    # -ffp-contract=on: a*b+c is fused only inside one source expression, so
+    # every instantiation (block shape, launch-per-stage vs persistent) rounds
+    # alike and multi-rank / persistent runs stay bitwise equal to one rank
+    # (hipcc's default "fast" lets the backend fuse across statements, which
+    # depends on the surrounding code: 8x8 blocks differed by ~1 ulp).
+    flags = [f"--offload-arch={ARCH}", "-O3", "-ffp-contract=on", "-std=c++17", "-fPIC", "-Wno-unused-result",
+             "-I", CSRC,
              "-I", "/opt/rocm/include", *VARIANT_FLAGS[variant]]
     objs, procs = [], []
     for src in SOURCES:

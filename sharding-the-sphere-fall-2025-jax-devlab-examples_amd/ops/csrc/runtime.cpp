@@ -337,6 +337,21 @@ extern "C" int stsp_xg_alloc(size_t bytes, void** out) {
   return 0;
 }
 
+// Device allocation with explicit hipExtMallocWithFlags flags (zeroed):
+// 1 = fine-grained, 3 = uncached (exchange-buffer memory-type experiments).
+extern "C" int stsp_alloc_flags(size_t bytes, unsigned flags, void** out) {
+  *out = nullptr;
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, bytes, flags) != hipSuccess) return -1;
+  if (hipMemset(p, 0, bytes) != hipSuccess) {
+    hipFree(p);
+    return -2;
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return -3;
+  *out = p;
+  return 0;
+}
+
 extern "C" int stsp_xg_free(void* p) { return p && hipFree(p) != hipSuccess ? -1 : 0; }
 
 extern "C" int stsp_ipc_handle_bytes(void) { return HIP_IPC_HANDLE_SIZE; }

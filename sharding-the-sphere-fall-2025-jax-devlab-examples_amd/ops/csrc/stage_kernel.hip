@@ -26,395 +26,14 @@
 //
 // Physics (compile-time):  0 = tracer advection (PDF s.13), 1 = diffusion
 // (PDF s.12), 2 = shallow water with Cartesian momentum (PY:2).
-#include "stsp_kernels.h"
-
-// Publish protocol of the arrival-counter hand-off (STSP_XG_TAG=0 below; probe
-// variants, tools/xg_fence_probe.py, profiles/r1_xg_fence_probe.jsonl; loopback
-// C96 µs/step, plain step 17.1):
-//   0 = __threadfence_system() + release add: 117.5 (the fence is seq_cst, so
-//       every wave also invalidates L2 and the whole grid re-reads from HBM)
-//   1 = release add only (one L2 write-back per producing block): 28.6  <- default
-//   2 = relaxed add after the storing waves drain: 26.8 (relies on the ring
-//       stores being system-scope write-through; not a release in the model)
-#ifndef STSP_XG_FENCE
-#define STSP_XG_FENCE 1
-#endif
-// Halo hand-off form (stsp_kernels.h, xg fields):
-//   0 = arrival counters (drain + release add per producing block, block-level poll)
-//   1 = tagged granules: the data is the flag.  Each 32-bit word of a ghost cell
-//       travels as ONE 8-byte {tag = stage epoch + 1, payload} relaxed system-scope
-//       atomic store (single-copy atomic, so never torn); the consumer thread
-//       re-reads its cell's granules until every tag matches.  The producer
-//       neither drains nor signals, and the consumer skips the separate poll
-//       round trip (cdna_hip_programming.md Guideline 16, R2).
-//   Measured (tools/xg_tag_round.sh, profiles/r1_xg_tag_probe.jsonl, C96 fp64 µs/step):
-//   loopback 28.9 (counters) -> 24.9 (tags); two ranks sharing one GPU 26.9 -> 21.8.
-#ifndef STSP_XG_TAG
-#define STSP_XG_TAG 1
-#endif
-// Ring slots.  A rank reads slot e % S during its stage e while a peer writes
-// slot (e_p + 1) % S during its stage e_p.  A peer can have STARTED at most two
-// stages past us: its stage e + 2 needs its stage e + 1 complete, which waited
-// for our stage-e output, i.e. our stage e started and e - 1 completed.  So the
-// peer writes slot (e + 1 .. e + 3) % S, never e % S, iff S does not divide 1,
-// 2 or 3: S = 4 (three slots left a window where a peer two stages ahead
-// overwrote the slot a slow block of ours was still reading).
-#define STSP_XG_SLOTS 4
-// Own-cell waves: 1 = the first waves not on SIMD 0, 0 = waves 0 .. n-1.
-#ifndef STSP_OWN_SKIP0
-#define STSP_OWN_SKIP0 1
-#endif
-// Face reconstruction fused into the flux phase for PLR (stage_body phase 2):
-// 1 = each edge thread computes its two faces from the window; 0 = separate
-// face phase through LDS (always for PPM).
-#ifndef STSP_FUSE_FACES
-#define STSP_FUSE_FACES 1
-#endif
-
-#include <cstdlib>
-#include <type_traits>
+#include "stage_common.h"
 
 namespace {
 
-template <int P> struct Phys;
-template <> struct Phys<0> { static constexpr int F = 1, NG = 2, FL = 1; };
-template <> struct Phys<1> { static constexpr int F = 1, NG = 1, FL = 1; };
-template <> struct Phys<2> { static constexpr int F = 4, NG = 2, FL = 5; };  // + sound speed
-
-// Ten-wave role map for 256-cell blocks (STSP_W10): SIMD s runs waves
-// {s, s+4, s+8}.  Nine waves (one per edge) left SIMD 1 with two own-cell waves
-// that also carried full flux waves, while SIMD 0 had three flux waves: the
-// slowest SIMD set both barriers.  With a tenth wave:
-//   SIMD 0: W0 flux+ring, W4 flux+ring, W8 flux
-//   SIMD 1: W1 own+flux,  W5 own,       W9 32 edges
-//   SIMD 2: W2 own+flux,  W6 flux+ring
-//   SIMD 3: W3 own+flux,  W7 flux
-// (ring = the window cells around the block, 144 for 16x16).
-// Tables: one nibble per wave (wave w at bits 4w), 0xF = no role.
-#ifndef STSP_W10
-#define STSP_W10 1
-#endif
-// Branch-free minmod / MC slopes through a sign factor (slope()).
-#ifndef STSP_SIGN_SLOPE
-#define STSP_SIGN_SLOPE 1
-#endif
-template <int BX, int BY> struct Geom {
-  static constexpr int NX = (BX + 1) * BY;   // x-edges
-  static constexpr int NY = BX * (BY + 1);   // y-edges
-  static constexpr bool W10 = STSP_W10 && (BX * BY == 256) && (NX + NY <= 9 * 64 - 32);
-  static constexpr int NT = W10 ? 640 : ((NX + NY + 63) / 64) * 64;
-  static constexpr unsigned long long OWN_TAB = 0xffff1f320fULL;    // own-cell slot
-  static constexpr unsigned long long FLUX_TAB = 0x8275f16430ULL;   // flux slot: edges slot*64 + lane
-  static constexpr unsigned long long RING_TAB = 0x5432f1fff0ULL;   // ring slot (non-own waves)
-};
-
-// Hardware min/max/abs/copysign (v_max_f64, |x| source modifier, v_bfi):
-// one VALU op each where compare + select pairs cost three (wave64 fp64 and
-// integer VALU ops issue at the same 4 cycles, so every instruction counts).
-__device__ __forceinline__ double tabs(double x) { return __builtin_fabs(x); }
-__device__ __forceinline__ float tabs(float x) { return __builtin_fabsf(x); }
-__device__ __forceinline__ double tmin(double a, double b) { return __builtin_fmin(a, b); }
-__device__ __forceinline__ float tmin(float a, float b) { return __builtin_fminf(a, b); }
-__device__ __forceinline__ double tmax(double a, double b) { return __builtin_fmax(a, b); }
-__device__ __forceinline__ float tmax(float a, float b) { return __builtin_fmaxf(a, b); }
-__device__ __forceinline__ double tsign(double m, double s) { return __builtin_copysign(m, s); }
-__device__ __forceinline__ float tsign(float m, float s) { return __builtin_copysignf(m, s); }
-// Sound speed sqrt(g h) for g h in [0, ~1e7]: v_rsq_f64 + one Goldschmidt
-// step + a final correction (~1 ulp, like the library expansion) without the
-// library's range scaling for denormal / huge arguments (~15 VALU ops -> ~9).
-// The bare v_sqrt_f64 is not enough: 3.6e-9 relative error in the state after
-// a few steps against the fp64 reference.
-#ifndef STSP_HW_SQRT
-#define STSP_HW_SQRT 1
-#endif
-#if STSP_HW_SQRT
-__device__ __forceinline__ double tsqrt(double x) {
-  const double r = __builtin_amdgcn_rsq(x);
-  double g = x * r, h = 0.5 * r;
-  const double e = __builtin_fma(-g, h, 0.5);
-  g = __builtin_fma(g, e, g);
-  h = __builtin_fma(h, e, h);
-  const double d = __builtin_fma(-g, g, x);
-  g = __builtin_fma(d, h, g);
-  return x > 0.0 ? g : 0.0;
-}
-__device__ __forceinline__ float tsqrt(float x) { return sqrtf(x); }
-#else
-__device__ __forceinline__ double tsqrt(double x) { return sqrt(x); }
-__device__ __forceinline__ float tsqrt(float x) { return sqrtf(x); }
-#endif
-// 1/x: hardware reciprocal + two Newton steps (within an ulp of IEEE division,
-// 5 VALU ops instead of the 12-op div_scale/div_fmas/div_fixup sequence)
-__device__ __forceinline__ double trcp(double x) {
-  double r = __builtin_amdgcn_rcp(x);
-  double e = __builtin_fma(-x, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-x, r, 1.0);
-  return __builtin_fma(r, e, r);
-}
-__device__ __forceinline__ float trcp(float x) {
-  float r = __builtin_amdgcn_rcpf(x);
-  return __builtin_fmaf(r, __builtin_fmaf(-x, r, 1.0f), r);
-}
-
-// Limited slope, identical to models/base.py::limited_slope; LIM is a
-// compile-time constant and every form is branch-free (selects only).
-template <int LIM, typename T>
-__device__ __forceinline__ T slope(T dl, T dr) {
-  if constexpr (LIM == 0) {
-    return T(0.5) * (dl + dr);
-  } else if constexpr ((LIM == 1 || LIM == 2) && STSP_SIGN_SLOPE) {
-    // sign factor instead of the dl * dr > 0 test and two selects: sg is +-1
-    // when dl and dr agree in sign and 0 otherwise; the magnitude is 0 when
-    // either difference is 0, so the result equals the select form
-    const T sg = tsign(T(0.5), dl) + tsign(T(0.5), dr);
-    T m = tmin(tabs(dl), tabs(dr));
-    if constexpr (LIM == 2) m = tmin(T(2) * m, tabs(T(0.5) * (dl + dr)));
-    return sg * m;
-  } else {
-    const bool same = dl * dr > T(0);
-    T s;
-    if constexpr (LIM == 1) {
-      s = tsign(tmin(tabs(dl), tabs(dr)), dl);
-    } else if constexpr (LIM == 2) {
-      const T c = T(0.5) * (dl + dr);
-      s = tsign(tmin(T(2) * tmin(tabs(dl), tabs(dr)), tabs(c)), c);
-    } else {
-      const T den = same ? dl + dr : T(1);
-      s = T(2) * dl * dr / den;
-    }
-    return same ? s : T(0);
-  }
-}
-
-// Half slope 0.5 * slope<LIM>(dl, dr), the offset from a cell average to its
-// face value, with the powers of two folded into the sign factor and the
-// limiter bound (exact: every folded factor is a power of two), so a face value
-// is one fma on top: c0 +- half_slope.
-template <int LIM, typename T>
-__device__ __forceinline__ T half_slope(T dl, T dr) {
-  if constexpr (LIM == 1 && STSP_SIGN_SLOPE) {
-    const T sg = tsign(T(0.25), dl) + tsign(T(0.25), dr);   // +-0.5 or 0
-    return sg * tmin(tabs(dl), tabs(dr));
-  } else if constexpr (LIM == 2 && STSP_SIGN_SLOPE) {
-    const T sg = tsign(T(0.5), dl) + tsign(T(0.5), dr);     // +-1 or 0
-    return sg * tmin(tmin(tabs(dl), tabs(dr)), T(0.25) * tabs(dl + dr));
-  } else if constexpr (LIM == 0) {
-    return T(0.25) * (dl + dr);
-  } else {
-    return T(0.5) * slope<LIM>(dl, dr);
-  }
-}
-
-// 16-byte vector loads (the CU's load path moves 16 B/lane at about twice the
-// byte rate of 8 B/lane).
-template <typename T> struct V16;
-template <> struct V16<double> { using type = double2; static constexpr int W = 2; };
-template <> struct V16<float> { using type = float4; static constexpr int W = 4; };
-
-// base + i with a 32-bit byte offset: keeps the address in the global_load
-// saddr + voffset form (uniform 64-bit base in SGPRs, one 32-bit VGPR offset)
-// instead of a 64-bit VALU add per access.  Every buffer here is < 4 GiB.
-template <typename T>
-__device__ __forceinline__ const T* o32(const T* base, unsigned i) {
-  return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (unsigned)(i * (unsigned)sizeof(T)));
-}
-template <typename T>
-__device__ __forceinline__ T* o32(T* base, unsigned i) {
-  return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (unsigned)(i * (unsigned)sizeof(T)));
-}
-
-template <typename T>
-__device__ __forceinline__ void load_rec8(const T* __restrict__ p, T (&r)[8]) {
-  using V = typename V16<T>::type;
-  constexpr int W = V16<T>::W;
-  const V* vp = reinterpret_cast<const V*>(p);
-#pragma unroll
-  for (int k = 0; k < 8 / W; ++k) {
-    const V v = vp[k];
-    if constexpr (W == 2) { r[2 * k] = v.x; r[2 * k + 1] = v.y; }
-    else { r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w; }
-  }
-}
-
-// Raw buffer access to the state and geometry arrays: one uniform resource per
-// array (4 SGPRs), the per-lane byte offset in one VGPR and the field offset
-// f * S in an SGPR (soffset).  A field costs no VALU address arithmetic: with
-// plain global pointers the compiler materialised a 64-bit VGPR address per
-// field (v_lshl_add_u64 chains, 42 in the SWE kernel) in front of every load
-// and store.  Stores take the cache policy as aux (16 = sc1, write-through).
-typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
-typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, -1, 0x00020000);
-}
-template <typename T>
-__device__ __forceinline__ T bld(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
-  if constexpr (sizeof(T) == 8)
-    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
-  else
-    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
-}
-template <int AUX, typename T>
-__device__ __forceinline__ void bst(T v, __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
-  if constexpr (sizeof(T) == 8)
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, v), r, (int)voff, (int)soff, AUX);
-  else
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)voff, (int)soff, AUX);
-}
-// 8-value cell record (64 B fp64 / 32 B fp32) as 16-byte buffer loads
-template <typename T>
-__device__ __forceinline__ void bld_rec8(__amdgpu_buffer_rsrc_t r, unsigned voff, T (&out)[8]) {
-  constexpr int W = 16 / sizeof(T);
-#pragma unroll
-  for (int k = 0; k < 8 / W; ++k) {
-    const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(voff + 16u * k), 0, 0);
-    if constexpr (W == 2) {
-      const double2 d = __builtin_bit_cast(double2, v);
-      out[2 * k] = (T)d.x; out[2 * k + 1] = (T)d.y;
-    } else {
-      const float4 f = __builtin_bit_cast(float4, v);
-      out[4 * k] = (T)f.x; out[4 * k + 1] = (T)f.y; out[4 * k + 2] = (T)f.z; out[4 * k + 3] = (T)f.w;
-    }
-  }
-}
-
-template <typename T>
-struct Args {
-  const T* X;
-  const T* Q;
-  const T* acc_in;
-  T* out;
-  T* acc_out;
-  const T* recv;
-  const int* gmap;
-  const int* push;
-  const int* blocks;
-  const T* invA;
-  const T* ex;
-  const T* ey;
-  const T* mx;
-  const T* my;
-  const T* cgeo;
-  int ntile, n, S, mg, pw, nblocks, limiter;
-  T a0, a1, a2, c0, c1, c2, dt, g, omega2;
-  unsigned long long* stamps;
-  unsigned mdiv_t, mdiv_r;   // ceil(2^32 / (nbx nby)), ceil(2^32 / nbx); 0 = divide
-  int diag_repeat;           // diag build only: run the block body this many extra times
-  int wt;                    // write-through output stores (st_out)
-  // direct xGMI halo (XG kernels only, see stsp_kernels.h)
-  int ring;
-  T* const* peer_ring;
-  unsigned long long* const* peer_cnt;
-  const unsigned long long* cnt;
-  const unsigned long long* nprod;
-  const int* bmask;
-  int* epoch;
-  int* err;
-  long long timeout_ticks;
-  const int* pedge;
-};
-
-#ifdef STSP_STAMPS
-// Diagnostic build: lane 0 of every wave records the shader clock at phase
-// boundaries into stamps[block][wave < 16][16] (shares only; never quote a
-// stamped build's run time).
-#define STAMP(k)                                                                        \
-  do {                                                                                  \
-    __builtin_amdgcn_sched_barrier(0);                                                  \
-    if ((threadIdx.x & 63) == 0 && a.stamps)                                            \
-      a.stamps[((long)blockIdx.x * 16 + (threadIdx.x >> 6)) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
-    __builtin_amdgcn_sched_barrier(0);                                                  \
-  } while (0)
-#else
-#define STAMP(k) do {} while (0)
-#endif
-
-// Rusanov flux of the SWE along unit normal (m0,m1,m2); L = edge length.
-// wl/wr: reconstructed primitive (h, v); cl/cr: cell-average primitive + sound speed.
-template <typename T>
-__device__ __forceinline__ void swe_flux(const T (&wl)[4], const T (&wr)[4], const T (&cl)[5], const T (&cr)[5],
-                                         T m0, T m1, T m2, T L, T g, T (&f)[4]) {
-  const T hL = wl[0], hR = wr[0];
-  const T vnL = wl[1] * m0 + wl[2] * m1 + wl[3] * m2;
-  const T vnR = wr[1] * m0 + wr[2] * m1 + wr[3] * m2;
-  const T sL = tabs(cl[1] * m0 + cl[2] * m1 + cl[3] * m2) + cl[4];
-  const T sR = tabs(cr[1] * m0 + cr[2] * m1 + cr[3] * m2) + cr[4];
-  const T hc = T(0.5) * tmax(sL, sR);
-  const T pL = hL * vnL, pR = hR * vnR;
-  f[0] = (T(0.5) * (pL + pR) - hc * (hR - hL)) * L;
-  const T pr = T(0.25) * g * (hL * hL + hR * hR);
-  const T mm[3] = {m0, m1, m2};
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const T uL = hL * wl[1 + k], uR = hR * wr[1 + k];
-    f[1 + k] = (T(0.5) * (uL * vnL + uR * vnR) + pr * mm[k] - hc * (uR - uL)) * L;
-  }
-}
-
-// State access: plain in launch-per-stage kernels; in the persistent kernel,
-// agent-scope relaxed atomics, which gfx950 lowers to global_load/store ... sc1
-// (L1 bypass / write-through), the hand-off form of cdna_hip_programming.md
-// Guideline 16 (R1) measured valid for one workgroup per CU.
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) unsigned int gu32;
-
-template <bool SYNC, typename T>
-__device__ __forceinline__ T ld_state(const T* p) {
-  if constexpr (!SYNC) {
-    return *p;
-  } else if constexpr (sizeof(T) == 8) {
-    return __builtin_bit_cast(T, __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  } else {
-    return __builtin_bit_cast(T, __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  }
-}
-
-// System-scope (cross-GPU) accesses of the direct xGMI halo: sc0 sc1, i.e.
-// no GPU cache keeps a copy, so a peer's store is seen by the next poll/load.
-template <typename T>
-__device__ __forceinline__ T ld_sys(const T* p) {
-  if constexpr (sizeof(T) == 8)
-    return __builtin_bit_cast(T, __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-  else
-    return __builtin_bit_cast(T, __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-}
-
-template <typename T>
-__device__ __forceinline__ void st_sys(T* p, T v) {
-  if constexpr (sizeof(T) == 8)
-    __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  else
-    __hip_atomic_store((gu32*)p, __builtin_bit_cast(unsigned int, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Stage output stores.  wt (block-uniform): write-through (agent-scope relaxed
-// atomic store, global_store ... sc1), so the kernel-end release has no dirty
-// L2 lines of the state to write back.  That shortens the kernel boundary on
-// latency-bound grids (C96: 15.2 -> 14.9 us/step) but costs HBM efficiency on
-// grids that stream (C360: 120 -> 221 us/step); launch_l decides per launch.
-template <bool SYNC, typename T>
-__device__ __forceinline__ void st_state(T* p, T v);
-template <bool SYNC, typename T>
-__device__ __forceinline__ void st_out(int wt, T* p, T v) {
-  if (wt) st_state<true>(p, v);
-  else st_state<SYNC>(p, v);
-}
-
-template <bool SYNC, typename T>
-__device__ __forceinline__ void st_state(T* p, T v) {
-  if constexpr (!SYNC) {
-    *p = v;
-  } else if constexpr (sizeof(T) == 8) {
-    __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    __hip_atomic_store((gu32*)p, __builtin_bit_cast(unsigned int, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// One RK stage of one BX x BY block (all phases).  SYNC = persistent-kernel
-// mode: every access to state written by other workgroups in this launch is an
-// agent-scope sc1 access (L1 bypass, write-through), see persistent_kernel.
+// One RK stage of one BX x BY block (all phases).  SYNC: every access to state
+// written by other workgroups in this launch is an agent-scope sc1 access (L1
+// bypass, write-through); the launch-per-stage kernels use SYNC = false (the
+// persistent step kernel, step_kernel.hip, hands its halos off as granules).
 // XG = direct xGMI halo: a block reads its remote ghosts from this rank's
 // receive ring (slot epoch % STSP_XG_SLOTS) once they have arrived (tags match,
 // or the peers' arrival counters are complete), and every block stores the cells
@@ -1002,27 +621,6 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 }
 
 
-// XCD-aware bijective remap: logical blocks [k*nb/8, ...) share one XCD
-// (blocks b and b+8 are dealt to the same XCD), so neighbouring blocks, which
-// share halo cells, share an L2.  Speed only, never correctness.
-__device__ __forceinline__ int xcd_remap(int orig, int nb) {
-  const int xcd = orig & 7, q = nb >> 3, r = nb & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-}
-
-template <typename T>
-__device__ __forceinline__ void pin_args(const Args<T>& a) {
-  // Pin every kernel argument in SGPRs here: hipcc otherwise issues the
-  // kernarg scalar loads lazily, each behind its own lgkmcnt(0) (3-4 serial
-  // round trips in the prologue, seen with in-kernel stamps).
-  asm volatile("" ::"s"(a.X), "s"(a.Q), "s"(a.acc_in), "s"(a.out), "s"(a.acc_out), "s"(a.recv), "s"(a.gmap),
-               "s"(a.push), "s"(a.blocks));
-  asm volatile("" ::"s"(a.invA), "s"(a.ex), "s"(a.ey), "s"(a.mx), "s"(a.my), "s"(a.cgeo));
-  asm volatile("" ::"s"(a.ntile), "s"(a.n), "s"(a.S), "s"(a.mg), "s"(a.pw), "s"(a.nblocks));
-  asm volatile("" ::"s"(a.a0), "s"(a.a1), "s"(a.a2), "s"(a.c0), "s"(a.c1), "s"(a.c2), "s"(a.dt), "s"(a.g),
-               "s"(a.omega2));
-}
-
 template <typename T, int P, int BX, int BY, int LIM, bool REMOTE, bool LIST, bool XG>
 __global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
   pin_args(a);
@@ -1036,160 +634,6 @@ __global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
     stage_body<T, P, BX, BY, LIM, REMOTE, false, XG>(a, bid);
   }
 #endif
-}
-
-// ---- persistent multi-step kernel (small grids) --------------------------------
-// One workgroup per CU, all co-resident (checked by the cooperative launch).
-// Each workgroup runs every stage of `nsteps` steps for its block; a stage
-// boundary is a neighbour-only hand-off instead of a kernel boundary:
-//   publish: all state stores are sc1 (write-through) -> every wave
-//            s_waitcnt vmcnt(0) -> barrier -> lane 0 stores flag[bid] = epoch (sc1)
-//   consume: lanes 0..nn-1 poll the flags of the blocks whose output this block
-//            reads (sc1 loads, s_sleep, bounded by a wall-clock timeout) -> barrier
-// so no block ever waits on the whole grid.  Any timeout sets *err and every
-// block drains out (no hang).
-template <typename T>
-struct PArgs {
-  Args<T> st[4];        // stage descriptors of one step (buffer-invariant period)
-  int nstages;
-  int nsteps;
-  unsigned* flags;      // [nblocks] epochs, zeroed before the launch
-  const int* nbr;       // [nblocks][maxnbr] producer blocks (-1 padded)
-  int maxnbr;
-  int* err;             // 0 ok; 1 timeout
-  unsigned long long timeout_ticks;   // s_memrealtime ticks (100 MHz)
-};
-
-__device__ __forceinline__ unsigned flag_load(const unsigned* p) {
-  return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <typename T, int P, int BX, int BY, int LIM>
-__global__ __launch_bounds__((Geom<BX, BY>::NT)) void persistent_kernel(PArgs<T> pa) {
-  pin_args(pa.st[0]);
-  const int bid = xcd_remap(blockIdx.x, pa.st[0].nblocks);
-  const int tid = threadIdx.x;
-  __shared__ int s_abort;
-  if (tid == 0) s_abort = 0;
-  __syncthreads();
-  unsigned epoch = 0;
-#ifdef STSP_STAMPS
-  unsigned long long acc_body = 0, acc_drain = 0, acc_wait = 0, tA = 0, tB = 0, tC = 0;
-#endif
-  for (int step = 0; step < pa.nsteps; ++step) {
-    for (int s = 0; s < pa.nstages; ++s) {
-#ifdef STSP_STAMPS
-      if (tid == 0) tA = __builtin_amdgcn_s_memtime();
-#endif
-      stage_body<T, P, BX, BY, LIM, false, true>(pa.st[s], bid);
-#ifdef STSP_STAMPS
-      if (tid == 0) tB = __builtin_amdgcn_s_memtime();
-#endif
-      // -- publish this block's stage output
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-#ifdef STSP_STAMPS
-      if (tid == 0) tC = __builtin_amdgcn_s_memtime();
-#endif
-      ++epoch;
-      if (tid == 0) __hip_atomic_store((gu32*)&pa.flags[bid], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // -- wait for every producer of the next stage's window
-      if (tid < pa.maxnbr) {
-        const int nb = pa.nbr[bid * pa.maxnbr + tid];
-        if (nb >= 0) {
-          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-          while (flag_load(&pa.flags[nb]) < epoch) {
-            if (__hip_atomic_load((gu32*)pa.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-              s_abort = 1;
-              break;
-            }
-            if (__builtin_amdgcn_s_memrealtime() - t0 > pa.timeout_ticks) {
-              __hip_atomic_store((gu32*)pa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              s_abort = 1;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-          }
-        }
-      }
-      __syncthreads();
-#ifdef STSP_STAMPS
-      if (tid == 0) {
-        const unsigned long long tD = __builtin_amdgcn_s_memtime();
-        acc_body += tB - tA; acc_drain += tC - tB; acc_wait += tD - tC;
-      }
-#endif
-      if (s_abort) return;
-    }
-  }
-#ifdef STSP_STAMPS
-  if (tid == 0 && pa.st[0].stamps) {
-    pa.st[0].stamps[(long)blockIdx.x * 256 + 0] = acc_body;
-    pa.st[0].stamps[(long)blockIdx.x * 256 + 1] = acc_drain;
-    pa.st[0].stamps[(long)blockIdx.x * 256 + 2] = acc_wait;
-  }
-#endif
-}
-
-template <typename T>
-Args<T> make_args(const StageDesc* d) {
-  Args<T> a;
-  a.X = (const T*)d->X; a.Q = (const T*)d->Q; a.acc_in = (const T*)d->acc_in;
-  a.out = (T*)d->out; a.acc_out = (T*)d->acc_out; a.recv = (const T*)d->recv;
-  a.gmap = d->gmap; a.push = d->push; a.blocks = d->blocks;
-  a.invA = (const T*)d->invA; a.ex = (const T*)d->ex; a.ey = (const T*)d->ey;
-  a.mx = (const T*)d->mx; a.my = (const T*)d->my; a.cgeo = (const T*)d->cgeo;
-  a.ntile = d->ntile; a.n = d->n; a.S = d->S; a.mg = d->mg; a.pw = d->pw; a.nblocks = d->nblocks;
-  a.limiter = d->limiter;
-  a.a0 = (T)d->a0; a.a1 = (T)d->a1; a.a2 = (T)d->a2; a.c0 = (T)d->c0; a.c1 = (T)d->c1; a.c2 = (T)d->c2;
-  a.dt = (T)d->dt; a.g = (T)d->g; a.omega2 = (T)d->omega2;
-  a.stamps = (unsigned long long*)d->stamps;
-  a.diag_repeat = 0;
-  a.wt = 0;
-  a.ring = d->ring;
-  a.peer_ring = (T* const*)d->peer_ring;
-  a.peer_cnt = d->peer_cnt;
-  a.cnt = d->cnt;
-  a.nprod = d->nprod;
-  a.bmask = d->bmask;
-  a.epoch = d->epoch;
-  a.err = d->err;
-  a.timeout_ticks = d->timeout_ticks;
-  a.pedge = d->pedge;
-  return a;
-}
-
-// ceil(2^32 / dv) if floor(x * M / 2^32) == x / dv for every x < xmax (holds
-// when xmax * dv <= 2^32: the rounding excess x (M dv - 2^32) / 2^32 < 1), else 0.
-inline unsigned magic_div(unsigned dv, unsigned long long xmax) {
-  if (dv <= 1 || xmax * dv > (1ull << 32)) return 0;
-  return (unsigned)(((1ull << 32) + dv - 1) / dv);
-}
-
-template <typename T, int BX, int BY>
-void set_magic(Args<T>& a) {
-  const unsigned nbx = (a.n + BX - 1) / BX, nby = (a.n + BY - 1) / BY;
-  const unsigned long long total = (unsigned long long)a.ntile * nbx * nby;
-  a.mdiv_t = magic_div(nbx * nby, total);
-  a.mdiv_r = magic_div(nbx, (unsigned long long)nbx * nby);
-}
-
-// Write-through output stores pay off while the launch is latency-bound: up to
-// about 1024 cells per CU (C180 on one GPU, every multi-GPU C96 rank).
-// STSP_WT_STORES=0/1 overrides (A/B runs).
-inline bool want_wt(long cells) {
-  static const int cus = [] {
-    int dev = 0, c = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      c = 256;
-    return c > 0 ? c : 256;
-  }();
-  static const int force = [] {
-    const char* e = std::getenv("STSP_WT_STORES");
-    return e ? std::atoi(e) : -1;
-  }();
-  if (force >= 0) return force != 0;
-  return cells <= 1024L * cus;
 }
 
 template <typename T, int P, int BX, int BY, int LIM>
@@ -1309,72 +753,7 @@ __global__ __launch_bounds__(256) void copy_index_kernel(const T* __restrict__ s
   dst[b * ds + didx[i]] = src[b * ss + sidx[i]];
 }
 
-template <typename T, int P, int BX, int BY, int LIM>
-int launch_persist(const StageDesc* st, int nstages, int nsteps, unsigned* flags, const int* nbr, int maxnbr,
-                   int* err, double timeout_s, hipStream_t s) {
-  PArgs<T> pa;
-  for (int k = 0; k < nstages; ++k) {
-    pa.st[k] = make_args<T>(&st[k]);
-    set_magic<T, BX, BY>(pa.st[k]);
-  }
-  pa.nstages = nstages;
-  pa.nsteps = nsteps;
-  pa.flags = flags;
-  pa.nbr = nbr;
-  pa.maxnbr = maxnbr;
-  pa.err = err;
-  pa.timeout_ticks = (unsigned long long)(timeout_s * 1e8);
-  const int nb = st[0].nblocks;
-  hipError_t e = hipMemsetAsync(flags, 0, sizeof(unsigned) * ((nb + 3) & ~3), s);
-  if (e != hipSuccess) return (int)e;
-  void* args[] = {&pa};
-  e = hipLaunchCooperativeKernel((const void*)persistent_kernel<T, P, BX, BY, LIM>, dim3(nb),
-                                 dim3(Geom<BX, BY>::NT), args, 0, s);
-  return (int)e;
-}
-
-template <typename T, int P>
-int persist_p(int bx, int by, const StageDesc* st, int nstages, int nsteps, unsigned* flags, const int* nbr,
-              int maxnbr, int* err, double timeout_s, hipStream_t s) {
-  if (bx != 16 || by != 16) return -2;
-  if (P == 1) return launch_persist<T, P, 16, 16, 0>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
-  switch (st[0].limiter) {
-    case 0: return launch_persist<T, P, 16, 16, 0>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
-    case 1: return launch_persist<T, P, 16, 16, 1>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
-    case 2: return launch_persist<T, P, 16, 16, 2>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
-    case 3: return launch_persist<T, P, 16, 16, 3>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
-    case 4: return launch_persist<T, P, 16, 16, 4>(st, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, s);
-  }
-  return -7;
-}
-
 }  // namespace
-
-extern "C" int stsp_persistent_launch(int phys, int dtype, int bx, int by, const StageDesc* stages, int nstages,
-                                      int nsteps, unsigned* flags, const int* nbr, int maxnbr, int* err,
-                                      double timeout_s, hipStream_t stream) {
-  if (nstages < 1 || nstages > 4 || nsteps < 1) return -8;
-  for (int k = 0; k < nstages; ++k) {
-    const StageDesc* d = &stages[k];
-    if (d->blocks || d->remote || !d->push || d->pw != d->n + 2 * d->mg) return -6;
-    if (d->limiter == 4 && (d->mg < 3 || !d->pedge)) return -5;
-    if (d->nblocks != stages[0].nblocks) return -9;
-  }
-  if (dtype == 1) {
-    switch (phys) {
-      case 0: return persist_p<double, 0>(bx, by, stages, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, stream);
-      case 1: return persist_p<double, 1>(bx, by, stages, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, stream);
-      case 2: return persist_p<double, 2>(bx, by, stages, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, stream);
-    }
-  } else if (dtype == 0) {
-    switch (phys) {
-      case 0: return persist_p<float, 0>(bx, by, stages, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, stream);
-      case 1: return persist_p<float, 1>(bx, by, stages, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, stream);
-      case 2: return persist_p<float, 2>(bx, by, stages, nstages, nsteps, flags, nbr, maxnbr, err, timeout_s, stream);
-    }
-  }
-  return -3;
-}
 
 extern "C" int stsp_stage_launch(int phys, int dtype, int bx, int by, const StageDesc* d, hipStream_t stream) {
   if (dtype == 1) return launch_d<double>(phys, bx, by, d, stream);

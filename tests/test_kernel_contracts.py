@@ -1,6 +1,6 @@
 """Host-side contracts of the gfx950 stage kernel that can be checked without a
 GPU: the ten-wave role tables of 256-cell blocks (ops/csrc/stage_kernel.hip,
-Geom::OWN_TAB / FLUX_TAB / RING_TAB) must give every own cell, every edge and
+Geom::OWN_TAB / FLUX_TAB / RING_TAB in stage_common.h) must give every own cell, every edge and
 every window-ring cell exactly one thread."""
 import os
 import re
@@ -8,7 +8,7 @@ import re
 import pytest
 
 SRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                   "sharding-the-sphere-fall-2025-jax-devlab-examples_amd", "ops", "csrc", "stage_kernel.hip")
+                   "sharding-the-sphere-fall-2025-jax-devlab-examples_amd", "ops", "csrc", "stage_common.h")
 
 
 def _tables():
