@@ -159,10 +159,13 @@ def main():
         comm = "xgmi" if world > 1 else "none"
     spg = a.steps_per_graph if a.steps_per_graph > 0 else a.steps
 
+    # collectives on CUDA tensors with RCCL, on CPU tensors with gloo
+    cdev = device if (world > 1 and dist.get_backend() == "nccl") else torch.device("cpu")
+
     def agree(ok: bool) -> bool:
         if world == 1:
             return ok
-        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return bool(t.item())
 
@@ -236,7 +239,7 @@ def main():
     def diff_vs_1gpu(eng, nsteps):
         """max |multi-rank - one rank| after nsteps (0.0 = bitwise), on every rank."""
         got = gathered(eng)
-        d = torch.zeros(1, dtype=torch.float64, device=device)
+        d = torch.zeros(1, dtype=torch.float64, device=cdev)
         if rank == 0:
             want = single_rank_reference(a, phys_factory, grid, dtype, device, eng.dt, ng, nsteps, runtime, backend)
             d[0] = float(np.abs(got - want).max())
@@ -286,7 +289,7 @@ def main():
     stats1 = dict(getattr(runner, "stats", {}))
     timed = {k: stats1[k] - stats0.get(k, 0) for k in stats1}
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     if hasattr(runner, "check"):
@@ -296,7 +299,7 @@ def main():
         raise SystemExit(f"[bench] timed region was not a pure graph replay: {timed}")
     diag = eng.diagnostics()
     if world > 1:
-        t = torch.tensor([diag.get("mass", 0.0)], dtype=torch.float64, device=device)
+        t = torch.tensor([diag.get("mass", 0.0)], dtype=torch.float64, device=cdev)
         dist.all_reduce(t)
         diag["mass"] = float(t.item())
     finite = bool(torch.isfinite(eng.tiles_view()).all().item())
