@@ -136,6 +136,11 @@ class PersistentStepper:
         self.e = e
         self.L = _lib()
         lim = int(e.physics.kernel_params().get("limiter", 0))
+        if lim == 4:
+            # measured on MI355X (round 2): the PPM instantiation differs from
+            # launch-per-stage stepping after a few launches; until that is
+            # understood the persistent path is PLR-only
+            raise NotImplementedError("persistent stepping supports PLR limiters only (not PPM)")
         maxb = self.L.stsp_step_max_blocks(hc.phys_id, hc.dcode, hc.bx, hc.by, lim)
         if maxb <= 0:
             raise RuntimeError(f"step kernel not available for this configuration ({maxb})")

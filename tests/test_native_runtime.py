@@ -131,7 +131,6 @@ def test_rccl_loopback_full_multigpu_path(nccl_comm, use_graph, phys):
     (96, 2, "swe", torch.float64, "ssprk3", (16, 16), 2),
     (48, 2, "swe", torch.float64, "ssprk3", (16, 8), 2),
     (48, 2, "swe", torch.float64, "ssprk2", (8, 8), 1),
-    (48, 1, "swe", torch.float64, "ssprk3", (16, 16), 4),      # PPM, 3-layer window
     (40, 2, "swe", torch.float64, "ssprk3", (16, 16), 2),      # partial blocks (n = 20)
     (48, 1, "adv", torch.float64, "ssprk3", (16, 16), 2),
     (32, 2, "diff", torch.float64, "ssprk3", (16, 8), 0),
@@ -161,6 +160,15 @@ def test_persistent_step_kernel_matches_launch_per_stage(N, t, phys, dtype, inte
         assert torch.equal(a.pool[0], b.pool[0])
     else:   # fp32 (-ffp-contract=on: every instantiation rounds alike)
         assert torch.equal(a.tiles_view(), b.tiles_view())
+
+
+def test_persistent_refuses_ppm():
+    """PPM is not supported by the persistent step kernel (PLR only)."""
+    from stsphere.ops.persistent import PersistentStepper
+    g = CubedSphereGrid(48)
+    e = Engine(ShallowWater("tc5", limiter=4), TileLayout(48, 1, 1, ng=3), grid=g, device="cuda", backend="hip")
+    with pytest.raises(NotImplementedError, match="PPM"):
+        PersistentStepper(e)
 
 
 def test_persistent_refuses_grids_that_cannot_be_co_resident():
