@@ -4,7 +4,8 @@
     info CONFIG.yaml                                   validate config, print sharding + halo plan
     schedule                                           print the reference 4-stage halo schedule
     roofline                                           slide-19 roofline / TT model for MI355X
-    plot HISTORY.zarr FIELD OUTDIR [--log]             render history frames
+    plot HISTORY.zarr FIELD OUTDIR [--log] [--products frames,band,six] [--every K]
+                                                       sphere frames, equatorial band, six-panel
     build                                              compile the gfx950 library
 """
 import argparse
@@ -30,6 +31,8 @@ def main(argv=None):
     p.add_argument("field")
     p.add_argument("outdir")
     p.add_argument("--log", action="store_true")
+    p.add_argument("--products", default="frames,band,six")
+    p.add_argument("--every", type=int, default=1)
     sub.add_parser("build")
     a = ap.parse_args(argv)
 
@@ -48,11 +51,9 @@ def main(argv=None):
         print(report())
         return 0
     if a.cmd == "plot":
-        from .models.geometry import CubedSphereGrid
-        from .utils import zarr_lite
-        from .utils.viz import history_frames
-        N = int(zarr_lite.read_attrs(a.history)["N"])
-        for f in history_frames(a.history, a.field, CubedSphereGrid(N), a.outdir, log=a.log):
+        from .utils.viz import history_products
+        for f in history_products(a.history, a.field, a.outdir, log=a.log, every=a.every,
+                                  products=tuple(a.products.split(","))):
             print(f)
         return 0
     from .utils.config import load_config
@@ -73,15 +74,20 @@ def main(argv=None):
         return 0
     s.initialize()
     summary = s.run(nsteps=a.nsteps, days=a.days)
+    g = s.gather_global() if a.plot else None     # collective under SPMD
     if s.rank == 0:
         print(json.dumps(summary, default=float))
         if a.plot:
-            from .utils.viz import six_panel, sphere_plot
-            g = s.gather_global()
+            from .utils.viz import history_products, sphere_plot
             out = s.cfg.io.output_dir
             os.makedirs(out, exist_ok=True)
-            print(sphere_plot(g[0], s.grid, os.path.join(out, f"{s.fields[0]}_final.png"),
-                              log=s.physics.name == "diffusion"))
+            hist = os.path.join(out, "history.zarr")
+            log = s.physics.name == "diffusion"
+            if os.path.exists(os.path.join(hist, ".zgroup")):
+                for f in history_products(hist, s.fields[0], os.path.join(out, "plots"), grid=s.grid, log=log,
+                                          products=("band", "six")):
+                    print(f)
+            print(sphere_plot(g[0], s.grid, os.path.join(out, f"{s.fields[0]}_final.png"), log=log))
     return 0
 
 

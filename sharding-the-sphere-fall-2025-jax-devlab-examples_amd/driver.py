@@ -126,7 +126,7 @@ class Solver:
         phys0 = make_physics(c.physics)
         # PPM reads three ghost layers: widen the halo if the config asks for fewer
         self.layout = TileLayout(N, t, nd, ng=max(c.grid.halo, phys0.halo), owner=self.sharding.owner)
-        self.grid = CubedSphereGrid(N, c.grid.radius or EARTH_RADIUS)
+        self.grid = self._geometry_stage(N, c.grid.radius or EARTH_RADIUS)
         dt = c.time.dt or (phys0.max_dt(self.grid, c.time.cfl) if c.time.cfl else phys0.max_dt(self.grid))
         kw = dict(grid=self.grid, dtype=dtype, device=device, backend=backend, integrator=c.time.integrator, dt=dt)
         if c.runtime.block:
@@ -157,12 +157,58 @@ class Solver:
         self.fields = list(phys0.fields)
         self._log(f"Initialized {phys0.name} ({getattr(phys0, 'case', '')}) C{N}, {self.mode} mode, "
                   f"backend={backend}, dtype={c.grid.dtype}, dt={dt:.3f} s, integrator={c.time.integrator}")
+        if c.io.initial_condition and not c.io.restore:
+            self._initial_condition_stage(c.io.initial_condition)
         if c.io.restore:
             path = c.io.restore
             if path == "latest":
                 path = ckpt.latest_checkpoint(self.checkpoint_root())
             if path:
                 self.restore_checkpoint(path)
+
+    # ---- pipeline stages: Geometry and Initial Conditions through zarr (PDF s.6) ----
+    def _geometry_stage(self, N: int, radius: float) -> CubedSphereGrid:
+        """Read the grid from ``io.geometry`` when that zarr group exists, else
+        compute it and (rank 0) write it there."""
+        path = self.cfg.io.geometry
+        if path and os.path.exists(os.path.join(path, ".zgroup")):
+            g = CubedSphereGrid.load_zarr(path, N=N, radius=radius)
+            self._log(f"Geometry: read C{N} grid from {path}")
+            return g
+        g = CubedSphereGrid(N, radius)
+        if path:
+            if self.rank == 0:
+                g.save_zarr(path)
+                self._log(f"Geometry: wrote C{N} grid to {path}")
+            self._barrier()
+        return g
+
+    def _initial_condition_stage(self, path: str) -> None:
+        """Read the initial state [F, 6, N, N] from ``io.initial_condition``
+        when that zarr group exists, else (rank 0) write the analytic initial
+        condition the engines were built with.  Partition-independent, like
+        checkpoints."""
+        from .utils import zarr_lite
+        if os.path.exists(os.path.join(path, ".zgroup")):
+            attrs = zarr_lite.read_attrs(path)
+            if int(attrs["N"]) != self.layout.N or list(attrs["fields"]) != list(self.fields):
+                raise ValueError(f"{path}: initial condition is C{attrs['N']} {attrs['fields']}, "
+                                 f"run is C{self.layout.N} {self.fields}")
+            glob = np.stack([zarr_lite.read_array(path, f) for f in self.fields])
+            for e in self.engines:
+                loc = np.stack([e.geo.gather_global(glob[k]) for k in range(len(self.fields))])
+                e.set_state(torch.as_tensor(loc, dtype=self.dtype))
+            self._log(f"Initial conditions: read {path}")
+            return
+        g = self.gather_global()
+        if self.rank == 0:
+            zarr_lite.create_group(path, attrs={"N": self.layout.N, "fields": self.fields,
+                                                "physics": self.physics.name,
+                                                "case": getattr(self.physics, "case", None), "time": self.time})
+            for k, f in enumerate(self.fields):
+                zarr_lite.write_array(path, f, g[k], chunks=(1, self.layout.N, self.layout.N))
+            self._log(f"Initial conditions: wrote {path}")
+        self._barrier()
 
     # ---- state access ---------------------------------------------------------
     @property
@@ -276,7 +322,29 @@ class Solver:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
 
+    # ticks per step at the run's initial dt: the watchdog halves dt at most
+    # three times, so every interval stays a whole number of steps
+    _SUB = 8
+
     def run(self, nsteps: Optional[int] = None, days: Optional[float] = None) -> Dict[str, Any]:
+        """Advance ``nsteps`` steps (or ``days``) of the run's initial dt.
+
+        The loop is graph-aware: history / checkpoint / metrics / watchdog
+        intervals cut the run into equal chunks, the native runner records one
+        graph of that chunk length (plus the final remainder) before the clock
+        starts, and every chunk is one graph replay.  History snapshots and
+        metrics are copied device -> pinned host memory on the stepping stream
+        and written out while the next chunk runs; the watchdog's finite-check
+        is read one chunk late (single-process modes).  The summary reports
+        the stepping throughput without setup (``setup_s``: graph capture and
+        first replay), plus the host time of each phase (``phase_s``; each phase
+        is also a roctx range).
+
+        Watchdog recovery restores a checkpoint, halves the *current* dt and
+        continues to the same simulated end time; history frames are indexed by
+        simulated time, so replayed intervals overwrite their frames.
+        """
+        from .utils.tracing import PhaseTimes
         if not self.engines:
             self.initialize()
         c = self.cfg
@@ -288,8 +356,20 @@ class Solver:
                 nsteps = c.time.nsteps or 1
         io = c.io
         out = io.output_dir
+        ph = PhaseTimes()
+        SUB = self._SUB
+        dt0, t0 = self.dt, self.time
+        end = nsteps * SUB
+        level = 0                               # dt = dt0 / 2**level
+
+        def pos() -> int:
+            return int(round((self.time - t0) / dt0 * SUB))
+
+        iv = {"history": io.history_interval, "checkpoint": io.checkpoint_interval,
+              "metrics": io.metrics_interval, "watchdog": c.runtime.watchdog_interval}
+        iv = {k: v * SUB for k, v in iv.items() if v > 0}
         hist = None
-        if io.history_interval > 0:
+        if "history" in iv:
             n_out = nsteps // io.history_interval + 1
             hpath = os.path.join(out, "history.zarr")
             if self.rank == 0:
@@ -298,63 +378,193 @@ class Solver:
                               attrs={"config": self.config})
             self._barrier()
             hist = HistoryWriter(hpath, self.fields, self.layout.N, self.layout.n, n_out, create=False)
-        metrics = MetricsLogger(os.path.join(out, "metrics.jsonl") if io.metrics_interval > 0 else None,
+        metrics = MetricsLogger(os.path.join(out, "metrics.jsonl") if "metrics" in iv else None,
                                 enabled=self.rank == 0)
-        intervals = [x for x in (io.history_interval, io.checkpoint_interval, io.metrics_interval,
-                                 c.runtime.watchdog_interval) if x > 0]
-        done = 0
-        k_hist = 0
-        if hist is not None:
-            self._write_history(hist, k_hist)
-            k_hist += 1
+        cells = 6 * self.layout.N ** 2
+        gpu = self.device.type == "cuda"
+        deferred = gpu and self.mode != "spmd"
+        pending: List[Any] = []               # (event, host work) done while the next chunk runs
+
+        def drain(block: bool = False) -> None:
+            while pending and (block or pending[0][0] is None or pending[0][0].query()):
+                ev, work = pending.pop(0)
+                if ev is not None:
+                    ev.synchronize()
+                work()
+
+        def chunk_at(p: int, step_ticks: int) -> int:
+            nxt = min([(p // v + 1) * v for v in iv.values()] + [end])
+            return max(1, (nxt - p) // step_ticks)
+
+        # ---- setup: graphs for the chunk lengths this run replays ------------------
+        with ph("setup"):
+            if ("checkpoint" in iv and "watchdog" in iv
+                    and self.step_count not in ckpt.list_checkpoints(self.checkpoint_root())):
+                self.save_checkpoint()      # the watchdog can always roll back to the run's start
+            if hist is not None:
+                self._snapshot_history(hist, 0, pending, async_copy=False)
+                drain(block=True)
+            if self._use_native() and nsteps > 0:
+                if self.runner is None:
+                    self.runner = self._make_runner()
+                lens, p, it = [], 0, 0
+                while p < end and it < 100000:        # the chunk sequence of a run without recovery
+                    k = chunk_at(p, SUB)
+                    if k not in lens:
+                        lens.append(k)
+                    p += k * SUB
+                    it += 1
+                per = self.runner.period
+                self.runner.graph_periods = max(1, min(max(lens), 512) // per)
+                for k in lens[:8]:
+                    if k >= per:
+                        self.runner.prepare(k)
+            self._sync()
         wall0 = time.perf_counter()
-        self._sync()
         recoveries = 0
-        while done < nsteps:
-            chunk = nsteps - done
-            for iv in intervals:
-                chunk = min(chunk, iv - (self.step_count % iv) if self.step_count % iv else iv)
-            chunk = max(1, min(chunk, nsteps - done))
-            self.step(chunk)
+        done = 0
+        self._wd_pending = None
+        while True:
+            p = pos()
+            if p >= end:
+                break
+            st = SUB >> level
+            chunk = chunk_at(p, st)
+            with ph("step"):
+                self.step(chunk)
             done += chunk
-            sc = self.step_count
-            if c.runtime.watchdog_interval and sc % c.runtime.watchdog_interval == 0:
-                if not self.all_finite():
-                    saved = ckpt.list_checkpoints(self.checkpoint_root())
+            drain()
+            p = pos()
+            due = {k for k, v in iv.items() if p % v == 0 or p >= end}
+            if "watchdog" in due:
+                with ph("watchdog"):
+                    ok = self._watchdog(pending, deferred and "checkpoint" not in due and p < end)
+                if not ok:
+                    saved = [s for s in ckpt.list_checkpoints(self.checkpoint_root())]
                     if recoveries < 3 and saved:
                         recoveries += 1
+                        pending.clear()
+                        self._wd_pending = None
                         # go back further on each repeated failure (recent checkpoints may
                         # already hold a growing instability)
                         last = ckpt.step_dir(self.checkpoint_root(), saved[-min(recoveries, len(saved))])
-                        self._log(f"watchdog: non-finite state at step {sc}; restarting from {last} with dt/2")
+                        dt_cur = self.dt
+                        self._log(f"watchdog: non-finite state at step {self.step_count}; restarting from {last} "
+                                  f"with dt/2")
                         self.restore_checkpoint(last)
-                        self.set_dt(self.dt * 0.5)
-                        done = max(0, done - (sc - self.step_count))
+                        level += 1
+                        self.set_dt(dt_cur * 0.5)
+                        if abs(self.dt * (1 << level) - dt0) > 1e-9 * dt0:
+                            self.set_dt(dt0 / (1 << level))
                         continue
-                    raise FloatingPointError(f"non-finite state detected at step {sc}")
-            if hist is not None and sc % io.history_interval == 0:
-                self._write_history(hist, k_hist)
-                k_hist += 1
-            if io.checkpoint_interval and sc % io.checkpoint_interval == 0:
-                self.save_checkpoint()
-            if io.metrics_interval and sc % io.metrics_interval == 0:
-                self._sync()
-                d = self.diagnostics()
-                wall = time.perf_counter() - wall0
-                metrics.log(step=sc, time_s=self.time, sim_days=self.time / DAY, dt=self.dt,
-                            cell_updates_per_s=6 * self.layout.N ** 2 * done / max(wall, 1e-12), **d)
-        self._sync()
+                    raise FloatingPointError(f"non-finite state detected at step {self.step_count}")
+            if hist is not None and "history" in due and p % iv["history"] == 0:
+                with ph("history"):
+                    self._snapshot_history(hist, p // iv["history"], pending, async_copy=deferred)
+            if "checkpoint" in due and p % iv["checkpoint"] == 0:
+                with ph("checkpoint"):
+                    drain(block=True)
+                    self.save_checkpoint()
+            if "metrics" in due:                 # every interval and the end of the run
+                with ph("metrics"):
+                    self._snapshot_metrics(metrics, pending, deferred, cells, done, wall0, p)
+        with ph("drain"):
+            self._sync()
+            drain(block=True)
         wall = time.perf_counter() - wall0
-        summary = {"steps": nsteps, "wall_s": wall, "sim_days": self.time / DAY,
-                   "cell_updates_per_s": 6 * self.layout.N ** 2 * nsteps / max(wall, 1e-12),
-                   "sim_days_per_day": (nsteps * self.dt / DAY) / max(wall / DAY, 1e-30)}
+        summary = {"steps": nsteps, "steps_run": done, "wall_s": wall, "setup_s": ph.times.get("setup", 0.0),
+                   "sim_days": self.time / DAY,
+                   "cell_updates_per_s": cells * done / max(wall, 1e-12),
+                   "sim_days_per_day": ((self.time - t0) / DAY) / max(wall / DAY, 1e-30),
+                   "recoveries": recoveries, "dt_final": self.dt,
+                   "graph_steps": (self.runner.stats["graph_steps"] if self.runner is not None else 0),
+                   "phase_s": dict(ph.times)}
         summary.update(self.diagnostics())
         norms = self.error_norms()
         if norms is not None:
             summary.update({f"err_{k}": v for k, v in norms.items()})
-        self._log(f"Run complete: {nsteps} steps, {summary['sim_days']:.3f} days, "
-                  f"{summary['cell_updates_per_s']:.3e} cell-updates/s")
+        self._log(f"Run complete: {done} steps, {summary['sim_days']:.3f} days, "
+                  f"{summary['cell_updates_per_s']:.3e} cell-updates/s (setup {summary['setup_s']:.3f} s excluded)")
         return summary
+
+    # ---- run-loop helpers ----------------------------------------------------------
+    def _snapshot_history(self, hist: HistoryWriter, k: int, pending: List[Any], async_copy: bool) -> None:
+        """History frame k: the interior values are copied to host memory on
+        the stepping stream; the zarr chunks are written when the copy is done
+        (``pending``), i.e. while the next chunk steps."""
+        t, sc = self.time, self.step_count
+        snaps = []
+        for e in self.engines:
+            v = e.tiles_view().detach()
+            if async_copy:
+                h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+                h.copy_(v, non_blocking=True)
+            else:
+                h = v.cpu()
+            snaps.append((e.plan.tiles, h))
+        ev = None
+        if async_copy:
+            ev = torch.cuda.Event()
+            ev.record()
+
+        def work():
+            for tiles, h in snaps:
+                hist.write_tiles(k, tiles, self.layout.tile_origin, h.double().numpy())
+            if self.rank == 0:
+                hist.write_time(k, t, sc)
+        pending.append((ev, work))
+
+    def _snapshot_metrics(self, metrics: MetricsLogger, pending: List[Any], deferred: bool, cells: int,
+                          done: int, wall0: float, p: int) -> None:
+        rec = dict(step=self.step_count, time_s=self.time, sim_days=self.time / DAY, dt=self.dt)
+        wall = time.perf_counter() - wall0
+        rec["cell_updates_per_s"] = cells * done / max(wall, 1e-12)
+        if not deferred:
+            metrics.log(**rec, **self.diagnostics())
+            return
+        keys, vals = [], []
+        for e in self.engines:
+            for k, v in e.physics.diagnostics(e.tiles_view(), e.tens).items():
+                keys.append(k)
+                vals.append(v.reshape(()).to(torch.float64))
+        dev = torch.stack(vals)
+        h = torch.empty(dev.shape, dtype=dev.dtype, pin_memory=True)
+        h.copy_(dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+
+        def work():
+            tot: Dict[str, float] = {}
+            for k, v in zip(keys, h.tolist()):
+                tot[k] = tot.get(k, 0.0) + v
+            metrics.log(**rec, **tot)
+        pending.append((ev, work))
+
+    def _watchdog(self, pending: List[Any], deferred: bool) -> bool:
+        """True while the state is finite.  Deferred (single process): the
+        check of this interval is queued and the previous interval's result is
+        returned, so the host never waits for the GPU here (a failure is seen
+        one interval late; checkpoints drain the queue first, so a checkpoint
+        never holds a state the watchdog has not passed)."""
+        if not deferred:
+            prev = getattr(self, "_wd_pending", None)
+            self._wd_pending = None
+            ok = self.all_finite()
+            if prev is not None:
+                prev[0].synchronize()
+                ok = ok and bool(prev[1].item())
+            return ok
+        flag = torch.stack([torch.isfinite(e.tiles_view()).all() for e in self.engines]).all()
+        h = torch.empty((), dtype=torch.bool, pin_memory=True)
+        h.copy_(flag, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        prev = getattr(self, "_wd_pending", None)
+        self._wd_pending = (ev, h)
+        if prev is None:
+            return True
+        prev[0].synchronize()
+        return bool(prev[1].item())
 
     def set_dt(self, dt: float) -> None:
         self.dt = dt

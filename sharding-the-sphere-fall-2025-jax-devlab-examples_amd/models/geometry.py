@@ -188,7 +188,13 @@ class CubedSphereGrid:
             "y_edge_lengths": self.y_edge_lengths(),
             "x_edge_normals": self.x_edge_normals(),
             "y_edge_normals": self.y_edge_normals(),
+            "x_edge_midpoints": self.x_edge_midpoints(),
+            "y_edge_midpoints": self.y_edge_midpoints(),
         }
+
+    _ZARR_KEYS = {"centers": "centers", "vertices": "vertices", "areas": "areas", "x_edge_lengths": "lx",
+                  "y_edge_lengths": "ly", "x_edge_normals": "mx", "y_edge_normals": "my",
+                  "x_edge_midpoints": "xmid", "y_edge_midpoints": "ymid"}
 
     def save_zarr(self, path: str) -> None:
         from ..utils import zarr_lite
@@ -197,13 +203,23 @@ class CubedSphereGrid:
             zarr_lite.write_array(path, k, v)
 
     @classmethod
-    def load_zarr(cls, path: str) -> "CubedSphereGrid":
+    def load_zarr(cls, path: str, N: Optional[int] = None, radius: Optional[float] = None) -> "CubedSphereGrid":
+        """Grid whose arrays are read from a zarr group written by
+        ``save_zarr`` (the pipeline's Geometry stage, PDF s.6).  ``N`` /
+        ``radius``, when given, must match the stored grid."""
         from ..utils import zarr_lite
         attrs = zarr_lite.read_attrs(path)
+        if attrs.get("grid") != "equiangular_gnomonic":
+            raise ValueError(f"{path}: not an equiangular gnomonic grid ({attrs.get('grid')!r})")
         g = cls(int(attrs["N"]), float(attrs["radius"]))
-        for k in ("centers", "vertices", "areas", "x_edge_lengths", "y_edge_lengths", "x_edge_normals", "y_edge_normals"):
-            key = {"x_edge_lengths": "lx", "y_edge_lengths": "ly", "x_edge_normals": "mx", "y_edge_normals": "my"}.get(k, k)
-            g._cache[key] = zarr_lite.read_array(path, k)
+        if N is not None and g.N != N:
+            raise ValueError(f"{path}: stored grid is C{g.N}, config asks for C{N}")
+        if radius is not None and g.radius != radius:
+            raise ValueError(f"{path}: stored radius {g.radius} != configured {radius}")
+        have = set(zarr_lite.list_arrays(path))
+        for k, key in cls._ZARR_KEYS.items():
+            if k in have:
+                g._cache[key] = zarr_lite.read_array(path, k)
         return g
 
 

@@ -14,7 +14,8 @@ time, io, runtime) configure the parts the reference only describes.
     grid:    {N: 96, halo: 2, dtype: float64}
     physics: {model: swe, case: tc5, limiter: mc}
     time:    {integrator: ssprk3, dt: null, cfl: 0.9, nsteps: 100, days: null}
-    io:      {output_dir: run, history_interval: 0, checkpoint_interval: 0, ...}
+    io:      {output_dir: run, history_interval: 0, checkpoint_interval: 0,
+              geometry: grid.zarr, initial_condition: ic.zarr, ...}
     runtime: {backend: auto, graph: true, steps_per_graph: 30, comm: auto, ...}
 """
 from __future__ import annotations
@@ -72,6 +73,10 @@ class IOConfig:
     keep_checkpoints: int = 3
     metrics_interval: int = 0          # steps; 0 = off
     restore: Optional[str] = None      # checkpoint path or "latest"
+    # pipeline stages of PDF s.6 ("Geometry: jax.zarr", "Initial Conditions:
+    # jax.zarr"): a zarr group written on the first run, read when present
+    geometry: Optional[str] = None
+    initial_condition: Optional[str] = None
 
 
 @dataclass

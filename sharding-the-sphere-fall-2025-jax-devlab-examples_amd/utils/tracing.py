@@ -19,15 +19,21 @@ from typing import Dict, Optional
 import torch
 
 
+_LIB = []
+
+
 def _lib():
-    if not torch.cuda.is_available():
-        return None
-    try:
-        from ..ops import native
-        L = native.load(build_if_missing=False)
-        return L if hasattr(L, "stsp_roctx_push") else None
-    except Exception:
-        return None
+    if not _LIB:
+        L = None
+        if torch.cuda.is_available():
+            try:
+                from ..ops import native
+                L = native.load(build_if_missing=False)
+                L = L if hasattr(L, "stsp_roctx_push") else None
+            except Exception:
+                L = None
+        _LIB.append(L)
+    return _LIB[0]
 
 
 @contextlib.contextmanager
@@ -68,6 +74,31 @@ class Timer:
             self.device_ms = self._e0.elapsed_time(self._e1)
         self.wall_s = time.perf_counter() - self._t0
         return False
+
+
+class PhaseTimes:
+    """Host wall time accumulated per named phase; every phase is also a
+    roctx range, so ``rocprofv3 --marker-trace`` shows the driver's step /
+    history / checkpoint / metrics phases next to the kernels.
+
+        ph = PhaseTimes()
+        with ph("step"): ...
+        ph.times -> {"step": seconds, ...}
+    """
+
+    def __init__(self):
+        self.times: Dict[str, float] = {}
+        self.counts: Dict[str, int] = {}
+
+    @contextlib.contextmanager
+    def __call__(self, name: str):
+        t0 = time.perf_counter()
+        with trace_range(name):
+            try:
+                yield
+            finally:
+                self.times[name] = self.times.get(name, 0.0) + time.perf_counter() - t0
+                self.counts[name] = self.counts.get(name, 0) + 1
 
 
 def summarize(times: Dict[str, float]) -> str:

@@ -121,3 +121,37 @@ def history_frames(history_path: str, field: str, grid: CubedSphereGrid, outdir:
         out.append(sphere_plot(h[k], grid, os.path.join(outdir, f"{field}_{k:04d}.png"),
                                title=f"{field}  day {t[k] / 86400.0:.2f}", log=log))
     return out
+
+
+def history_products(history_path: str, field: str, outdir: str, grid: Optional[CubedSphereGrid] = None,
+                     log: bool = False, every: int = 1,
+                     products: Sequence[str] = ("frames", "band", "six")) -> Sequence[str]:
+    """The analysis products of a run from its zarr history (PDF s.6
+    "Analysis/Viz: jax.zarr"):
+
+    * ``frames``  one 3-D sphere PNG per history frame (PDF s.12 / s.17);
+    * ``band``    lon-lat equatorial band (0-360 x +-50 deg) of the first and
+                  the last frame (PDF s.13 "Cosine Bell Advection - Equatorial
+                  Band", title carries day and peak);
+    * ``six``     per-face initial vs final panels (PDF s.18).
+    """
+    import os
+    from .history import read_history
+    from . import zarr_lite
+    if grid is None:
+        grid = CubedSphereGrid(int(zarr_lite.read_attrs(history_path)["N"]))
+    h = read_history(history_path, field)
+    t = zarr_lite.read_array(history_path, "time")
+    os.makedirs(outdir, exist_ok=True)
+    out = []
+    if "frames" in products:
+        out += list(history_frames(history_path, field, grid, os.path.join(outdir, "frames"), log=log, every=every))
+    last = h.shape[0] - 1
+    if "band" in products:
+        for k, name in ((0, "initial"), (last, "final")):
+            out.append(latlon_band(h[k], grid, os.path.join(outdir, f"{field}_band_{name}.png"),
+                                   title=f"{field} equatorial band, day {t[k] / 86400.0:.2f}, peak {h[k].max():.1f}"))
+    if "six" in products:
+        out.append(six_panel(h[0], h[last], os.path.join(outdir, f"{field}_six_panel.png"),
+                             title=f"{field}: initial (day {t[0] / 86400.0:.2f}) vs final (day {t[last] / 86400.0:.2f})"))
+    return out

@@ -86,8 +86,43 @@ def test_watchdog_recovers_from_checkpoint(tmp_path):
     s.run(nsteps=2)                # good checkpoint at step 2
     s.cfg.io.checkpoint_interval = 0
     s.set_dt(dt0 * 8)              # unstable from here on
-    s.run(nsteps=40)               # watchdog: restore step 2, halve dt, until stable
-    assert s.all_finite() and s.dt <= dt0
+    t1 = s.time
+    out = s.run(nsteps=40)         # watchdog: restore step 2, halve the current dt, until stable
+    assert s.all_finite() and out["recoveries"] >= 1
+    # each recovery halves the dt in use (not the checkpoint's), and the run
+    # still ends at the requested simulated time
+    assert s.dt == dt0 * 8 / 2 ** out["recoveries"]
+    assert abs(s.time - (t1 + 40 * 8 * dt0)) < 1e-6 * s.time
+    assert out["steps_run"] > 40
+
+
+def test_history_frames_follow_simulated_time_across_recovery(tmp_path):
+    """After a watchdog rollback the replayed interval overwrites its own
+    history frames (frames are indexed by simulated time, not by a counter)."""
+    c = _cfg(tmp_path, checkpoint_interval=2, history_interval=2)
+    c["runtime"] = {"watchdog_interval": 1}
+    s = S.Solver(c, verbose=False)
+    s.initialize()
+    dt0 = s.dt
+    s.set_dt(dt0 * 8)
+    out = s.run(nsteps=6)
+    t = zarr_lite.read_array(str(tmp_path / "history.zarr"), "time")
+    assert out["recoveries"] >= 1 and len(t) == 4
+    assert np.allclose(t, [0, 16 * dt0, 32 * dt0, 48 * dt0])
+    h = read_history(str(tmp_path / "history.zarr"), "h")
+    assert np.isfinite(h).all() and np.allclose(h[-1], s.global_field("h"))
+
+
+def test_run_chunks_follow_io_intervals(tmp_path):
+    """Chunk lengths come from the I/O intervals, so every interval boundary
+    is hit exactly (metrics at 3, 6, 9, history at 0, 4, 8, 10 = end)."""
+    s = S.Solver(_cfg(tmp_path, history_interval=4, metrics_interval=3), verbose=False)
+    out = s.run(nsteps=10)
+    m = read_metrics(str(tmp_path / "metrics.jsonl"))
+    assert [r["step"] for r in m] == [3, 6, 9, 10]
+    t = zarr_lite.read_array(str(tmp_path / "history.zarr"), "time")
+    assert np.allclose(t, [0, 4 * s.dt, 8 * s.dt])
+    assert out["steps_run"] == 10 and set(out["phase_s"]) >= {"step", "history", "metrics"}
 
 
 def test_run_summary_reports_williamson_norms(tmp_path):
@@ -100,3 +135,43 @@ def test_run_summary_reports_williamson_norms(tmp_path):
     c["physics"]["case"] = "tc5"
     s5 = S.Solver(S.load_config(c), verbose=False)
     assert "err_l2" not in s5.run(nsteps=2) and s5.error_norms() is None
+
+
+def test_geometry_and_initial_condition_zarr_stages(tmp_path):
+    """Pipeline stages of PDF s.6: the first run writes the grid and the
+    initial condition as zarr groups; a second run (another partition) reads
+    them and reproduces the first run bitwise."""
+    io = {"geometry": str(tmp_path / "grid.zarr"), "initial_condition": str(tmp_path / "ic.zarr")}
+    s = S.Solver(_cfg(tmp_path / "a", nd=1, **io), verbose=False)
+    s.initialize()
+    assert zarr_lite.read_attrs(io["geometry"])["N"] == 8
+    assert set(zarr_lite.list_arrays(io["initial_condition"])) == set(s.fields)
+    ic = s.gather_global()
+    s.run(nsteps=3)
+    # second run: geometry and IC come from the zarr groups
+    from stsphere.models.geometry import CubedSphereGrid
+    s2 = S.Solver(_cfg(tmp_path / "b", nd=6, **io), verbose=False)
+    s2.initialize()
+    assert np.array_equal(s2.gather_global(), ic)
+    assert np.array_equal(s2.grid.x_edge_normals(), CubedSphereGrid(8).x_edge_normals())
+    s2.run(nsteps=3)
+    assert np.array_equal(s2.gather_global(), s.gather_global())
+    # a changed IC on disk is what the next run starts from
+    zarr_lite.write_array(io["initial_condition"], "h", ic[0] * 1.01, chunks=(1, 8, 8))
+    s3 = S.Solver(_cfg(tmp_path / "c", nd=1, **io), verbose=False)
+    s3.initialize()
+    assert np.array_equal(s3.gather_global()[0], ic[0] * 1.01)
+    with pytest.raises(ValueError):
+        S.Solver(dict(_cfg(tmp_path / "d", **io), grid={"N": 12}), verbose=False).initialize()
+
+
+def test_plot_cli_products(tmp_path):
+    """`stsphere plot` renders the s.12 sphere frames, the s.13 equatorial
+    band and the s.18 six-panel from a run's history."""
+    from stsphere.__main__ import main
+    s = S.Solver(_cfg(tmp_path, history_interval=2), verbose=False)
+    s.run()
+    out = tmp_path / "plots"
+    assert main(["plot", str(tmp_path / "history.zarr"), "h", str(out)]) == 0
+    names = {p.name for p in out.rglob("*.png")}
+    assert {"h_band_initial.png", "h_band_final.png", "h_six_panel.png", "h_0000.png"} <= names
