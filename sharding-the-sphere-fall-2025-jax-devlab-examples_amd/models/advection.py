@@ -16,7 +16,7 @@ from typing import Dict
 import numpy as np
 import torch
 
-from .base import Physics, RankGeometry, plr_x, plr_y, recon_halo
+from .base import Physics, RankGeometry, reconstruct, recon_halo
 from .geometry import DAY, CubedSphereGrid
 from . import initial_conditions as ic
 
@@ -67,16 +67,18 @@ class Advection(Physics):
         uy = np.sum(self.wind(geo.grid, geo.ymid) * geo.my[:, :, None, :], axis=-1) * geo.ly
         t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=device)
         return {"area": t(geo.area), "invA": t(1.0 / geo.area), "ex": t(ux), "ey": t(uy),
-                "pedge": torch.as_tensor(geo.pedge, device=device)}   # [T] panel-edge side bits (PPM)
+                "pedge": torch.as_tensor(geo.pedge, device=device),   # [T] panel-edge side bits
+                "pe_base": torch.as_tensor(geo.pe_base, device=device),   # [T,4,3,n] panel-edge ghost stencils
+                "pe_t": t(geo.pe_t)}
 
     def kernel_params(self):
         return {"limiter": self.limiter}
 
     def rhs(self, qe, qi, tens, n, g):
-        qL, qR = plr_x(qe, g, n, self.limiter, tens.get("pedge"))
+        (qL, qR, _, _), (yL, yR, _, _) = reconstruct(qe, tens, g, n, self.limiter)
         U = tens["ex"]
         Fx = U * torch.where(U > 0, qL, qR)
-        qL, qR = plr_y(qe, g, n, self.limiter, tens.get("pedge"))
+        qL, qR = yL, yR
         V = tens["ey"]
         Gy = V * torch.where(V > 0, qL, qR)
         return -((Fx[..., 1:] - Fx[..., :-1]) + (Gy[..., 1:, :] - Gy[..., :-1, :])) * tens["invA"]

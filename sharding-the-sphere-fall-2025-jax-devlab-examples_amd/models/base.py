@@ -33,6 +33,53 @@ def recon_halo(lim: int) -> int:
     return 3 if lim == PPM else 2
 
 
+PE_LAYERS = 3    # ghost layers that carry panel-edge interpolation tables
+
+
+def panel_edge_target(N: int, J: np.ndarray, k: int) -> np.ndarray:
+    """Fractional along-edge index (global, in this panel's index direction)
+    of the point where this panel's grid line J, extended across a panel edge
+    to ghost layer k, lands on the neighbouring panel.
+
+    Equiangular gnomonic geometry: a point at angle delta = (k + 1/2) dalpha
+    beyond the edge of this panel has, on the neighbouring panel, the same
+    distance delta from the edge (so the neighbour's ghost-layer cells lie on
+    the right normal line), but along-edge angle
+    beta' = atan(tan(beta) / tan(pi/4 + delta)), pulled toward the edge middle.
+    The index-space ghost copy puts the neighbour's cell at beta instead; this
+    is the kink that made PLR and PPM lose order at panel edges
+    (Putman & Lin 2007, PDF s.14: ghost values by interpolation along the
+    neighbouring panel's grid lines)."""
+    da = 0.5 * np.pi / N
+    beta = -0.25 * np.pi + (np.asarray(J, dtype=np.float64) + 0.5) * da
+    delta = (k + 0.5) * da
+    bp = np.arctan(np.tan(beta) / np.tan(0.25 * np.pi + delta))
+    return (bp + 0.25 * np.pi) / da - 0.5
+
+
+def panel_edge_tables(N: int, layout: TileLayout, tiles, layers: int):
+    """Linear interpolation tables along the ghost strips that lie on panel
+    edges: for tile side s (W, E, S, N), ghost layer k and strip cell j,
+    the interpolated ghost is  x[b] + t (x[b+1] - x[b])  over the raw strip x
+    of that layer (tile-local b in [0, n-2]: the stencil never leaves the
+    tile's own strip, so no corner ghost is read and both panels of an edge use
+    the same stencil).  Returns (base [T,4,layers,n] int32, t [T,4,layers,n])."""
+    n = layout.n
+    T = len(tiles)
+    base = np.zeros((T, 4, layers, n), dtype=np.int32)
+    frac = np.zeros((T, 4, layers, n))
+    for li, tid in enumerate(tiles):
+        f, I0, J0 = layout.tile_origin(tid)
+        for side in range(4):
+            o = J0 if side < 2 else I0
+            for k in range(layers):
+                u = panel_edge_target(N, o + np.arange(n), k) - o
+                b = np.clip(np.floor(u).astype(np.int64), 0, max(n - 2, 0))
+                base[li, side, k] = b
+                frac[li, side, k] = u - b
+    return base, frac
+
+
 def limiter_code(name) -> int:
     if isinstance(name, int):
         return name
@@ -88,6 +135,7 @@ class RankGeometry:
             self.xmid[li] = XM[f, sj, I0:I0 + n + 1]
             self.ymid[li] = YM[f, J0:J0 + n + 1, si]
             self.ext1[li] = layout.tile_extended_index(tid, 1)
+        self.pe_base, self.pe_t = panel_edge_tables(N, layout, tiles, PE_LAYERS)
 
     def gather_global(self, arr_global: np.ndarray) -> np.ndarray:
         """[6, N, N, ...] global array -> [T, n, n, ...] local tiles."""
@@ -211,13 +259,7 @@ def ppm_faces(q: torch.Tensor, g: int, n: int, lo_edge=None, hi_edge=None):
     a = (7.0 / 12.0) * (cell(-2, n + 1) + cell(-1, n + 2)) - (1.0 / 12.0) * (cell(-3, n) + cell(0, n + 3))
     aL, aR = a[..., :-1], a[..., 1:]
     qc = cell(-1, n + 1)
-    flat = (aR - qc) * (qc - aL) <= 0
-    d = aR - aL
-    m6 = 6.0 * (qc - 0.5 * (aL + aR))
-    over_l = d * m6 > d * d
-    over_r = -(d * d) > d * m6
-    aL2 = torch.where(flat, qc, torch.where(over_l, 3.0 * qc - 2.0 * aR, aL))
-    aR2 = torch.where(flat, qc, torch.where(~over_l & over_r, 3.0 * qc - 2.0 * aL, aR))
+    aL2, aR2 = ppm_limit(qc, aL, aR)
     if lo_edge is not None or hi_edge is not None:
         s = 0.5 * limited_slope(qc - cell(-2, n), cell(0, n + 2) - qc, 2)
         x = torch.arange(-1, n + 1, device=q.device)
@@ -256,6 +298,118 @@ def plr_y(qe: torch.Tensor, g: int, n: int, lim: int, pedge: Optional[torch.Tens
     pe = None if pedge is None else (pedge >> 2)      # S, N bits -> low, high
     qL, qR = plr_x(qe.transpose(-1, -2), g, n, lim, pe)
     return qL.transpose(-1, -2), qR.transpose(-1, -2)
+
+
+def _strip(w: torch.Tensor, side: int, k: int, g: int, n: int) -> torch.Tensor:
+    """Ghost layer k of tile side (0 W, 1 E, 2 S, 3 N) of a window [..., T, W, W]
+    as [..., T, n] (along-strip index in the panel's index direction)."""
+    if side == 0:
+        return w[..., g:g + n, g - 1 - k]
+    if side == 1:
+        return w[..., g:g + n, g + n + k]
+    if side == 2:
+        return w[..., g - 1 - k, g:g + n]
+    return w[..., g + n + k, g:g + n]
+
+
+def _own(w: torch.Tensor, side: int, k: int, g: int, n: int) -> torch.Tensor:
+    """The tile's own cells at depth k from side (k = 0: the edge cells)."""
+    if side == 0:
+        return w[..., g:g + n, g + k]
+    if side == 1:
+        return w[..., g:g + n, g + n - 1 - k]
+    if side == 2:
+        return w[..., g + k, g:g + n]
+    return w[..., g + n - 1 - k, g:g + n]
+
+
+def _interp(x: torch.Tensor, b: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+    """x [..., T, n]; b, t [T, n]: x[b] + t (x[b+1] - x[b]) along the last axis."""
+    idx = b.long().expand(x.shape)
+    x0 = x.gather(-1, idx)
+    x1 = x.gather(-1, idx + 1)
+    return x0 + t * (x1 - x0)
+
+
+def ppm_limit(qc, aL, aR):
+    """Colella-Woodward monotonicity limiter of a cell's interface values."""
+    flat = (aR - qc) * (qc - aL) <= 0
+    d = aR - aL
+    m6 = 6.0 * (qc - 0.5 * (aL + aR))
+    over_l = d * m6 > d * d
+    over_r = -(d * d) > d * m6
+    aL2 = torch.where(flat, qc, torch.where(over_l, 3.0 * qc - 2.0 * aR, aL))
+    aR2 = torch.where(flat, qc, torch.where(~over_l & over_r, 3.0 * qc - 2.0 * aL, aR))
+    return aL2, aR2
+
+
+def _inner_face(line, lim: int):
+    """Face value, on the side of index g - 1, of the cell at index g of a
+    1-D line [..., 2g] (cells g-1, g-2, ... are on the other panel)."""
+    g = line.shape[-1] // 2
+    c, l, r = line[..., g], line[..., g - 1], line[..., g + 1]
+    if lim == PPM:
+        l2, r2 = line[..., g - 2], line[..., g + 2]
+        aL = (7.0 / 12.0) * (l + c) - (1.0 / 12.0) * (l2 + r)
+        aR = (7.0 / 12.0) * (c + r) - (1.0 / 12.0) * (l + r2)
+        return ppm_limit(c, aL, aR)[0]
+    return c - 0.5 * limited_slope(c - l, r - c, lim)
+
+
+def reconstruct(w: torch.Tensor, tens: Dict[str, torch.Tensor], g: int, n: int, lim: int):
+    """Edge states of the interior x- and y-edges with the panel-edge
+    treatment.  w: window [F, T, W, W] with raw (index-space copy) ghosts.
+
+    * Ghost strips on panel edges are replaced by linear interpolation along
+      the strip to where this panel's grid lines really cross into the
+      neighbour (``panel_edge_tables``); every face of this tile's cells is then
+      reconstructed on straight grid lines (PLR, or PPM without any fallback).
+    * The neighbour's state at a panel edge is reconstructed in the neighbour's
+      own frame: on the line [its ghosts = our cells interpolated at its grid
+      lines | its real cells].  Both panels evaluate the same pair of states at
+      their common edge, so the flux is single-valued (conservative).
+    * The cell values returned for wave-speed estimates are real cells on both
+      sides of every edge.
+
+    Returns (xL, xR, cxL, cxR) at the x-edges [F,T,n,n+1] and (yL, yR, cyL, cyR)
+    at the y-edges [F,T,n+1,n]."""
+    pe = tens.get("pedge")
+    if pe is None or "pe_base" not in tens:
+        xL, xR = plr_x(w, g, n, lim, pe)
+        yL, yR = plr_y(w, g, n, lim, pe)
+        return (xL, xR) + cells_x(w, g, n), (yL, yR) + cells_y(w, g, n)
+    base, frac = tens["pe_base"], tens["pe_t"]
+    wi = w.clone()
+    faces = {}
+    for side in range(4):
+        m = ((pe >> side) & 1) != 0
+        if not bool(m.any()):
+            continue
+        mk = m[:, None]
+        gp, raw = [], []
+        for k in range(g):
+            b, t = base[:, side, k], frac[:, side, k]
+            x = _strip(w, side, k, g, n)
+            raw.append(x)
+            _strip(wi, side, k, g, n).copy_(torch.where(mk, _interp(x, b, t), x))
+            gp.append(_interp(_own(w, side, k, g, n), b, t))
+        line = torch.stack(gp[::-1] + raw, -1)              # [F,T,n,2g]
+        faces[side] = (m, _inner_face(line, lim), raw[0])
+    xL, xR = plr_x(wi, g, n, lim)
+    yL, yR = plr_y(wi, g, n, lim)
+    cxL, cxR = cells_x(w, g, n)
+    cyL, cyR = cells_y(w, g, n)
+    for side, (m, fv, r0) in faces.items():
+        mk = m[:, None]
+        if side == 0:
+            xL[..., 0] = torch.where(mk, fv, xL[..., 0])
+        elif side == 1:
+            xR[..., n] = torch.where(mk, fv, xR[..., n])
+        elif side == 2:
+            yL[..., 0, :] = torch.where(mk, fv, yL[..., 0, :])
+        else:
+            yR[..., n, :] = torch.where(mk, fv, yR[..., n, :])
+    return (xL, xR, cxL, cxR), (yL, yR, cyL, cyR)
 
 
 class Physics:

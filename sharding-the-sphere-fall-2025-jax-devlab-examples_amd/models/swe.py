@@ -24,7 +24,7 @@ from typing import Dict
 import numpy as np
 import torch
 
-from .base import Physics, RankGeometry, cells_x, cells_y, plr_x, plr_y, recon_halo
+from .base import Physics, RankGeometry, reconstruct, recon_halo
 from .geometry import GRAVITY, OMEGA, CubedSphereGrid
 from . import initial_conditions as ic
 
@@ -104,7 +104,9 @@ class ShallowWater(Physics):
             "cgeo": t(np.concatenate([(1.0 / geo.area)[..., None], geo.center, gb,
                                       np.zeros(geo.area.shape + (1,))], axis=-1)),   # [T,n,n,8]
             "b": t(geo.gather_global(b)),
-            "pedge": torch.as_tensor(geo.pedge, device=device),   # [T] panel-edge side bits (PPM)
+            "pedge": torch.as_tensor(geo.pedge, device=device),   # [T] panel-edge side bits
+            "pe_base": torch.as_tensor(geo.pe_base, device=device),   # [T,4,3,n] panel-edge ghost stencils
+            "pe_t": t(geo.pe_t),
         }
 
     def kernel_params(self):
@@ -128,13 +130,10 @@ class ShallowWater(Physics):
         h = qe[0]
         safe = torch.where(h != 0, h, torch.ones_like(h))
         w = torch.stack([h, qe[1] / safe, qe[2] / safe, qe[3] / safe])
-        lim = self.limiter
-        wL, wR = plr_x(w, g, n, lim, tens.get("pedge"))                                  # [4,T,n,n+1]
-        cL, cR = cells_x(w, g, n)
+        (wL, wR, cL, cR), (yL, yR, dL, dR) = reconstruct(w, tens, g, n, self.limiter)   # x: [4,T,n,n+1]
         mx = tens["mx"].permute(1, 0, 2)[:, :, None, :]              # [3,T,1,n+1]
         Fx = self._flux(wL, wR, cL, cR, mx, tens["ex"])
-        wL, wR = plr_y(w, g, n, lim, tens.get("pedge"))                                  # [4,T,n+1,n]
-        cL, cR = cells_y(w, g, n)
+        wL, wR, cL, cR = yL, yR, dL, dR                             # y: [4,T,n+1,n]
         my = tens["my"].permute(1, 0, 2)[:, :, :, None]              # [3,T,n+1,1]
         Gy = self._flux(wL, wR, cL, cR, my, tens["ey"])
         invA = tens["invA"]

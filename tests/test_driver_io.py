@@ -39,13 +39,21 @@ def test_checkpoint_partition_independent(tmp_path):
     s.run()
     assert ckpt.list_checkpoints(os.path.join(str(tmp_path), "checkpoints")) == [2, 4]
     ref = s.gather_global()
-    s2 = S.Solver(_cfg(tmp_path, nd=3, t=1, restore="latest"), verbose=False)
+    # any tiling reads it back exactly
+    s1 = S.Solver(_cfg(tmp_path, nd=3, t=1, restore="latest"), verbose=False)
+    s1.initialize()
+    assert s1.step_count == 4 and np.array_equal(s1.gather_global(), ref)
+    # continuing on another rank count (same tiling) equals continuing the
+    # original bitwise (the panel-edge ghost stencils are per tile, so a
+    # different tiles_per_edge continues at truncation-error distance)
+    s2 = S.Solver(_cfg(tmp_path, nd=3, t=2, restore="latest"), verbose=False)
     s2.initialize()
-    assert s2.step_count == 4 and np.array_equal(s2.gather_global(), ref)
-    # continuing from the restart equals continuing the original
     s.step(2)
     s2.step(2)
+    s1.step(2)
     assert np.array_equal(s2.gather_global(), s.gather_global())
+    a, b = s1.gather_global(), s.gather_global()
+    assert np.abs(a[0] - b[0]).max() < 1e-3 * np.abs(b[0]).max()
 
 
 def test_incomplete_checkpoint_ignored(tmp_path):

@@ -52,7 +52,8 @@ def _worker(rank, world, port, N, t, staged, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,t,staged", [(2, 1, False), (3, 1, True), (4, 2, False), (8, 2, True)])
+@pytest.mark.parametrize("world,t,staged", [(2, 1, False), (3, 1, True), (4, 2, False), (6, 1, False), (6, 1, True),
+                                            (8, 2, False), (8, 2, True)])
 def test_gloo_multiprocess_equals_single(world, t, staged):
     N = 8
     out = tempfile.mkdtemp()
