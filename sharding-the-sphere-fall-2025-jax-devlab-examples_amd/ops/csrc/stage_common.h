@@ -292,6 +292,8 @@ struct Args {
   int* err;
   long long timeout_ticks;
   const int* pedge;
+  const int* pe_base;
+  const T* pe_t;
 };
 
 #ifdef STSP_STAMPS
@@ -437,6 +439,8 @@ Args<T> make_args(const StageDesc* d) {
   a.err = d->err;
   a.timeout_ticks = d->timeout_ticks;
   a.pedge = d->pedge;
+  a.pe_base = d->pe_base;
+  a.pe_t = (const T*)d->pe_t;
   return a;
 }
 

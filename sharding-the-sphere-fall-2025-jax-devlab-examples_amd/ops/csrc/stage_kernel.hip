@@ -72,6 +72,12 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   __shared__ T s_fl[F][NE];                            // edge fluxes
   __shared__ T s_nrm[SW ? 3 : 1][SW ? BX + BY + 2 : 1];  // edge normals: x columns, then y rows
   __shared__ T s_len[SW ? NE : 1];                     // edge lengths (for the curvature balance)
+  // panel edges: the neighbour's state at each panel-edge edge of the block,
+  // reconstructed in the neighbour's frame, and its raw cell (wave speeds)
+  constexpr int BM = BX > BY ? BX : BY;
+  constexpr int KG = (LIM == 4) ? 2 : 1;             // interpolated ghost layers the faces read
+  __shared__ T s_pf[RECON ? F : 1][RECON ? 4 * BM : 1];
+  __shared__ T s_pr[SW ? FL : 1][SW ? 4 * BM : 1];
 
   const int n = a.n, S = a.S, nn = n * n, mg = a.mg, pw = a.pw;
   const int nbx = (n + BX - 1) / BX, nby = (n + BY - 1) / BY;
@@ -246,6 +252,40 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     coef = is_x ? *o32(a.ex, (unsigned)(tile * n * (n + 1) + ey_ * (n + 1) + ex_))
                 : *o32(a.ey, (unsigned)(tile * (n + 1) * n + ey_ * n + ex_));
   }
+  // (c) panel edges (models/base.py::reconstruct).  bsides: the sides of this
+  // block that lie on a cube edge (block-uniform).  Fix-up thread tid < 4 BM
+  // owns strip cell jl of side tid / BM: it interpolates that cell's ghost
+  // layers along the neighbour's grid lines and reconstructs the neighbour's
+  // edge state in the neighbour's frame.  Its table entries are issued here.
+  int bsides = 0;
+  if constexpr (RECON) {
+    const int pe = a.pedge[tile];
+    bsides = (x0 == 0 ? (pe & 1) : 0) | (x0 + BX >= n ? (pe & 2) : 0) | (y0 == 0 ? (pe & 4) : 0) |
+             (y0 + BY >= n ? (pe & 8) : 0);
+  }
+  const int pside = tid / BM, pjl = tid - pside * BM;
+  const int pj = (pside < 2 ? y0 : x0) + pjl;           // strip cell (tile-local, along the side)
+  const bool pact = RECON && tid < 4 * BM && ((bsides >> pside) & 1) && pjl < (pside < 2 ? BY : BX) && pj < n;
+  int pb[KG];
+  T pt_[KG];
+  if (pact) {
+#pragma unroll
+    for (int k = 0; k < KG; ++k) {
+      const unsigned ti = (unsigned)(((tile * 4 + pside) * 3 + k) * n + pj);
+      pb[k] = *o32(a.pe_base, ti);
+      pt_[k] = *o32(a.pe_t, ti);
+    }
+  }
+  // the edge thread of a panel-edge edge takes the neighbour's state from the
+  // fix-up slot pslot (the neighbour is on the left of the edge when plo)
+  int pslot = -1;
+  bool plo = false;
+  if (RECON && bsides && edge_ok) {
+    if (is_x && ex_ == 0 && (bsides & 1)) { pslot = 0 * BM + ey_ - y0; plo = true; }
+    else if (is_x && ex_ == n && (bsides & 2)) { pslot = 1 * BM + ey_ - y0; }
+    else if (!is_x && ey_ == 0 && (bsides & 4)) { pslot = 2 * BM + ex_ - x0; plo = true; }
+    else if (!is_x && ey_ == n && (bsides & 8)) { pslot = 3 * BM + ex_ - x0; }
+  }
   STAMP(1);
 
   // ---- 0b. direct xGMI: wait for the peers whose ghosts this block reads ------
@@ -376,14 +416,84 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   __syncthreads();
   STAMP(3);
 
+  // ---- 1a. panel edges: interpolated ghosts + the neighbour's edge state ------
+  // Ghost layer k of a panel-edge strip holds the neighbour's cells on ITS grid
+  // lines (index-space copy); this panel's grid lines cross into the neighbour
+  // elsewhere (beta' = atan(tan beta / tan(pi/4 + delta_k)), pulled toward the
+  // edge middle).  The ghosts the faces read are replaced by x[b] + t (x[b+1] -
+  // x[b]) along the strip; the neighbour's state at the edge is reconstructed
+  // from [our cells interpolated at its grid line | its raw cells], exactly as
+  // the neighbour block computes it, so the edge flux is single-valued.
+  if constexpr (RECON) {
+    if (bsides) {                      // block-uniform
+      T gk[KG][F], nf[F], r0v[FL];
+      const bool low = (pside & 1) == 0;
+      auto widx = [&](int cn, int al) {  // window index of (normal coord, along coord), tile-local
+        const int x = pside < 2 ? cn : al, y = pside < 2 ? al : cn;
+        return (y - y0 + NG) * WS + (x - x0 + NG);
+      };
+      const T* w0 = &s_w[0][0][0];
+      if (pact) {
+        T gp[KG][F];
+#pragma unroll
+        for (int k = 0; k < KG; ++k) {
+          const int cg = low ? -1 - k : n + k, co = low ? k : n - 1 - k;
+          const int ig0 = widx(cg, pb[k]), ig1 = widx(cg, pb[k] + 1);
+          const int io0 = widx(co, pb[k]), io1 = widx(co, pb[k] + 1);
+#pragma unroll
+          for (int f = 0; f < F; ++f) {
+            const T g0 = w0[f * WF + ig0], g1 = w0[f * WF + ig1];
+            gk[k][f] = g0 + pt_[k] * (g1 - g0);
+            const T o0 = w0[f * WF + io0], o1 = w0[f * WF + io1];
+            gp[k][f] = o0 + pt_[k] * (o1 - o0);
+          }
+        }
+        const int i0 = widx(low ? -1 : n, pj), i1 = widx(low ? -2 : n + 1, pj);
+#pragma unroll
+        for (int f = 0; f < FL; ++f) r0v[f] = w0[f * WF + i0];
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+          const T c = r0v[f], r = w0[f * WF + i1], l = gp[0][f];
+          if constexpr (LIM == 4) {
+            const T l2 = gp[1][f], r2 = w0[f * WF + widx(low ? -3 : n + 2, pj)];
+            const T aL = T(7.0 / 12.0) * (l + c) - T(1.0 / 12.0) * (l2 + r);
+            const T aR = T(7.0 / 12.0) * (c + r) - T(1.0 / 12.0) * (l + r2);
+            const bool flat = (aR - c) * (c - aL) <= T(0);
+            const T d = aR - aL;
+            const T m6 = T(6) * (c - T(0.5) * (aL + aR));
+            const bool ovl = d * m6 > d * d;
+            nf[f] = flat ? c : (ovl ? T(3) * c - T(2) * aR : aL);
+          } else {
+            nf[f] = c - half_slope<LIM>(c - l, r - c);
+          }
+        }
+      }
+      __syncthreads();                 // every raw value is read before any is replaced
+      if (pact) {
+        T* wm = &s_w[0][0][0];
+#pragma unroll
+        for (int k = 0; k < KG; ++k) {
+          const int ig = widx(low ? -1 - k : n + k, pj);
+#pragma unroll
+          for (int f = 0; f < F; ++f) wm[f * WF + ig] = gk[k][f];
+        }
+#pragma unroll
+        for (int f = 0; f < F; ++f) s_pf[f][tid] = nf[f];
+        if constexpr (SW) {
+#pragma unroll
+          for (int f = 0; f < FL; ++f) s_pr[f][tid] = r0v[f];
+        }
+      }
+      __syncthreads();
+    }
+  }
+
   // ---- 1b. PLR face values, one (cell, direction) per thread -------------------
   // task t < NFX: x-direction, cell (x0 + c - 1, y0 + r), t = r (BX + 2) + c;
   // else y-direction, cell (x0 + c, y0 + r - 1), t - NFX = r BX + c.
   if constexpr (FACES) {
     const T* w0 = &s_w[0][0][0];
-    // PPM: tile sides on a cube (panel) edge; cells whose 5-cell stencil
-    // crosses one use MC-limited PLR faces (models/base.py::ppm_faces)
-    const int pe = (LIM == 4) ? a.pedge[tile] : 0;
+    // (panel-edge ghosts are already interpolated in the window: no fallback)
     for (int t = tid; t < NFT; t += NT) {
       const bool tx = t < NFX;
       const int u = tx ? t : t - NFX;
@@ -396,13 +506,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 #pragma unroll
         for (int f = 0; f < F; ++f) {
           const T m1 = w0[f * WF + ci - st], c0 = w0[f * WF + ci], p1 = w0[f * WF + ci + st];
-          const int xc = tx ? x : y;                  // cell index along the task direction
-          const bool edge_cell = (LIM == 4) && (((pe & (tx ? 1 : 4)) && xc <= 1) || ((pe & (tx ? 2 : 8)) && xc >= n - 2));
-          if (LIM == 4 && edge_cell) {
-            const T hs = T(0.5) * slope<2>(c0 - m1, p1 - c0);
-            s_fm[f][t] = c0 - hs;
-            s_fp[f][t] = c0 + hs;
-          } else if constexpr (LIM == 4) {
+          if constexpr (LIM == 4) {
             // PPM (models/base.py::ppm_faces): 4th-order interface values,
             // Colella-Woodward monotonicity limiter
             const T m2 = w0[f * WF + ci - 2 * st], p2 = w0[f * WF + ci + 2 * st];
@@ -451,6 +555,10 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
         wl = s_fp[0][fl_];
         wr = s_fm[0][fl_ + fst];
       }
+      if (pslot >= 0) {
+        if (plo) wl = s_pf[0][pslot];
+        else wr = s_pf[0][pslot];
+      }
       s_fl[0][eid] = coef * (coef > T(0) ? wl : wr);
     } else {
       T wl[4], wr[4], cl[5], cr[5];
@@ -469,6 +577,19 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       } else {
 #pragma unroll
         for (int f = 0; f < 4; ++f) { wl[f] = s_fp[f][fl_]; wr[f] = s_fm[f][fl_ + fst]; }
+      }
+      if (pslot >= 0) {                 // panel edge: the neighbour's state and raw cell
+        if (plo) {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) wl[f] = s_pf[f][pslot];
+#pragma unroll
+          for (int f = 0; f < 5; ++f) cl[f] = s_pr[f][pslot];
+        } else {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) wr[f] = s_pf[f][pslot];
+#pragma unroll
+          for (int f = 0; f < 5; ++f) cr[f] = s_pr[f][pslot];
+        }
       }
       const int ni = is_x ? e_c : BX + 1 + e_r;
       T fl[4];
@@ -661,7 +782,8 @@ int launch_l(const StageDesc* d, hipStream_t s) {
 template <typename T, int P, int BX, int BY>
 int launch_t(const StageDesc* d, hipStream_t s) {
   if (d->nblocks <= 0) return 0;
-  if (d->pw != d->n + 2 * d->mg || d->mg < Phys<P>::NG || (d->limiter == 4 && (d->mg < 3 || !d->pedge))) return -5;
+  if (d->pw != d->n + 2 * d->mg || d->mg < Phys<P>::NG || (d->limiter == 4 && d->mg < 3)) return -5;
+  if (P != 1 && (!d->pedge || !d->pe_base || !d->pe_t || d->n < 2)) return -12;   // panel-edge tables
   if (!d->push || (d->remote && (!d->gmap || !d->blocks))) return -6;
   if (d->xg && (d->remote || d->blocks || !d->gmap || !d->recv || !d->peer_ring || !d->peer_cnt || !d->cnt ||
                 !d->nprod || !d->bmask || !d->epoch || !d->err || d->ring <= 0))

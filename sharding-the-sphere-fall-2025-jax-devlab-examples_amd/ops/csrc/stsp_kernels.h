@@ -53,7 +53,12 @@ typedef struct StageDesc {
   int* epoch;           // [nblocks] stages completed
   int* err;             // set to 1 on a poll timeout (all later polls fall through)
   long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
-  const int* pedge;     // [T] tile sides on a panel edge (bits W, E, S, N); PPM only
+  const int* pedge;     // [T] tile sides on a panel edge (bits W, E, S, N); PLR / PPM physics
+  // panel-edge ghost interpolation (models/base.py::panel_edge_tables): for tile
+  // side s, ghost layer k < 3, strip cell j: ghost = x[b] + t (x[b+1] - x[b]) over
+  // the raw strip x of that layer, b = pe_base[t][s][k][j] (tile-local), t = pe_t[...]
+  const int* pe_base;   // [T][4][3][n]
+  const void* pe_t;     // [T][4][3][n] element type
 } StageDesc;
 
 int stsp_stage_launch(int phys, int dtype, int bx, int by, const StageDesc* d, hipStream_t stream);

@@ -141,6 +141,10 @@ class HipCompute:
         assert t["ex"].shape == (T, n, n + 1) and t["ey"].shape == (T, n + 1, n)
         if "pedge" in t:
             assert t["pedge"].dtype == torch.int32 and t["pedge"].shape == (T,)
+        if "pe_base" in t:      # panel-edge ghost interpolation tables (models/base.py)
+            assert t["pe_base"].dtype == torch.int32 and t["pe_base"].shape == (T, 4, 3, n)
+            assert t["pe_t"].dtype == e.dtype and t["pe_t"].shape == (T, 4, 3, n)
+            assert int(t["pe_base"].min()) >= 0 and int(t["pe_base"].max()) <= max(n - 2, 0)
         if self.phys_id == 2:
             assert t["mx"].shape == (T, 3, n + 1) and t["my"].shape == (T, 3, n + 1)
             assert t["cgeo"].shape == (T, n, n, 8)
@@ -187,6 +191,8 @@ class HipCompute:
             d.mx, d.my, d.cgeo = p(t["mx"]), p(t["my"]), p(t["cgeo"])
         if "pedge" in t:
             d.pedge = p(t["pedge"])
+        if "pe_base" in t:
+            d.pe_base, d.pe_t = p(t["pe_base"]), p(t["pe_t"])
         d.ntile = e.plan.T
         d.n = e.plan.n
         d.S = e.plan.S

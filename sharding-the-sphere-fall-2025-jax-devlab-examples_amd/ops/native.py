@@ -39,7 +39,7 @@ class StageDesc(ctypes.Structure):
         ("peer_ring", ctypes.c_void_p), ("peer_cnt", ctypes.c_void_p), ("cnt", ctypes.c_void_p),
         ("nprod", ctypes.c_void_p), ("bmask", ctypes.c_void_p), ("epoch", ctypes.c_void_p), ("err", ctypes.c_void_p),
         ("timeout_ticks", ctypes.c_longlong),
-        ("pedge", ctypes.c_void_p),
+        ("pedge", ctypes.c_void_p), ("pe_base", ctypes.c_void_p), ("pe_t", ctypes.c_void_p),
     ]
 
 

@@ -141,6 +141,13 @@ class PersistentStepper:
             # launch-per-stage stepping after a few launches; until that is
             # understood the persistent path is PLR-only
             raise NotImplementedError("persistent stepping supports PLR limiters only (not PPM)")
+        if hc.phys_id != 1:
+            # the panel-edge ghost interpolation (models/base.py::reconstruct,
+            # stage_kernel.hip phase 1a) reads strip cells beyond a block's rows,
+            # which the persistent kernel's side-neighbour granule hand-off does
+            # not deliver; it lost to graph replay anyway (profiles/r2_persistent)
+            raise NotImplementedError("persistent stepping predates the panel-edge reconstruction: "
+                                      "diffusion only")
         maxb = self.L.stsp_step_max_blocks(hc.phys_id, hc.dcode, hc.bx, hc.by, lim)
         if maxb <= 0:
             raise RuntimeError(f"step kernel not available for this configuration ({maxb})")
