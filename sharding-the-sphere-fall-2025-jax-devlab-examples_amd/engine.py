@@ -78,7 +78,8 @@ class Engine:
         self.gmap = torch.as_tensor(self.plan.ghost_map, device=self.device)
         self.integ: Integrator = get_integrator(integrator)
         F, S = physics.F, self.plan.S
-        # padded storage, zero-initialised (corner ghost blocks stay 0 forever)
+        # padded storage, zero-initialised (corner ghost blocks are never written
+        # nor read: see corner_slots / poison_corners)
         self.pool: List[torch.Tensor] = [torch.zeros((F, S), dtype=dtype, device=self.device) for _ in range(self.integ.nbuf)]
         self.halo_src = torch.as_tensor(self.plan.halo_src, dtype=torch.long, device=self.device)
         self.halo_dst = torch.as_tensor(self.plan.halo_dst, dtype=torch.long, device=self.device)
@@ -120,6 +121,28 @@ class Engine:
 
     def tiles_view(self, q: Optional[torch.Tensor] = None) -> torch.Tensor:
         return self.interior(self.state if q is None else q)
+
+    def corner_slots(self) -> torch.Tensor:
+        """Flat padded-storage indices of the tile-corner ghost blocks (both
+        coordinates outside the tile).  No exchange writes them: at a cube
+        corner three panels meet and the block has no single source.  The
+        dimension-split stencils never read them (x-sweeps read ghost
+        columns of the tile's own rows, y-sweeps ghost rows of its own
+        columns); ``poison_corners`` makes that a checked property."""
+        n, mg, T = self.plan.n, self.plan.ng, self.plan.T
+        pw = n + 2 * mg
+        c = torch.arange(pw)
+        out = (c < mg) | (c >= n + mg)
+        m2 = out[:, None] & out[None, :]
+        idx = torch.nonzero(m2.reshape(-1)).reshape(-1)
+        return (torch.arange(T)[:, None] * pw * pw + idx[None, :]).reshape(-1).to(self.device)
+
+    def poison_corners(self) -> None:
+        """Fill every corner ghost slot of every buffer with NaN: a stencil
+        that ever reads one poisons the state (tests/test_numerics.py)."""
+        idx = self.corner_slots()
+        for b in self.pool:
+            b[:, idx] = float("nan")
 
     # ---- stepping -----------------------------------------------------------
     canary = False   # debug race screen (SURVEY.md 5.2), HIP backend, eager only

@@ -167,11 +167,12 @@ def test_persistent_refuses_ppm():
 
 def test_persistent_refuses_grids_that_cannot_be_co_resident():
     """A persistent grid whose blocks cannot all be resident would deadlock:
-    the launcher refuses it up front (5-wave 16x8 blocks at C96: 432 blocks,
-    one guaranteed per CU)."""
+    the launcher refuses it up front (5-wave 16x8 blocks,
+    one guaranteed per CU; the lighter diffusion blocks fit several per CU, so
+    the grid is C384: 6912 blocks)."""
     from stsphere.ops.persistent import PersistentStepper
-    g = CubedSphereGrid(96)
+    g = CubedSphereGrid(384)
     from stsphere.models.diffusion import Diffusion
-    e = Engine(Diffusion(), TileLayout(96, 2, 1, ng=2), grid=g, device="cuda", backend="hip", block=(16, 8))
+    e = Engine(Diffusion(), TileLayout(384, 2, 1, ng=2), grid=g, device="cuda", backend="hip", block=(16, 8))
     with pytest.raises(RuntimeError, match="co-resident"):
         PersistentStepper(e)

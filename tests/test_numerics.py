@@ -206,3 +206,27 @@ def test_williamson_norms_definition():
     assert math.isclose(nr["l2"], math.sqrt((0.01 + 0.08) / 13.0))
     assert math.isclose(nr["linf"], 0.2 / 2.0)
     assert math.isclose(convergence_order([4.0, 1.0], [10, 20]), 2.0)
+
+
+@pytest.mark.parametrize("mk", [lambda: ShallowWater("tc5"), lambda: ShallowWater("tc5", limiter=4),
+                                lambda: Advection(), lambda: Advection(limiter=4), lambda: Diffusion()])
+@pytest.mark.parametrize("t", [1, 2])
+def test_no_stencil_reads_a_corner_ghost(mk, t):
+    """Tile-corner ghost blocks (cube corners included) are never written; with
+    every one of them NaN the state stays finite and bitwise equal to the
+    zero-corner run (the zeros were an unguarded assumption)."""
+    from stsphere.engine import Engine
+    from stsphere.parallel.layout import TileLayout
+    N = 12
+    g = CubedSphereGrid(N)
+    phys = mk()
+    ng = 3 if getattr(phys, "limiter", 0) == 4 else 2
+    a = Engine(mk(), TileLayout(N, t, 1, ng=ng), grid=g)
+    b = Engine(mk(), TileLayout(N, t, 1, ng=ng), grid=g, dt=a.dt)
+    b.poison_corners()
+    assert b.corner_slots().numel() == b.plan.T * 4 * ng * ng
+    a.step(3)
+    b.step(3)
+    assert torch.isfinite(b.tiles_view()).all()
+    assert torch.equal(a.tiles_view(), b.tiles_view())
+    assert torch.isnan(b.state[:, b.corner_slots()]).all()
