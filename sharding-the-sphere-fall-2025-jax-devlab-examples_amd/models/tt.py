@@ -21,6 +21,11 @@ MI355X runs on the matrix cores through hipBLASLt / rocSOLVER):
                     runs the step on the gfx950 kernels of ops/tt_ops.py
                     (rank-2r expansion, MFMA Gram matrices, host k x k
                     eigen/SVD, MFMA tall-skinny products)
+* ``CubedSphereLowRankDiffusion``: the same factored diffusion on all six
+                    panels of the cube, coupled through the cube's halo in
+                    factored form (each panel side's ghost strip is gathered as
+                    rows of the neighbour's factors, O(N r) instead of the
+                    N x N field; orientation from the tile layout's ghost map)
 * ``compress_cubed_sphere``: per-panel TT ranks / errors of a [6, N, N] field
 """
 from __future__ import annotations
@@ -294,6 +299,184 @@ class LowRankDiffusion:
 
     def dense_step(self, U: torch.Tensor, dt: float) -> torch.Tensor:
         return U + dt * self.kappa * (self.D @ U + U @ self.D.T)
+
+
+def _second_diff_rows(X: torch.Tensor) -> torch.Tensor:
+    """(D X) with D the unscaled 1-D second difference, zero outside."""
+    out = -2.0 * X
+    out[1:] += X[:-1]
+    out[:-1] += X[1:]
+    return out
+
+
+class CubedSphereLowRankDiffusion:
+    """Explicit diffusion on the six panels of the cube in factored form
+    (PDF s.3, s.5, s.19: TT numerics on the cubed sphere).
+
+    Each panel field is U_p = A_p B_p^T (rows y, columns x, N x N, uniform
+    flat cells of side h), and one forward-Euler step of the five-point
+    Laplacian whose ghost cells come from the neighbouring panels (the
+    index-space halo of ``TileLayout(N, 1, 1, ng=1)``: the same orientation
+    rules as the FV solver's cube-edge exchange, PY:105-163) is
+
+        U_p' = U_p + c (D U_p + U_p D^T) + c (g_W e_0^T + g_E e_{N-1}^T
+                                              + e_0 g_S^T + e_{N-1} g_N^T)
+
+    with c = kappa dt / h^2 and g_s the ghost strip of side s, i.e.
+
+        A^ = [A, c D A, c g_W, c g_E, c e_0, c e_{N-1}]
+        B^ = [B + c D B, B, e_0, e_{N-1}, g_S, g_N]            (k = 2 r + 4)
+
+    recompressed to rank <= max_rank.  The halo exchange itself is factored:
+    ghost j of a strip is the neighbour cell (y, x) = A_q[y] . B_q[x], so a
+    side costs O(N r) and no panel is ever expanded.  The coupling is
+    symmetric, so the total sum (mass) is conserved up to the truncation.
+
+    backend "torch": thin QRs + a k x k SVD (rocBLAS / rocSOLVER on the GPU);
+    backend "hip": the MFMA Gram kernels (ops/tt_ops.gram), the native k x k
+    core (stsp_tt_core, one host round trip for all six panels) and the MFMA
+    tall-skinny products (ops/tt_ops.tsmm).  ``dense_step`` is the N x N
+    six-panel reference of the same operator."""
+
+    def __init__(self, N: int, kappa: float = 1.0, L: float = 1.0, eps: float = 1e-10,
+                 max_rank: Optional[int] = None, dtype=torch.float64, device="cpu", backend: str = "torch"):
+        from ..parallel.layout import TileLayout
+        if backend not in ("torch", "hip"):
+            raise ValueError(f"unknown backend {backend!r}")
+        self.N, self.kappa, self.h = N, kappa, L / N
+        self.eps, self.max_rank, self.backend = eps, max_rank, backend
+        self.dtype, self.device = dtype, torch.device(device)
+        self.dt_max = self.h * self.h / (4.0 * kappa)
+        lay = TileLayout(N, 1, 1, ng=1)
+        plan = lay.plan(0)
+        pw = N + 2
+        face_of = [lay.tile_origin(t)[0] for t in plan.tiles]
+        src = np.asarray(plan.halo_src, dtype=np.int64)
+        dst = np.asarray(plan.halo_dst, dtype=np.int64)
+        # ghost slot -> (panel, side, position) and its source cell (panel, y, x)
+        self.nbr = [[None] * 4 for _ in range(6)]
+        gy = np.full((6, 4, N), -1, np.int64)
+        gx = np.full((6, 4, N), -1, np.int64)
+        for d, s_ in zip(dst, src):
+            tp, r = divmod(int(d), pw * pw)
+            py, px = divmod(r, pw)
+            py, px = py - 1, px - 1
+            tq, r2 = divmod(int(s_), pw * pw)
+            qy, qx = divmod(r2, pw)
+            qy, qx = qy - 1, qx - 1
+            if not (0 <= qy < N and 0 <= qx < N):
+                raise RuntimeError("halo source outside the neighbour panel")
+            inx, iny = 0 <= px < N, 0 <= py < N
+            if iny and px == -1:
+                side, pos = 0, py
+            elif iny and px == N:
+                side, pos = 1, py
+            elif inx and py == -1:
+                side, pos = 2, px
+            elif inx and py == N:
+                side, pos = 3, px
+            else:
+                continue
+            p, q = face_of[tp], face_of[tq]
+            if self.nbr[p][side] not in (None, q):
+                raise RuntimeError("a panel side borders more than one panel")
+            self.nbr[p][side] = q
+            gy[p, side, pos], gx[p, side, pos] = qy, qx
+        if (gy < 0).any():
+            raise RuntimeError("incomplete cube halo")
+        self.gy = torch.as_tensor(gy, device=self.device)
+        self.gx = torch.as_tensor(gx, device=self.device)
+        # dense reference: padded [6, N+2, N+2] with the same ghost map, by face
+        self._dsrc, self._ddst = [], []
+        for d, s_ in zip(dst, src):
+            tp, r = divmod(int(d), pw * pw)
+            tq, r2 = divmod(int(s_), pw * pw)
+            self._ddst.append(face_of[tp] * pw * pw + r)
+            self._dsrc.append(face_of[tq] * pw * pw + r2)
+        self._ddst = torch.as_tensor(self._ddst, device=self.device)
+        self._dsrc = torch.as_tensor(self._dsrc, device=self.device)
+        e = torch.zeros((N, 2), dtype=dtype, device=self.device)
+        e[0, 0] = 1.0
+        e[N - 1, 1] = 1.0
+        self._e = e
+        self.stats = {"host_syncs": 0}
+
+    def ghosts(self, F: Sequence[LowRankField], p: int) -> torch.Tensor:
+        """[4, N] ghost strips (W, E, S, N) of panel p, gathered in factored form."""
+        out = []
+        for side in range(4):
+            q = self.nbr[p][side]
+            out.append((F[q].A[self.gy[p, side]] * F[q].B[self.gx[p, side]]).sum(1))
+        return torch.stack(out)
+
+    def expanded(self, F: Sequence[LowRankField], dt: float):
+        """Per panel (A^, B^) of the step (k = 2 r + 4 columns), from the old fields."""
+        c = dt * self.kappa / (self.h * self.h)
+        out = []
+        for p in range(6):
+            A, B = F[p].A, F[p].B
+            g = self.ghosts(F, p)
+            Ah = torch.cat([A, c * _second_diff_rows(A), c * g[0:2].T, c * self._e], dim=1)
+            Bh = torch.cat([B + c * _second_diff_rows(B), B, self._e, g[2:4].T], dim=1)
+            out.append((Ah.contiguous(), Bh.contiguous()))
+        return out
+
+    def step(self, F: Sequence[LowRankField], dt: float) -> List[LowRankField]:
+        ex = self.expanded(F, dt)
+        if self.backend == "torch":
+            return [recompress(Ah, Bh, self.eps, self.max_rank) for Ah, Bh in ex]
+        return self._recompress_hip(ex)
+
+    def _recompress_hip(self, ex) -> List[LowRankField]:
+        """Gram route on the gfx950 kernels: 12 MFMA Gram matrices, one copy to
+        the host, six native k x k cores, 12 MFMA tall-skinny products."""
+        import ctypes
+        from ..ops import native, tt_ops
+        L = native.require_native()
+        k = ex[0][0].shape[1]
+        if k > 64:
+            raise ValueError(f"hip cube step supports rank <= 30 (k = {k})")
+        G = torch.empty((6, 2, k, k), dtype=ex[0][0].dtype, device=ex[0][0].device)
+        for p, (Ah, Bh) in enumerate(ex):
+            tt_ops.gram(Ah, Ah, out=G[p, 0])
+            tt_ops.gram(Bh, Bh, out=G[p, 1])
+        Gh = G.double().cpu()                   # the one host round trip of the step
+        self.stats["host_syncs"] += 1
+        X = torch.zeros((6, k, 2 * k), dtype=torch.float64)
+        ranks = []
+        for p in range(6):
+            g = Gh[p].contiguous()
+            rn = L.stsp_tt_core(k, ctypes.c_void_p(g.data_ptr()), float(self.eps), int(self.max_rank or 0),
+                                ctypes.c_void_p(X[p].data_ptr()), 2 * k)
+            if rn <= 0:
+                raise RuntimeError(f"stsp_tt_core failed ({rn})")
+            ranks.append(rn)
+        Xd = X.to(device=ex[0][0].device, dtype=ex[0][0].dtype)
+        out = []
+        for p, (Ah, Bh) in enumerate(ex):
+            rn = ranks[p]
+            A2 = tt_ops.tsmm(Ah, Xd[p, :, :rn].contiguous())
+            B2 = tt_ops.tsmm(Bh, Xd[p, :, rn:2 * rn].contiguous())
+            out.append(LowRankField(A2, B2))
+        return out
+
+    # ---- dense reference / conversions ---------------------------------------
+    def to_factored(self, U6: torch.Tensor) -> List[LowRankField]:
+        return [LowRankField.from_dense(U6[p].to(self.dtype), self.eps, self.max_rank) for p in range(6)]
+
+    @staticmethod
+    def to_dense(F: Sequence[LowRankField]) -> torch.Tensor:
+        return torch.stack([f.dense() for f in F])
+
+    def dense_step(self, U6: torch.Tensor, dt: float) -> torch.Tensor:
+        N = self.N
+        c = dt * self.kappa / (self.h * self.h)
+        P = torch.zeros((6, N + 2, N + 2), dtype=U6.dtype, device=U6.device)
+        P[:, 1:-1, 1:-1] = U6
+        flat = P.reshape(-1)
+        flat[self._ddst] = flat[self._dsrc]
+        lap = (P[:, :-2, 1:-1] + P[:, 2:, 1:-1]) + (P[:, 1:-1, :-2] + P[:, 1:-1, 2:]) - 4.0 * U6
+        return U6 + c * lap
 
 
 def compress_cubed_sphere(field: np.ndarray, eps: float = 1e-6, qtt: bool = False) -> List[dict]:
