@@ -87,6 +87,42 @@ template <int BX, int BY> struct Geom {
   static constexpr unsigned long long RING_TAB = 0x5432f1fff0ULL;   // ring slot (non-own waves)
 };
 
+// Border-edge flux slots for the panel-edge fix-up (stage_kernel.hip, PEW):
+// slot PEW_SX = x-edges at columns {0, 1, BX-1, BX} of every row (lane = row * 4 + q),
+// slot PEW_SY = y-edges at rows {0, 1, BY-1, BY} of every column, the other
+// seven slots (in slot order) = the interior x-edges (columns 2 .. BX-2) then
+// the interior y-edges (rows 2 .. BY-2), 64 per slot.  The border slots sit on
+// waves 7 (SIMD 3) and 6 (SIMD 2), the SIMDs with the most slack before the
+// flux barrier (SIMD 0 already runs three flux waves; profiles/r2_pe_stamps).
+// Returns the canonical edge id (x-edge r (BX+1) + c, y-edge NX + r BX + c) or
+// NX + NY past the last edge.  A bijection onto the edges for 16 x 16 blocks
+// (tests/test_kernel_contracts.py mirrors it).
+#ifndef STSP_PE_WAVE
+#define STSP_PE_WAVE 1
+#endif
+constexpr int PEW_SX = 7, PEW_SY = 5;
+template <int BX, int BY>
+__device__ __forceinline__ int edge_of_slot(int slot, int lane) {
+  constexpr int NX = (BX + 1) * BY, NY = BX * (BY + 1);
+  constexpr int IX = BX - 3, IY = BY - 3;         // interior columns / rows per line
+  static_assert(BX == 16 && BY == 16, "border slots are laid out for 16 x 16 blocks");
+  const int q = lane & 3, u4 = lane >> 2;
+  const int b = q < 2 ? q : q + (BX - 3);         // 0, 1, B-1, B
+  if (slot == PEW_SX) return u4 * (BX + 1) + b;
+  if (slot == PEW_SY) return NX + b * BX + u4;
+  const int u = (slot - (slot > PEW_SY) - (slot > PEW_SX)) * 64 + lane;
+  if (u < BY * IX) {
+    const int r = u / IX;
+    return r * (BX + 1) + 2 + (u - r * IX);
+  }
+  const int v = u - BY * IX;
+  if (v < IY * BX) {
+    const int r = v / BX;
+    return NX + (2 + r) * BX + (v - r * BX);
+  }
+  return NX + NY;
+}
+
 // Hardware min/max/abs/copysign (v_max_f64, |x| source modifier, v_bfi):
 // one VALU op each where compare + select pairs cost three (wave64 fp64 and
 // integer VALU ops issue at the same 4 cycles, so every instruction counts).
@@ -281,6 +317,7 @@ struct Args {
   unsigned mdiv_t, mdiv_r;   // ceil(2^32 / (nbx nby)), ceil(2^32 / nbx); 0 = divide
   int diag_repeat;           // diag build only: run the block body this many extra times
   int wt;                    // write-through output stores (st_out)
+  int pew;                   // border-wave panel-edge fix-up allowed (full blocks: n % BX == n % BY == 0)
   // direct xGMI halo (XG kernels only, see stsp_kernels.h)
   int ring;
   T* const* peer_ring;
@@ -429,6 +466,7 @@ Args<T> make_args(const StageDesc* d) {
   a.stamps = (unsigned long long*)d->stamps;
   a.diag_repeat = 0;
   a.wt = 0;
+  a.pew = 0;
   a.ring = d->ring;
   a.peer_ring = (T* const*)d->peer_ring;
   a.peer_cnt = d->peer_cnt;

@@ -49,6 +49,16 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   // the window (PLR only; PPM keeps the separate face phase, its stencil is wider)
   constexpr bool FUSED = RECON && (LIM != 4) && STSP_FUSE_FACES;
   constexpr bool FACES = RECON && !FUSED;
+  // PEW: panel-edge fix-up inside the two border-edge waves (PLR, ten-wave
+  // 256-cell blocks): flux slot 0 holds the x-edges at columns 0, 1, BX-1, BX
+  // of every row and slot 1 the y-edges at rows 0, 1, BY-1, BY (edge_of_slot),
+  // so the only readers of an interpolated ghost or of the neighbour's edge
+  // state are the lanes of the wave that computes them: no barrier, and the
+  // other seven flux waves never wait for the fix-up
+  // (a partial block's panel edge is not at border column BX, so grids with
+  // n % 16 != 0 take the block-wide fix-up: pew below)
+  constexpr bool PEW = FUSED && Geom<BX, BY>::W10 && STSP_PE_WAVE;
+  const bool pew = PEW && a.pew != 0;            // block-uniform
   constexpr int NT = Geom<BX, BY>::NT;
   constexpr int NX = Geom<BX, BY>::NX;
   constexpr int NY = Geom<BX, BY>::NY;
@@ -78,6 +88,13 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   constexpr int KG = (LIM == 4) ? 2 : 1;             // interpolated ghost layers the faces read
   __shared__ T s_pf[RECON ? F : 1][RECON ? 4 * BM : 1];
   __shared__ T s_pr[SW ? FL : 1][SW ? 4 * BM : 1];
+  // raw (index-space copied) ghost layers k < KG of the panel-edge strips, by
+  // window position along the side: the interpolation reads these, so the
+  // interpolated ghosts can replace the raw ones in the window without a
+  // barrier between the reads and the writes
+  constexpr int EM = EX > EY ? EX : EY;
+  constexpr bool RAWC = RECON;                 // the block-wide fix-up's raw copy
+  __shared__ T s_raw[RAWC ? 4 : 1][RAWC ? KG : 1][RAWC ? F : 1][RAWC ? EM : 1];
 
   const int n = a.n, S = a.S, nn = n * n, mg = a.mg, pw = a.pw;
   const int nbx = (n + BX - 1) / BX, nby = (n + BY - 1) / BY;
@@ -123,6 +140,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   static_assert(RING <= NT - NIN, "one ring cell per thread without an own cell");
   const int wv = tid >> 6;
   int oid, rid, eid;    // own-cell slot, ring slot (RING: none), edge (NE_: none)
+  int eslot = -1;       // flux slot of this wave (ten-wave map)
   if constexpr (Geom<BX, BY>::W10) {
     const int lane = tid & 63;
     const unsigned os = (unsigned)(Geom<BX, BY>::OWN_TAB >> (4 * wv)) & 15u;
@@ -130,7 +148,11 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     const unsigned rs = (unsigned)(Geom<BX, BY>::RING_TAB >> (4 * wv)) & 15u;
     oid = os != 15u ? (int)os * 64 + lane : -1;
     eid = fs != 15u ? (int)fs * 64 + lane : NE_;
+    if constexpr (PEW) {
+      if (pew) eid = fs != 15u ? edge_of_slot<BX, BY>((int)fs, lane) : NE_;
+    }
     rid = rs != 15u ? (int)rs * 64 + lane : RING;
+    eslot = (int)fs;
   } else {
     static_assert(Geom<BX, BY>::W10 || NOWN <= NT / 64 - (NT / 64 + 3) / 4, "enough waves off SIMD 0");
 #if STSP_OWN_SKIP0
@@ -253,22 +275,45 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
                 : *o32(a.ey, (unsigned)(tile * (n + 1) * n + ey_ * n + ex_));
   }
   // (c) panel edges (models/base.py::reconstruct).  bsides: the sides of this
-  // block that lie on a cube edge (block-uniform).  Fix-up thread tid < 4 BM
-  // owns strip cell jl of side tid / BM: it interpolates that cell's ghost
-  // layers along the neighbour's grid lines and reconstructs the neighbour's
-  // edge state in the neighbour's frame.  Its table entries are issued here.
+  // block that lie on a cube edge (block-uniform).  Fix-up thread tid < 4 BM F
+  // owns field pf of strip cell pjl of side pside: it interpolates that cell's
+  // ghost layers along the neighbour's grid lines and reconstructs the
+  // neighbour's edge state in the neighbour's frame (one field per thread, so
+  // the F fields run on F waves / SIMDs side by side).  Its table entries are
+  // issued here.
   int bsides = 0;
   if constexpr (RECON) {
     const int pe = a.pedge[tile];
     bsides = (x0 == 0 ? (pe & 1) : 0) | (x0 + BX >= n ? (pe & 2) : 0) | (y0 == 0 ? (pe & 4) : 0) |
              (y0 + BY >= n ? (pe & 8) : 0);
   }
-  const int pside = tid / BM, pjl = tid - pside * BM;
+  constexpr int NPF = RECON ? 4 * BM * F : 0;
+  static_assert(NPF <= NT, "one fix-up thread per (side, strip cell, field)");
+  int pf, pslt, pside, pjl;
+  bool pown;
+  if (pew) {
+    // border wave of slot PEW_SX: sides W, E; of slot PEW_SY: sides S, N.
+    // lane = side bit (5) | strip cell (4..1) | field pair (0): fields pf, pf + 1
+    const int lane = tid & 63;
+    pside = (eslot == PEW_SY ? 2 : 0) + (lane >> 5);
+    pjl = (lane >> 1) & (BM - 1);
+    pf = F == 4 ? 2 * (lane & 1) : 0;
+    pown = (eslot == PEW_SX || eslot == PEW_SY) && (F == 4 || (lane & 1) == 0);
+  } else {
+    pf = tid / (4 * BM);
+    pown = tid < NPF;
+    pside = (tid - pf * (4 * BM)) / BM;
+    pjl = tid - pf * (4 * BM) - pside * BM;
+  }
+  pslt = pside * BM + pjl;
   const int pj = (pside < 2 ? y0 : x0) + pjl;           // strip cell (tile-local, along the side)
-  const bool pact = RECON && tid < 4 * BM && ((bsides >> pside) & 1) && pjl < (pside < 2 ? BY : BX) && pj < n;
+  const bool pin = RECON && pown && pjl < (pside < 2 ? BY : BX) && pj < n;   // a strip cell of this tile
+  const bool pact = pin && ((bsides >> pside) & 1);
   int pb[KG];
   T pt_[KG];
-  if (pact) {
+  // (issued for every tile side, not only panel edges: the tables cover all
+  // four sides, and the loads then need not wait for the pedge word)
+  if (pin) {
 #pragma unroll
     for (int k = 0; k < KG; ++k) {
       const unsigned ti = (unsigned)(((tile * 4 + pside) * 3 + k) * n + pj);
@@ -400,6 +445,21 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       load_win(wly, wlx, v);
     }
     put(wly, wlx, v);
+    if constexpr (RECON) {
+      if (bsides && !own && !pew) {  // a raw panel-edge ghost the fix-up interpolates from
+        const int x = x0 + wlx - NG, y = y0 + wly - NG;
+        const bool inx = (x >= 0) & (x < n), iny = (y >= 0) & (y < n);
+        int side = -1, k = 0, al = 0;
+        if (iny && x < 0) { side = 0; k = -1 - x; al = wly; }
+        else if (iny && x >= n) { side = 1; k = x - n; al = wly; }
+        else if (inx && y < 0) { side = 2; k = -1 - y; al = wlx; }
+        else if (inx && y >= n) { side = 3; k = y - n; al = wlx; }
+        if (side >= 0 && k < KG && ((bsides >> side) & 1)) {
+#pragma unroll
+          for (int f = 0; f < F; ++f) s_raw[side][k][f][al] = s_w[f][wly][wlx];   // primitives, as put() stored them
+        }
+      }
+    }
   }
   if constexpr (P == 2) {
     if (tid < 3 * (BX + 1)) {
@@ -424,66 +484,73 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   // x[b]) along the strip; the neighbour's state at the edge is reconstructed
   // from [our cells interpolated at its grid line | its raw cells], exactly as
   // the neighbour block computes it, so the edge flux is single-valued.
+  // fix-up of field f for strip cell pj of side pside.  PEW reads the raw
+  // ghosts straight from the window (the lanes that replace them are the
+  // lanes of this wave, and all reads come first); the block-wide path reads
+  // them from s_raw
+  const bool plow = (pside & 1) == 0;
+  auto widx = [&](int cn, int al) {  // window index of (normal coord, along coord), tile-local
+    const int x = pside < 2 ? cn : al, y = pside < 2 ? al : cn;
+    return (y - y0 + NG) * WS + (x - x0 + NG);
+  };
+  const int pab = (pside < 2 ? y0 : x0) - NG;           // tile-local coordinate of window position 0
+  auto fix_read = [&](int f, T (&gk)[KG], T& nf, T& c) {
+    const T* wf = &s_w[f][0][0];
+    T gp[KG];
+#pragma unroll
+    for (int k = 0; k < KG; ++k) {
+      const int cg = plow ? -1 - k : n + k;
+      T g0, g1;
+      if (pew) {
+        g0 = wf[widx(cg, pb[k])];
+        g1 = wf[widx(cg, pb[k] + 1)];
+      } else {
+        g0 = s_raw[pside][k][f][pb[k] - pab];
+        g1 = s_raw[pside][k][f][pb[k] + 1 - pab];
+      }
+      gk[k] = g0 + pt_[k] * (g1 - g0);
+      const int co = plow ? k : n - 1 - k;
+      const T o0 = wf[widx(co, pb[k])], o1 = wf[widx(co, pb[k] + 1)];
+      gp[k] = o0 + pt_[k] * (o1 - o0);
+    }
+    if (pew) c = wf[widx(plow ? -1 : n, pj)];
+    else c = s_raw[pside][0][f][pj - pab];
+    T r;
+    if constexpr (KG > 1) r = s_raw[pside][KG - 1][f][pj - pab];   // raw layer 1 (replaced in the window)
+    else r = wf[widx(plow ? -2 : n + 1, pj)];
+    const T l = gp[0];
+    if constexpr (LIM == 4) {
+      const T l2 = gp[KG - 1], r2 = wf[widx(plow ? -3 : n + 2, pj)];
+      const T aL = T(7.0 / 12.0) * (l + c) - T(1.0 / 12.0) * (l2 + r);
+      const T aR = T(7.0 / 12.0) * (c + r) - T(1.0 / 12.0) * (l + r2);
+      const bool flat = (aR - c) * (c - aL) <= T(0);
+      const T d = aR - aL;
+      const T m6 = T(6) * (c - T(0.5) * (aL + aR));
+      const bool ovl = d * m6 > d * d;
+      nf = flat ? c : (ovl ? T(3) * c - T(2) * aR : aL);
+    } else {
+      nf = c - half_slope<LIM>(c - l, r - c);
+    }
+  };
+  auto fix_write = [&](int f, const T (&gk)[KG], T nf, T c) {
+    T* wm = &s_w[f][0][0];
+#pragma unroll
+    for (int k = 0; k < KG; ++k) wm[widx(plow ? -1 - k : n + k, pj)] = gk[k];
+    s_pf[f][pslt] = nf;
+    if constexpr (SW) s_pr[f][pslt] = c;
+  };
+  auto fix_sound = [&]() {   // raw sound speed of the neighbour cell (never replaced)
+    if constexpr (SW) s_pr[FL - 1][pslt] = (&s_w[FL - 1][0][0])[widx(plow ? -1 : n, pj)];
+  };
   if constexpr (RECON) {
-    if (bsides) {                      // block-uniform
-      T gk[KG][F], nf[F], r0v[FL];
-      const bool low = (pside & 1) == 0;
-      auto widx = [&](int cn, int al) {  // window index of (normal coord, along coord), tile-local
-        const int x = pside < 2 ? cn : al, y = pside < 2 ? al : cn;
-        return (y - y0 + NG) * WS + (x - x0 + NG);
-      };
-      const T* w0 = &s_w[0][0][0];
+    if (bsides && !pew) {              // block-uniform
       if (pact) {
-        T gp[KG][F];
-#pragma unroll
-        for (int k = 0; k < KG; ++k) {
-          const int cg = low ? -1 - k : n + k, co = low ? k : n - 1 - k;
-          const int ig0 = widx(cg, pb[k]), ig1 = widx(cg, pb[k] + 1);
-          const int io0 = widx(co, pb[k]), io1 = widx(co, pb[k] + 1);
-#pragma unroll
-          for (int f = 0; f < F; ++f) {
-            const T g0 = w0[f * WF + ig0], g1 = w0[f * WF + ig1];
-            gk[k][f] = g0 + pt_[k] * (g1 - g0);
-            const T o0 = w0[f * WF + io0], o1 = w0[f * WF + io1];
-            gp[k][f] = o0 + pt_[k] * (o1 - o0);
-          }
-        }
-        const int i0 = widx(low ? -1 : n, pj), i1 = widx(low ? -2 : n + 1, pj);
-#pragma unroll
-        for (int f = 0; f < FL; ++f) r0v[f] = w0[f * WF + i0];
-#pragma unroll
-        for (int f = 0; f < F; ++f) {
-          const T c = r0v[f], r = w0[f * WF + i1], l = gp[0][f];
-          if constexpr (LIM == 4) {
-            const T l2 = gp[1][f], r2 = w0[f * WF + widx(low ? -3 : n + 2, pj)];
-            const T aL = T(7.0 / 12.0) * (l + c) - T(1.0 / 12.0) * (l2 + r);
-            const T aR = T(7.0 / 12.0) * (c + r) - T(1.0 / 12.0) * (l + r2);
-            const bool flat = (aR - c) * (c - aL) <= T(0);
-            const T d = aR - aL;
-            const T m6 = T(6) * (c - T(0.5) * (aL + aR));
-            const bool ovl = d * m6 > d * d;
-            nf[f] = flat ? c : (ovl ? T(3) * c - T(2) * aR : aL);
-          } else {
-            nf[f] = c - half_slope<LIM>(c - l, r - c);
-          }
-        }
+        T gk[KG], nf, c;
+        fix_read(pf, gk, nf, c);
+        fix_write(pf, gk, nf, c);
+        if (pf == 0) fix_sound();
       }
-      __syncthreads();                 // every raw value is read before any is replaced
-      if (pact) {
-        T* wm = &s_w[0][0][0];
-#pragma unroll
-        for (int k = 0; k < KG; ++k) {
-          const int ig = widx(low ? -1 - k : n + k, pj);
-#pragma unroll
-          for (int f = 0; f < F; ++f) wm[f * WF + ig] = gk[k][f];
-        }
-#pragma unroll
-        for (int f = 0; f < F; ++f) s_pf[f][tid] = nf[f];
-        if constexpr (SW) {
-#pragma unroll
-          for (int f = 0; f < FL; ++f) s_pr[f][tid] = r0v[f];
-        }
-      }
+      STAMP(11);
       __syncthreads();
     }
   }
@@ -537,6 +604,26 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   // x-edge (e_r, e_c) lies between cells e_c - 1 and e_c of row e_r (face tasks
   // e_r (BX + 2) + e_c and + 1); y-edge (e_r, e_c) between rows e_r - 1 and e_r
   // (face tasks NFX + e_r BX + e_c and + BX).
+  if constexpr (PEW) {
+    if (pew && bsides && (eslot == PEW_SX || eslot == PEW_SY)) {   // the border-edge waves (wave-uniform)
+      if (pact) {
+        constexpr int NF = F == 4 ? 2 : 1;
+        T gk[NF][KG], nf[NF], c[NF];
+#pragma unroll
+        for (int i = 0; i < NF; ++i) fix_read(pf + i, gk[i], nf[i], c[i]);   // every read first
+#pragma unroll
+        for (int i = 0; i < NF; ++i) fix_write(pf + i, gk[i], nf[i], c[i]);
+        if (pf == 0) fix_sound();
+      }
+      // LDS operations of one wave complete in order: the flux reads below see
+      // the writes above (the wave barrier only keeps the compiler from moving
+      // them across)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      STAMP(11);
+    }
+  }
   if (edge_ok) {
     const int fl_ = is_x ? e_r * (BX + 2) + e_c : NFX + e_r * BX + e_c;   // face task of the left cell
     const int fst = is_x ? 1 : BX;
@@ -762,6 +849,7 @@ int launch_l(const StageDesc* d, hipStream_t s) {
   Args<T> a = make_args<T>(d);
   set_magic<T, BX, BY>(a);
   a.wt = want_wt((long)d->nblocks * BX * BY) ? 1 : 0;
+  a.pew = (d->n % BX == 0 && d->n % BY == 0) ? 1 : 0;   // partial blocks: the block-wide fix-up
 #ifdef STSP_STAMPS
   const char* rp = std::getenv("STSP_DIAG_REPEAT");
   a.diag_repeat = rp ? std::atoi(rp) : 0;

@@ -145,6 +145,14 @@ class HipCompute:
             assert t["pe_base"].dtype == torch.int32 and t["pe_base"].shape == (T, 4, 3, n)
             assert t["pe_t"].dtype == e.dtype and t["pe_t"].shape == (T, 4, 3, n)
             assert int(t["pe_base"].min()) >= 0 and int(t["pe_base"].max()) <= max(n - 2, 0)
+            # the kernel reads the interpolation pair (b, b + 1) of ghost layer k < KG
+            # from the block's window: -NG <= b - j <= NG - 1 for strip cell j
+            # (PLR: NG = 2, one layer; PPM: NG = 3, two layers)
+            ppm = int(phys.kernel_params().get("limiter", 0)) == 4
+            ng_k, kg = (3, 2) if ppm else (2, 1)
+            off = t["pe_base"][:, :, :kg].long() - torch.arange(n, device=t["pe_base"].device)
+            assert int(off.min()) >= -ng_k and int(off.max()) <= ng_k - 1, \
+                "panel-edge interpolation pair outside the block window"
         if self.phys_id == 2:
             assert t["mx"].shape == (T, 3, n + 1) and t["my"].shape == (T, 3, n + 1)
             assert t["cgeo"].shape == (T, n, n, 8)

@@ -57,3 +57,47 @@ def test_block_threads_matches_library():
         assert nt == block_threads(bx, by) == block_threads_formula(bx, by)
     assert L.stsp_block_threads(7, 7) == -1
     assert block_threads_formula(16, 16, w10=False) == 576
+
+
+def _edge_of_slot(slot, lane, bx=16, by=16, sx=7, sy=5):
+    """Python mirror of stage_common.h::edge_of_slot (border-edge flux slots)."""
+    nx, ny = (bx + 1) * by, bx * (by + 1)
+    ix, iy = bx - 3, by - 3
+    q, u4 = lane & 3, lane >> 2
+    b = q if q < 2 else q + (bx - 3)
+    if slot == sx:
+        return u4 * (bx + 1) + b
+    if slot == sy:
+        return nx + b * bx + u4
+    u = (slot - (slot > sy) - (slot > sx)) * 64 + lane
+    if u < by * ix:
+        r = u // ix
+        return r * (bx + 1) + 2 + (u - r * ix)
+    v = u - by * ix
+    if v < iy * bx:
+        r = v // bx
+        return nx + (2 + r) * bx + (v - r * bx)
+    return nx + ny
+
+
+def test_border_edge_slots_are_a_bijection():
+    """The PEW edge layout (panel-edge fix-up inside the border-edge waves)
+    gives every edge of a 16x16 block exactly one lane of the nine flux slots;
+    slot 7 holds exactly the x-edges at columns 0, 1, 15, 16 and slot 5 the
+    y-edges at rows 0, 1, 15, 16, on waves of SIMDs 3 and 2."""
+    bx = by = 16
+    nx, ny = (bx + 1) * by, bx * (by + 1)
+    t = _tables()
+    slots = [f for f in t["FLUX_TAB"] if f != 15]
+    assert sorted(slots) == list(range(9))
+    ids = [_edge_of_slot(s, l) for s in slots for l in range(64)]
+    real = sorted(i for i in ids if i < nx + ny)
+    assert real == list(range(nx + ny))
+    src = open(SRC).read()
+    assert "constexpr int PEW_SX = 7, PEW_SY = 5;" in src
+    flux = t["FLUX_TAB"]
+    assert flux.index(7) % 4 == 3 and flux.index(5) % 4 == 2
+    s0 = {_edge_of_slot(7, l) for l in range(64)}
+    assert s0 == {r * (bx + 1) + c for r in range(by) for c in (0, 1, bx - 1, bx)}
+    s1 = {_edge_of_slot(5, l) for l in range(64)}
+    assert s1 == {nx + r * bx + c for r in (0, 1, by - 1, by) for c in range(bx)}

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--blocks", default="16x16,16x8,8x16,32x8,8x8")
     ap.add_argument("--limit", type=int, default=0, help="launch only this many blocks (latency probe)")
+    ap.add_argument("--no-pedge", action="store_true",
+                    help="timing only: clear the panel-edge bits (no ghost interpolation; wrong numerics)")
     a = ap.parse_args()
     if a.stamps and not os.environ.get("STSP_VARIANT", "").startswith("diag"):
         os.environ["STSP_VARIANT"] = "diag"
@@ -39,11 +41,13 @@ def main():
     mk = {"swe": lambda: ShallowWater("tc5"), "adv": lambda: Advection(), "diff": lambda: Diffusion()}[a.phys]
     grid = CubedSphereGrid(a.N)
     L = TileLayout(a.N, a.t, 1, ng=2)
-    res = {"N": a.N, "t": a.t, "dtype": a.dtype, "phys": a.phys}
+    res = {"N": a.N, "t": a.t, "dtype": a.dtype, "phys": a.phys, "no_pedge": a.no_pedge}
     for bs in a.blocks.split(","):
         bx, by = map(int, bs.split("x"))
         e = Engine(mk(), L, grid=grid, dtype=dtype, device="cuda", backend="hip", block=(bx, by))
         hc = e.compute
+        if a.no_pedge and "pedge" in e.tens:
+            e.tens["pedge"].zero_()
         hc.bx, hc.by = bx, by
         hc.nbx, hc.nby = -(-L.n // bx), -(-L.n // by)
         hc.nblocks = e.plan.T * hc.nbx * hc.nby
@@ -85,7 +89,7 @@ def main():
             t0_ = st_[:, :, 0].min(axis=1)                         # block start (first wave)
             rel = st_ - t0_[:, None, None]
             names = ["start", "prefetch", "window", "barrier1", "faces+barrier", "flux", "end", "barrier2",
-                     "update_computed", "out_stored", "pushes_stored"]
+                     "update_computed", "out_stored", "pushes_stored", "pe_fixup"]
             # median over blocks of each wave's time at each stamp, relative to block start
             r["wave_stamp_cycles_median"] = {names[k]: [float(np.median(rel[:, w, k])) for w in range(nw)]
                                              for k in range(len(names))}
