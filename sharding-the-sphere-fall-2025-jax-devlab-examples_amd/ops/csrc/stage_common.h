@@ -100,6 +100,14 @@ template <int BX, int BY> struct Geom {
 #ifndef STSP_PE_WAVE
 #define STSP_PE_WAVE 1
 #endif
+// timing-only probes (wrong numerics; build variants "pnotab" / "pnoslot"):
+// skip the panel-edge table loads / the edge threads' panel-edge selects
+#ifndef STSP_PROBE_NOTAB
+#define STSP_PROBE_NOTAB 0
+#endif
+#ifndef STSP_PROBE_NOSLOT
+#define STSP_PROBE_NOSLOT 0
+#endif
 constexpr int PEW_SX = 7, PEW_SY = 5;
 template <int BX, int BY>
 __device__ __forceinline__ int edge_of_slot(int slot, int lane) {

@@ -126,6 +126,16 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     need = a.bmask[2 * bid];
     feed = a.bmask[2 * bid + 1];
   }
+  // panel-edge bits of the tile: a vector load (the compiler cannot prove the
+  // array unwritten, so no s_load), issued before the prefetch and first used
+  // after the window is loaded, so waiting for it never waits for anything
+  // else.  (Read in the prologue, its vmcnt(0) held every wave for a whole
+  // memory round trip before the window loads: +0.3 us per C96 stage.)
+  // The lane-dependent zero (mbcnt of an empty mask) keeps the compiler from
+  // treating the word as uniform: a uniform load result is moved to an SGPR
+  // with v_readfirstlane right at the load, i.e. a vmcnt(0) in the prologue.
+  int pe_word = 0;
+  if constexpr (P != 1) pe_word = a.pedge[tile + (int)__builtin_amdgcn_mbcnt_lo(0u, 0u)];
   // Thread roles.  Waves run on SIMD (wave % 4).  256-cell blocks use the
   // ten-wave map of Geom (STSP_W10).  Otherwise edge e is thread e, and since
   // SIMD 0 carries the extra waves, the own-cell waves (prefetch, sources,
@@ -281,12 +291,14 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   // neighbour's edge state in the neighbour's frame (one field per thread, so
   // the F fields run on F waves / SIMDs side by side).  Its table entries are
   // issued here.
-  int bsides = 0;
-  if constexpr (RECON) {
-    const int pe = a.pedge[tile];
-    bsides = (x0 == 0 ? (pe & 1) : 0) | (x0 + BX >= n ? (pe & 2) : 0) | (y0 == 0 ? (pe & 4) : 0) |
-             (y0 + BY >= n ? (pe & 8) : 0);
-  }
+  // sides of this block on a cube edge; evaluated where first needed (after the window)
+  auto block_sides = [&]() {
+    if constexpr (RECON)
+      return (x0 == 0 ? (pe_word & 1) : 0) | (x0 + BX >= n ? (pe_word & 2) : 0) | (y0 == 0 ? (pe_word & 4) : 0) |
+             (y0 + BY >= n ? (pe_word & 8) : 0);
+    else
+      return 0;
+  };
   constexpr int NPF = RECON ? 4 * BM * F : 0;
   static_assert(NPF <= NT, "one fix-up thread per (side, strip cell, field)");
   int pf, pslt, pside, pjl;
@@ -308,28 +320,17 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   pslt = pside * BM + pjl;
   const int pj = (pside < 2 ? y0 : x0) + pjl;           // strip cell (tile-local, along the side)
   const bool pin = RECON && pown && pjl < (pside < 2 ? BY : BX) && pj < n;   // a strip cell of this tile
-  const bool pact = pin && ((bsides >> pside) & 1);
   int pb[KG];
   T pt_[KG];
   // (issued for every tile side, not only panel edges: the tables cover all
   // four sides, and the loads then need not wait for the pedge word)
-  if (pin) {
+  if (pin && !STSP_PROBE_NOTAB) {
 #pragma unroll
     for (int k = 0; k < KG; ++k) {
       const unsigned ti = (unsigned)(((tile * 4 + pside) * 3 + k) * n + pj);
       pb[k] = *o32(a.pe_base, ti);
       pt_[k] = *o32(a.pe_t, ti);
     }
-  }
-  // the edge thread of a panel-edge edge takes the neighbour's state from the
-  // fix-up slot pslot (the neighbour is on the left of the edge when plo)
-  int pslot = -1;
-  bool plo = false;
-  if (RECON && bsides && edge_ok) {
-    if (is_x && ex_ == 0 && (bsides & 1)) { pslot = 0 * BM + ey_ - y0; plo = true; }
-    else if (is_x && ex_ == n && (bsides & 2)) { pslot = 1 * BM + ey_ - y0; }
-    else if (!is_x && ey_ == 0 && (bsides & 4)) { pslot = 2 * BM + ex_ - x0; plo = true; }
-    else if (!is_x && ey_ == n && (bsides & 8)) { pslot = 3 * BM + ex_ - x0; }
   }
   STAMP(1);
 
@@ -446,6 +447,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     }
     put(wly, wlx, v);
     if constexpr (RECON) {
+      const int bsides = block_sides();
       if (bsides && !own && !pew) {  // a raw panel-edge ghost the fix-up interpolates from
         const int x = x0 + wlx - NG, y = y0 + wly - NG;
         const bool inx = (x >= 0) & (x < n), iny = (y >= 0) & (y < n);
@@ -542,6 +544,8 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   auto fix_sound = [&]() {   // raw sound speed of the neighbour cell (never replaced)
     if constexpr (SW) s_pr[FL - 1][pslt] = (&s_w[FL - 1][0][0])[widx(plow ? -1 : n, pj)];
   };
+  const int bsides = block_sides();
+  const bool pact = pin && ((bsides >> pside) & 1);
   if constexpr (RECON) {
     if (bsides && !pew) {              // block-uniform
       if (pact) {
@@ -624,6 +628,16 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       STAMP(11);
     }
   }
+  // the edge thread of a panel-edge edge takes the neighbour's state from the
+  // fix-up slot pslot (the neighbour is on the left of the edge when plo)
+  int pslot = -1;
+  bool plo = false;
+  if (RECON && bsides && edge_ok && !STSP_PROBE_NOSLOT) {
+    if (is_x && ex_ == 0 && (bsides & 1)) { pslot = 0 * BM + ey_ - y0; plo = true; }
+    else if (is_x && ex_ == n && (bsides & 2)) { pslot = 1 * BM + ey_ - y0; }
+    else if (!is_x && ey_ == 0 && (bsides & 4)) { pslot = 2 * BM + ex_ - x0; plo = true; }
+    else if (!is_x && ey_ == n && (bsides & 8)) { pslot = 3 * BM + ex_ - x0; }
+  }
   if (edge_ok) {
     const int fl_ = is_x ? e_r * (BX + 2) + e_c : NFX + e_r * BX + e_c;   // face task of the left cell
     const int fst = is_x ? 1 : BX;
@@ -642,7 +656,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
         wl = s_fp[0][fl_];
         wr = s_fm[0][fl_ + fst];
       }
-      if (pslot >= 0) {
+      if (!STSP_PROBE_NOSLOT && pslot >= 0) {
         if (plo) wl = s_pf[0][pslot];
         else wr = s_pf[0][pslot];
       }
@@ -665,7 +679,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 #pragma unroll
         for (int f = 0; f < 4; ++f) { wl[f] = s_fp[f][fl_]; wr[f] = s_fm[f][fl_ + fst]; }
       }
-      if (pslot >= 0) {                 // panel edge: the neighbour's state and raw cell
+      if (!STSP_PROBE_NOSLOT && pslot >= 0) {   // panel edge: the neighbour's state and raw cell
         if (plo) {
 #pragma unroll
           for (int f = 0; f < 4; ++f) wl[f] = s_pf[f][pslot];
