@@ -93,8 +93,11 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   // interpolated ghosts can replace the raw ones in the window without a
   // barrier between the reads and the writes
   constexpr int EM = EX > EY ? EX : EY;
-  constexpr bool RAWC = RECON;                 // the block-wide fix-up's raw copy
-  __shared__ T s_raw[RAWC ? 4 : 1][RAWC ? KG : 1][RAWC ? F : 1][RAWC ? EM : 1];
+  // It lives in the flux array, which nothing writes before the flux phase
+  // (LDS per block decides how many blocks share a CU on the large grids:
+  // 16x8 fp64 SWE 29 -> 26.6 KB, six blocks per CU instead of five).
+  static_assert(4 * KG * F * EM <= F * NE, "the raw strip copy fits in the flux array");
+  T (&s_raw)[4][KG][F][EM] = *reinterpret_cast<T (*)[4][KG][F][EM]>(&s_fl[0][0]);
 
   const int n = a.n, S = a.S, nn = n * n, mg = a.mg, pw = a.pw;
   const int nbx = (n + BX - 1) / BX, nby = (n + BY - 1) / BY;
@@ -323,15 +326,22 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   int pb[KG];
   T pt_[KG];
   // (issued for every tile side, not only panel edges: the tables cover all
-  // four sides, and the loads then need not wait for the pedge word)
-  if (pin && !STSP_PROBE_NOTAB) {
+  // four sides, and the loads then need not wait for the pedge word).  The
+  // blocks that run several per CU (all but the 640-thread 16x16 map) load
+  // them after the window instead: held across the window phase they cost
+  // three VGPRs there, which is what decides the waves per SIMD.
+  constexpr bool LATE_TAB = !Geom<BX, BY>::W10;
+  auto load_tab = [&]() {
+    if (pin && !STSP_PROBE_NOTAB) {
 #pragma unroll
-    for (int k = 0; k < KG; ++k) {
-      const unsigned ti = (unsigned)(((tile * 4 + pside) * 3 + k) * n + pj);
-      pb[k] = *o32(a.pe_base, ti);
-      pt_[k] = *o32(a.pe_t, ti);
+      for (int k = 0; k < KG; ++k) {
+        const unsigned ti = (unsigned)(((tile * 4 + pside) * 3 + k) * n + pj);
+        pb[k] = *o32(a.pe_base, ti);
+        pt_[k] = *o32(a.pe_t, ti);
+      }
     }
-  }
+  };
+  if constexpr (!LATE_TAB) load_tab();
   STAMP(1);
 
   // ---- 0b. direct xGMI: wait for the peers whose ghosts this block reads ------
@@ -548,6 +558,9 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   const bool pact = pin && ((bsides >> pside) & 1);
   if constexpr (RECON) {
     if (bsides && !pew) {              // block-uniform
+      if constexpr (LATE_TAB) {
+        if (pact) load_tab();
+      }
       if (pact) {
         T gk[KG], nf, c;
         fix_read(pf, gk, nf, c);
@@ -843,8 +856,17 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 }
 
 
+// Waves per SIMD: the large grids run several blocks per CU, and the VGPR
+// count decides how many (512 / ceil8(vgprs) waves per SIMD).  The panel-edge
+// treatment took the fp64 16x8 / 8x8 bodies from 93 to 100 VGPRs, i.e. from 5
+// to 4 waves per SIMD (C180 stage 11.0 -> 15.1 us even without panel edges,
+// C720 143 -> 169 us); asking for 5 keeps them at <= 96.  The 640-thread
+// 16x16 blocks run one per CU at C96 and are left alone.
+template <int BX, int BY> struct StageOcc { static constexpr int WPE = Geom<BX, BY>::W10 ? 1 : 5; };
+
 template <typename T, int P, int BX, int BY, int LIM, bool REMOTE, bool LIST, bool XG>
-__global__ __launch_bounds__((Geom<BX, BY>::NT)) void stage_kernel(Args<T> a) {
+__global__ __launch_bounds__((Geom<BX, BY>::NT)) __attribute__((amdgpu_waves_per_eu(StageOcc<BX, BY>::WPE)))
+void stage_kernel(Args<T> a) {
   pin_args(a);
   const int bid = LIST ? a.blocks[blockIdx.x] : xcd_remap(blockIdx.x, a.nblocks);
   stage_body<T, P, BX, BY, LIM, REMOTE, false, XG>(a, bid);
