@@ -223,7 +223,7 @@ class LowRankDiffusion:
 
     def __init__(self, N: int, L: float = 1.0, kappa: float = 1.0, bc: str = "dirichlet",
                  eps: float = 1e-10, max_rank: Optional[int] = None, dtype=torch.float64, device="cpu",
-                 backend: str = "torch"):
+                 backend: str = "torch", substeps: int = 1):
         self.h = L / (N + 1) if bc == "dirichlet" else L / N
         self.bc = bc
         self.kappa = kappa
@@ -233,15 +233,28 @@ class LowRankDiffusion:
         if backend not in ("torch", "hip"):
             raise ValueError(f"unknown backend {backend!r}")
         self.backend = backend
+        # explicit steps per call; the factors grow exactly (rank x 2 per step)
+        # and are recompressed once at the end (the hip step is latency-bound:
+        # one host round trip per call, so rounding every second step halves
+        # its cost per step; tools/tt_bench.py)
+        if substeps < 1:
+            raise ValueError("substeps must be >= 1")
+        self.substeps = substeps
         # the hip path never forms the N x N operator
         self.D = second_difference(N, self.h, bc, dtype, device) if backend == "torch" else None
 
     def step(self, U: LowRankField, dt: float) -> LowRankField:
+        """``substeps`` explicit steps of size dt, one recompression."""
         if self.backend == "hip":
             return self._step_hip(U, dt)
         c = dt * self.kappa
-        A = torch.cat([U.A, c * (self.D @ U.A), c * U.A], dim=1)
-        B = torch.cat([U.B, U.B, self.D @ U.B], dim=1)
+        if self.substeps == 1:
+            A = torch.cat([U.A, c * (self.D @ U.A), c * U.A], dim=1)
+            B = torch.cat([U.B, U.B, self.D @ U.B], dim=1)
+            return recompress(A, B, self.eps, self.max_rank)
+        A, B = U.A, U.B
+        for _ in range(self.substeps):     # exact rank-doubling form [A, c D A] [B + c D B, B]^T
+            A, B = torch.cat([A, c * (self.D @ A)], dim=1), torch.cat([B + c * (self.D @ B), B], dim=1)
         return recompress(A, B, self.eps, self.max_rank)
 
     def _step_hip(self, U: LowRankField, dt: float) -> LowRankField:
@@ -259,23 +272,25 @@ class LowRankDiffusion:
         from ..ops import native
         L = native.require_native()
         N, r = U.A.shape
-        if 2 * r > 64:
-            raise ValueError(f"hip low-rank step supports rank <= 32 (got {r})")
+        ns = self.substeps
+        if (r << ns) > 64:
+            raise ValueError(f"hip low-rank step: rank {r} x 2^{ns} substeps exceeds the 64-column kernels")
         A = U.A if U.A.stride(1) == 1 else U.A.contiguous()
         B = U.B if U.B.stride(1) == 1 else U.B.contiguous()
         dev, dt_ = A.device, A.dtype
-        key = (N, r, dt_, dev)
+        k = r << ns
+        key = (N, r, ns, dt_, dev)
         if getattr(self, "_wkey", None) != key:
-            self._ws = torch.empty(L.stsp_tt_step_workspace(N, r), dtype=dt_, device=dev)
-            self._hbuf = torch.empty(4 * (2 * r) ** 2, dtype=torch.float64).pin_memory()
+            self._ws = torch.empty(L.stsp_tt_step_workspace2(N, r, ns), dtype=dt_, device=dev)
+            self._hbuf = torch.empty(4 * k * k, dtype=torch.float64).pin_memory()
             self._wkey = key
-        rmax = 2 * r if self.max_rank is None else min(2 * r, self.max_rank)
+        rmax = k if self.max_rank is None else min(k, self.max_rank)
         out = torch.empty((2, N, rmax), dtype=dt_, device=dev)
-        rn = L.stsp_tt_lr_step(native.dtype_code(dt_), native.ptr(A), A.stride(0), native.ptr(B), B.stride(0), N, r,
-                               dt * self.kappa,
-                               1.0 / (self.h * self.h), int(self.bc == "periodic"), self.eps,
-                               self.max_rank or 0, native.ptr(self._ws), native.ptr(self._hbuf),
-                               native.ptr(out[0]), native.ptr(out[1]), rmax, native.current_stream_handle())
+        rn = L.stsp_tt_lr_step2(native.dtype_code(dt_), native.ptr(A), A.stride(0), native.ptr(B), B.stride(0), N, r,
+                                ns, dt * self.kappa,
+                                1.0 / (self.h * self.h), int(self.bc == "periodic"), self.eps,
+                                self.max_rank or 0, native.ptr(self._ws), native.ptr(self._hbuf),
+                                native.ptr(out[0]), native.ptr(out[1]), rmax, native.current_stream_handle())
         if rn <= 0:
             raise RuntimeError(f"stsp_tt_lr_step failed ({rn})")
         return LowRankField(out[0, :, :rn], out[1, :, :rn])
@@ -433,30 +448,35 @@ class CubedSphereLowRankDiffusion:
         import ctypes
         from ..ops import native, tt_ops
         L = native.require_native()
-        k = ex[0][0].shape[1]
-        if k > 64:
-            raise ValueError(f"hip cube step supports rank <= 30 (k = {k})")
-        G = torch.empty((6, 2, k, k), dtype=ex[0][0].dtype, device=ex[0][0].device)
-        for p, (Ah, Bh) in enumerate(ex):
-            tt_ops.gram(Ah, Ah, out=G[p, 0])
-            tt_ops.gram(Bh, Bh, out=G[p, 1])
-        Gh = G.double().cpu()                   # the one host round trip of the step
+        ks = [Ah.shape[1] for Ah, _ in ex]          # 2 r_p + 4: the panels' ranks differ
+        if max(ks) > 64:
+            raise ValueError(f"hip cube step supports rank <= 30 (k = {max(ks)})")
+        Gs = []
+        for (Ah, Bh), k in zip(ex, ks):
+            G = torch.empty((2, k, k), dtype=Ah.dtype, device=Ah.device)
+            tt_ops.gram(Ah, Ah, out=G[0])
+            tt_ops.gram(Bh, Bh, out=G[1])
+            Gs.append(G.reshape(-1))
+        Gh = torch.cat(Gs).double().cpu()           # the one host round trip of the step
         self.stats["host_syncs"] += 1
-        X = torch.zeros((6, k, 2 * k), dtype=torch.float64)
-        ranks = []
-        for p in range(6):
-            g = Gh[p].contiguous()
+        Xs, ranks, o = [], [], 0
+        for k in ks:
+            g = Gh[o:o + 2 * k * k].contiguous()
+            o += 2 * k * k
+            X = torch.zeros((k, 2 * k), dtype=torch.float64)
             rn = L.stsp_tt_core(k, ctypes.c_void_p(g.data_ptr()), float(self.eps), int(self.max_rank or 0),
-                                ctypes.c_void_p(X[p].data_ptr()), 2 * k)
+                                ctypes.c_void_p(X.data_ptr()), 2 * k)
             if rn <= 0:
                 raise RuntimeError(f"stsp_tt_core failed ({rn})")
+            Xs.append(X)
             ranks.append(rn)
-        Xd = X.to(device=ex[0][0].device, dtype=ex[0][0].dtype)
-        out = []
-        for p, (Ah, Bh) in enumerate(ex):
-            rn = ranks[p]
-            A2 = tt_ops.tsmm(Ah, Xd[p, :, :rn].contiguous())
-            B2 = tt_ops.tsmm(Bh, Xd[p, :, rn:2 * rn].contiguous())
+        Xd = torch.cat([X.reshape(-1) for X in Xs]).to(device=ex[0][0].device, dtype=ex[0][0].dtype)
+        out, o = [], 0
+        for (Ah, Bh), k, rn in zip(ex, ks, ranks):
+            X = Xd[o:o + 2 * k * k].view(k, 2 * k)
+            o += 2 * k * k
+            A2 = tt_ops.tsmm(Ah, X[:, :rn].contiguous())
+            B2 = tt_ops.tsmm(Bh, X[:, rn:2 * rn].contiguous())
             out.append(LowRankField(A2, B2))
         return out
 

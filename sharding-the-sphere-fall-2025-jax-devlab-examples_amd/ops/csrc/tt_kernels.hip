@@ -522,36 +522,54 @@ int stsp_tt_core(int k, const double* G, double eps, int max_rank, double* X, in
   return lr_core(k, G, G + k * k, eps, max_rank, X, ldx);
 }
 
-// One explicit factored diffusion step U' = U + c (D U + U D^T) for U = A B^T
-// (A, B: N x r, row strides lda / ldb), recompressed to rank rn <= max_rank:
-// expand (2 launches) -> MFMA Gram (2 x 2 launches) -> Gram to pinned host ->
-// host core -> maps to the device -> MFMA products into Aout / Bout (N x rn,
-// row stride ldo).  ws = device workspace (stsp_tt_step_workspace elements),
-// hbuf = pinned host buffer of 2 k^2 + 2 k^2 doubles.  Returns rn (> 0) or an
-// error (< 0).  The stream is synchronised once (for the Gram matrices).
-size_t stsp_tt_step_workspace(int N, int r) {
-  const int k = 2 * r, kp = (k + 15) / 16 * 16;
-  return (size_t)2 * N * k + 2 * (size_t)k * k + (size_t)stsp_tt_gram_blocks(N) * kp * kp + (size_t)k * 2 * k;
+// nsub explicit factored diffusion steps U' = U + c (D U + U D^T) for U = A B^T
+// (A, B: N x r, row strides lda / ldb), then ONE recompression to rank
+// rn <= max_rank: expand nsub times (2 launches each; the rank doubles every
+// step, k = 2^nsub r <= 64, exact: no truncation in between) -> MFMA Gram
+// (2 x 2 launches) -> Gram to pinned host -> host core -> maps to the device
+// -> MFMA products into Aout / Bout (N x rn, row stride ldo).  The sync and the
+// host core are paid once per nsub steps: the step is latency-bound (~70 us at
+// every N with nsub = 1, profiles/r1_tt_bench.log), so rounding every second
+// step halves its cost per step.  ws = device workspace
+// (stsp_tt_step_workspace2 elements), hbuf = pinned host buffer of 4 k^2
+// doubles.  Returns rn (> 0) or an error (< 0).
+size_t stsp_tt_step_workspace2(int N, int r, int nsub) {
+  const int k = r << nsub, kp = (k + 15) / 16 * 16;
+  return (size_t)2 * 2 * N * k + 2 * (size_t)k * k + (size_t)stsp_tt_gram_blocks(N) * kp * kp + (size_t)k * 2 * k;
 }
+size_t stsp_tt_step_workspace(int N, int r) { return stsp_tt_step_workspace2(N, r, 1); }
 
-int stsp_tt_lr_step(int dtype, const void* A, int lda, const void* B, int ldb, int N, int r, double c, double ih2,
-                    int periodic,
-                    double eps, int max_rank, void* ws, double* hbuf, void* Aout, void* Bout, int ldo,
-                    hipStream_t st) {
-  const int k = 2 * r;
-  if (N < 1 || r < 1 || k > 64) return -1;
+int stsp_tt_lr_step2(int dtype, const void* A, int lda, const void* B, int ldb, int N, int r, int nsub, double c,
+                     double ih2, int periodic, double eps, int max_rank, void* ws, double* hbuf, void* Aout,
+                     void* Bout, int ldo, hipStream_t st) {
+  if (N < 1 || r < 1 || nsub < 1 || nsub > 6) return -1;
+  const int k = r << nsub;
+  if (k > 64) return -1;
   const size_t es = dtype == 1 ? 8 : 4;
   char* w = (char*)ws;
-  void* Ah = w;
-  void* Bh = w + es * (size_t)N * k;
-  void* G = w + es * 2 * (size_t)N * k;
+  // ping-pong expansion buffers: [A-side, B-side] x 2, each N x k (row stride k)
+  void* buf[2][2] = {{w, w + es * (size_t)N * k}, {w + es * 2 * (size_t)N * k, w + es * 3 * (size_t)N * k}};
+  void* G = w + es * 4 * (size_t)N * k;
   void* part = (char*)G + es * 2 * (size_t)k * k;
   const int P = stsp_tt_gram_blocks(N);
   const int kp = (k + 15) / 16 * 16;
   void* dX = (char*)part + es * (size_t)P * kp * kp;
   int rc;
-  if ((rc = stsp_tt_expand(dtype, A, lda, Ah, k, N, r, 1.0, 0.0, 0.0, c, ih2, periodic, st))) return rc;
-  if ((rc = stsp_tt_expand(dtype, B, ldb, Bh, k, N, r, 1.0, c, 1.0, 0.0, ih2, periodic, st))) return rc;
+  const void* srcA = A;
+  const void* srcB = B;
+  int sa = lda, sb = ldb, rr = r, cur = 0;
+  for (int s = 0; s < nsub; ++s, rr *= 2) {
+    void* dA = buf[cur][0];
+    void* dB = buf[cur][1];
+    if ((rc = stsp_tt_expand(dtype, srcA, sa, dA, 2 * rr, N, rr, 1.0, 0.0, 0.0, c, ih2, periodic, st))) return rc;
+    if ((rc = stsp_tt_expand(dtype, srcB, sb, dB, 2 * rr, N, rr, 1.0, c, 1.0, 0.0, ih2, periodic, st))) return rc;
+    srcA = dA;
+    srcB = dB;
+    sa = sb = 2 * rr;
+    cur ^= 1;
+  }
+  void* Ah = (void*)srcA;
+  void* Bh = (void*)srcB;
   if ((rc = stsp_tt_gram(dtype, Ah, k, Ah, k, N, k, k, part, P, G, k, 1.0, st))) return rc;
   if ((rc = stsp_tt_gram(dtype, Bh, k, Bh, k, N, k, k, part, P, (char*)G + es * k * k, k, 1.0, st))) return rc;
   double* hG = hbuf;
@@ -572,6 +590,13 @@ int stsp_tt_lr_step(int dtype, const void* A, int lda, const void* B, int ldb, i
   if ((rc = stsp_tt_mm(dtype, Ah, k, dX, 2 * k, Aout, ldo, N, k, rn, 1.0, 0.0, st))) return rc;
   if ((rc = stsp_tt_mm(dtype, Bh, k, (char*)dX + es * rn, 2 * k, Bout, ldo, N, k, rn, 1.0, 0.0, st))) return rc;
   return rn;
+}
+
+int stsp_tt_lr_step(int dtype, const void* A, int lda, const void* B, int ldb, int N, int r, double c, double ih2,
+                    int periodic, double eps, int max_rank, void* ws, double* hbuf, void* Aout, void* Bout, int ldo,
+                    hipStream_t st) {
+  return stsp_tt_lr_step2(dtype, A, lda, B, ldb, N, r, 1, c, ih2, periodic, eps, max_rank, ws, hbuf, Aout, Bout, ldo,
+                          st);
 }
 
 }  // extern "C"

@@ -117,6 +117,10 @@ def _declare_tt(L):
     L.stsp_tt_step_workspace.restype = ctypes.c_size_t
     L.stsp_tt_lr_step.argtypes = [ci, vp, ci, vp, ci, ci, ci, cd, cd, ci, cd, ci, vp, vp, vp, vp, ci, vp]
     L.stsp_tt_lr_step.restype = ci
+    L.stsp_tt_step_workspace2.argtypes = [ci, ci, ci]
+    L.stsp_tt_step_workspace2.restype = ctypes.c_size_t
+    L.stsp_tt_lr_step2.argtypes = [ci, vp, ci, vp, ci, ci, ci, ci, cd, cd, ci, cd, ci, vp, vp, vp, vp, ci, vp]
+    L.stsp_tt_lr_step2.restype = ci
 
 
 def available() -> bool:

@@ -140,3 +140,22 @@ def test_cube_low_rank_halo_is_the_dense_halo():
         assert torch.allclose(g[1], P[p, 1:-1, -1], atol=1e-12)
         assert torch.allclose(g[2], P[p, 0, 1:-1], atol=1e-12)
         assert torch.allclose(g[3], P[p, -1, 1:-1], atol=1e-12)
+
+
+@pytest.mark.parametrize("substeps", [2, 3])
+def test_low_rank_diffusion_substeps_exact_between_recompressions(substeps):
+    """substeps > 1: the factors grow exactly ([A, c D A], [B + c D B, B] per
+    step) and are recompressed once per call; equal to dense stepping."""
+    N = 64
+    x = torch.linspace(0, 1, N + 2, dtype=torch.float64)[1:-1]
+    U = torch.outer(torch.sin(math.pi * x), torch.sin(2 * math.pi * x)) + \
+        0.3 * torch.outer(torch.sin(3 * math.pi * x), torch.sin(math.pi * x))
+    s = tt.LowRankDiffusion(N, eps=1e-12, substeps=substeps)
+    dt = 0.5 * s.dt_max
+    F, D = tt.LowRankField.from_dense(U, 1e-12), U.clone()
+    for _ in range(12 // substeps):
+        F = s.step(F, dt)
+    for _ in range(12):
+        D = s.dense_step(D, dt)
+    assert float((F.dense() - D).norm() / D.norm()) < 1e-13
+    assert F.rank == 2
