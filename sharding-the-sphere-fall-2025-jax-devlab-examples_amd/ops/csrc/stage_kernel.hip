@@ -862,7 +862,10 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 // to 4 waves per SIMD (C180 stage 11.0 -> 15.1 us even without panel edges,
 // C720 143 -> 169 us); asking for 5 keeps them at <= 96.  The 640-thread
 // 16x16 blocks run one per CU at C96 and are left alone.
-template <int BX, int BY> struct StageOcc { static constexpr int WPE = Geom<BX, BY>::W10 ? 1 : 5; };
+#ifndef STSP_WPE
+#define STSP_WPE 5
+#endif
+template <int BX, int BY> struct StageOcc { static constexpr int WPE = Geom<BX, BY>::W10 ? 1 : STSP_WPE; };
 
 template <typename T, int P, int BX, int BY, int LIM, bool REMOTE, bool LIST, bool XG>
 __global__ __launch_bounds__((Geom<BX, BY>::NT)) __attribute__((amdgpu_waves_per_eu(StageOcc<BX, BY>::WPE)))
