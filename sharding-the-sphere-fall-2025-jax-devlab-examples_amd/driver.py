@@ -419,6 +419,8 @@ class Solver:
                 for k in lens[:8]:
                     if k >= per:
                         self.runner.prepare(k)
+            if deferred and ("watchdog" in iv or "metrics" in iv):
+                self._warm_checks()
             self._sync()
         wall0 = time.perf_counter()
         recoveries = 0
@@ -539,6 +541,21 @@ class Solver:
                 tot[k] = tot.get(k, 0.0) + v
             metrics.log(**rec, **tot)
         pending.append((ev, work))
+
+    def _warm_checks(self) -> None:
+        """Run the watchdog and metrics reductions once before the clock
+        starts.  Their first use in a process loads the kernels' code objects
+        and the first pinned host blocks: measured on a 2-day C48 run
+        (tools/run_phase_probe.py, profiles/r2_run_phases) that cost ~15 ms
+        and took the run from 14.6 to 156 us/step with only the watchdog on."""
+        flag = torch.stack([torch.isfinite(e.tiles_view()).all() for e in self.engines]).all()
+        vals = [v.reshape(()).to(torch.float64) for e in self.engines
+                for v in e.physics.diagnostics(e.tiles_view(), e.tens).values()]
+        hf = torch.empty((), dtype=torch.bool, pin_memory=True)
+        hf.copy_(flag, non_blocking=True)
+        hv = torch.empty((len(vals),), dtype=torch.float64, pin_memory=True)
+        hv.copy_(torch.stack(vals), non_blocking=True)
+        torch.cuda.current_stream().synchronize()
 
     def _watchdog(self, pending: List[Any], deferred: bool) -> bool:
         """True while the state is finite.  Deferred (single process): the
