@@ -52,8 +52,6 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--N", type=int, default=96)
     ap.add_argument("--tiles-per-edge", type=int, default=2)
-    ap.add_argument("--lead-steps", type=int, default=0,
-                    help="replay the first L timed steps as their own short graph (launch-overlap probe)")
     ap.add_argument("--case", default="tc5")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--integrator", default="ssprk3")
@@ -205,7 +203,6 @@ def main():
             elif comm == "rccl":
                 nc = create_nccl_comm(rank, world, local)
             runner = NativeStepper(eng, nccl_comm=nc, use_graph=True, steps_per_graph=spg, xgmi=xg)
-            runner.lead_periods = a.lead_steps // runner.period
         elif runtime == "graph":
             runner = GraphStepper(eng, spg)
         return eng, runner, xg

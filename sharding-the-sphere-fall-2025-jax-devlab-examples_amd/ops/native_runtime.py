@@ -194,7 +194,6 @@ class NativeStepper:
         self._cxx_graph = self.use_graph and os.environ.get("STSP_NATIVE_GRAPH") == "1"
         d.use_graph = 1 if self._cxx_graph else 0
         self.graph_periods = max(1, steps_per_graph // period)
-        self.lead_periods = 0
         d.graph_periods = self.graph_periods
         self._graphs = {}          # periods -> torch.cuda.CUDAGraph
         self._primed = set()       # graph lengths replayed at least once
@@ -293,16 +292,10 @@ class NativeStepper:
         ``steps_per_graph`` chunks, then one graph for the remainder, so every
         step of a run is a graph replay whatever ``nsteps`` is."""
         periods = nsteps // self.period
-        # lead_periods: a short first graph, so the GPU starts while the host
-        # is still launching the long one (hipGraphLaunch returns before the
-        # first kernel of its graph runs; profiles/r2_launch)
-        lead = min(self.lead_periods, periods - 1) if self.lead_periods > 0 else 0
-        chunks = [lead] if lead > 0 else []
-        rest = periods - max(lead, 0)
         k = self.graph_periods
-        chunks += [k] * (rest // k)
-        if rest % k:
-            chunks.append(rest % k)
+        chunks = [k] * (periods // k)
+        if periods % k:
+            chunks.append(periods % k)
         return chunks
 
     def prepare(self, nsteps: int, prime: bool = True) -> None:
