@@ -22,6 +22,7 @@ from .ops.halo import (exchange_edge_pair, extract_boundary_data, make_halo_exch
                        remove_ghosts, add_ghosts)
 from .engine import Engine, GraphStepper, VirtualCluster
 from .driver import Solver, make_physics
+from .ensemble import Ensemble
 
 __all__ = [
     "apply_operations", "create_communication_schedule", "derive_edge_pairs", "edge_coloring", "neighbor_cell",
@@ -29,5 +30,5 @@ __all__ = [
     "TileMesh", "TileSharding", "setup_sharding", "Config", "load_config", "save_config", "CubedSphereGrid",
     "get_integrator", "ShallowWater", "Advection", "Diffusion", "exchange_edge_pair", "extract_boundary_data",
     "make_halo_exchange", "set_ghost_data", "remove_ghosts", "add_ghosts", "Engine", "GraphStepper",
-    "VirtualCluster", "Solver", "make_physics",
+    "VirtualCluster", "Solver", "make_physics", "Ensemble",
 ]
