@@ -2,6 +2,8 @@
 # Does the border-slot edge order cost through its scattered edge-coefficient
 # loads?  Stage launch time (C96 fp64 16x16, graph-timed) of production vs the
 # pcoef probe (coefficients loaded in canonical edge order: timing only).
+# Historical: the STSP_PROBE_COEF macro and the pcoef build variant were removed
+# after the probe lost (profiles/r2_pe/README.md, v4); re-add them to rerun.
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/${TAG:-pcoef}
