@@ -6,6 +6,8 @@
     roofline                                           slide-19 roofline / TT model for MI355X
     plot HISTORY.zarr FIELD OUTDIR [--log] [--products frames,band,six] [--every K]
                                                        sphere frames, equatorial band, six-panel
+    ensemble CONFIG.yaml [--members M] [--amplitude A] [--days D | --nsteps K]
+                                                       perturbed members of one config on one device
     build                                              compile the gfx950 library
 """
 import argparse
@@ -33,6 +35,12 @@ def main(argv=None):
     p.add_argument("--log", action="store_true")
     p.add_argument("--products", default="frames,band,six")
     p.add_argument("--every", type=int, default=1)
+    en = sub.add_parser("ensemble")
+    en.add_argument("config")
+    en.add_argument("--members", type=int, default=2)
+    en.add_argument("--amplitude", type=float, default=1e-4)
+    en.add_argument("--days", type=float)
+    en.add_argument("--nsteps", type=int)
     sub.add_parser("build")
     a = ap.parse_args(argv)
 
@@ -55,6 +63,9 @@ def main(argv=None):
         for f in history_products(a.history, a.field, a.outdir, log=a.log, every=a.every,
                                   products=tuple(a.products.split(","))):
             print(f)
+        return 0
+    if a.cmd == "ensemble":
+        print(json.dumps(run_ensemble(a.config, a.members, a.amplitude, a.days, a.nsteps), default=float))
         return 0
     from .utils.config import load_config
     if a.cmd == "run" and load_config(a.config).physics.model == "planar_swe":
@@ -89,6 +100,37 @@ def main(argv=None):
                     print(f)
             print(sphere_plot(g[0], s.grid, os.path.join(out, f"{s.fields[0]}_final.png"), log=log))
     return 0
+
+
+def run_ensemble(config, members: int, amplitude: float, days=None, nsteps=None) -> dict:
+    """``members`` perturbed copies of a run configuration stepped together
+    on one device (``stsphere.Ensemble``); returns throughput and spread."""
+    import math
+    import time
+    import torch
+    from .ensemble import Ensemble
+    from .models.geometry import DAY
+    from .utils.config import load_config
+    c = load_config(config)
+    ens = Ensemble.from_config(c, members, amplitude=amplitude)
+    if nsteps is None:
+        d = days if days is not None else c.time.days
+        nsteps = int(math.ceil(d * DAY / ens.dt - 1e-9)) if d is not None else (c.time.nsteps or 1)
+    ens.prepare(nsteps)
+    before = ens.spread()
+    sync = torch.cuda.synchronize if ens.native else (lambda: None)
+    sync()
+    t0 = time.perf_counter()
+    ens.run(nsteps)
+    sync()
+    wall = time.perf_counter() - t0
+    after = ens.spread()
+    ens.close()
+    cells = 6 * c.grid.N ** 2
+    return {"members": members, "steps": nsteps, "dt": ens.dt, "wall_s": wall,
+            "aggregate_cell_updates_per_s": members * cells * nsteps / max(wall, 1e-12),
+            "native": ens.native, "h_mean": after["mean"], "h_spread_rms_initial": before["spread_rms"],
+            "h_spread_rms_final": after["spread_rms"]}
 
 
 if __name__ == "__main__":

@@ -72,6 +72,33 @@ class Ensemble:
                 self.runners.append(NativeStepper(e, use_graph=True, steps_per_graph=steps_per_graph))
                 self.streams.append(torch.cuda.Stream(e.device))
 
+    @classmethod
+    def from_config(cls, config, members: int, amplitude: float = 1e-4, seed: int = 0,
+                    steps_per_graph: int = 100) -> "Ensemble":
+        """Members of a run configuration (YAML path, dict or Config): the
+        grid, physics, dtype, integrator and dt of ``Solver``; each member is
+        a whole grid on one device (cuda:0 for ``device_type: gpu``)."""
+        from .driver import make_physics
+        from .models.geometry import EARTH_RADIUS
+        from .utils.config import load_config
+        c = load_config(config)
+        gpu = c.parallelization.device_type == "gpu"
+        if gpu and not torch.cuda.is_available():
+            raise RuntimeError("device_type 'gpu' requested but no GPU is visible (use device_type: cpu)")
+        device = torch.device("cuda:0") if gpu else torch.device("cpu")
+        backend = c.runtime.backend
+        if backend == "auto":
+            backend = "hip" if gpu else "torch"
+        dtype = {"float64": torch.float64, "fp64": torch.float64, "float32": torch.float32,
+                 "fp32": torch.float32}[c.grid.dtype]
+        phys0 = make_physics(c.physics)
+        grid = CubedSphereGrid(c.grid.N, c.grid.radius or EARTH_RADIUS)
+        layout = TileLayout(c.grid.N, c.parallelization.tiles_per_edge, 1, ng=max(c.grid.halo, phys0.halo))
+        dt = c.time.dt or (phys0.max_dt(grid, c.time.cfl) if c.time.cfl else phys0.max_dt(grid))
+        return cls(lambda: make_physics(c.physics), layout, members, amplitude=amplitude, seed=seed, grid=grid,
+                   dtype=dtype, device=device, backend=backend, integrator=c.time.integrator, dt=dt,
+                   steps_per_graph=steps_per_graph)
+
     @property
     def members(self) -> int:
         return len(self.engines)

@@ -60,3 +60,15 @@ def test_ensemble_native_concurrent_members_bitwise():
         alone = _alone(grid, L, ens, m, 6, "cuda", "hip")
         assert torch.equal(got[m], alone), float((got[m] - alone).abs().max())
     ens.close()
+
+
+def test_ensemble_cli_from_config_cpu():
+    import os
+    from stsphere.__main__ import run_ensemble
+    cfg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "sharding-the-sphere-fall-2025-jax-devlab-examples_amd", "configs", "plumbing_cpu.yaml")
+    r = run_ensemble(cfg, 2, 1e-3, nsteps=2)
+    assert r["members"] == 2 and r["steps"] == 2 and not r["native"]
+    assert r["h_spread_rms_initial"] > 0 and np.isfinite(r["h_spread_rms_final"])
+    r1 = run_ensemble(cfg, 1, 1e-3, nsteps=1)
+    assert r1["h_spread_rms_initial"] == 0.0
