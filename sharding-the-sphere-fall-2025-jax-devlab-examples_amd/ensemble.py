@@ -104,9 +104,17 @@ class Ensemble:
         return len(self.engines)
 
     def prepare(self, nsteps: int) -> None:
-        """Record (and upload) every member's graphs for ``run(nsteps)``."""
-        for r in self.runners:
-            r.prepare(nsteps)
+        """Record (and upload) every member's graphs for ``run(nsteps)``,
+        each primed on the stream it will replay on (the first replay of a
+        graph on another stream pays a one-time cost again)."""
+        for m, r in enumerate(self.runners):
+            if m == 0:
+                r.prepare(nsteps)
+            else:
+                with torch.cuda.stream(self.streams[m]):
+                    r.prepare(nsteps)
+        if self.runners:
+            torch.cuda.synchronize(self.engines[0].device)
 
     def run(self, nsteps: int) -> None:
         """Advance every member ``nsteps`` steps.  Native: the members' graph
@@ -120,13 +128,23 @@ class Ensemble:
         # stream costs ~3 us/step more at C96, docs/ARCHITECTURE.md "Graph
         # replay"), the others on their own streams, ordered after the
         # caller's earlier work
+        # Launches are interleaved chunk by chunk across the members: a graph
+        # exec launched again while its previous launch is still running
+        # holds the host until that one is done, so issuing all of member 0's
+        # chunks first would keep member 1 from starting until member 0 is
+        # nearly finished (measured: no overlap at C96 with 6 chunks each).
         cur = torch.cuda.current_stream(self.engines[0].device)
         for s in self.streams[1:]:
             s.wait_stream(cur)
-        self.runners[0].run(nsteps)
-        for r, s in zip(self.runners[1:], self.streams[1:]):
-            with torch.cuda.stream(s):
-                r.run(nsteps)
+        per = self.runners[0].period
+        chunks = [c * per for c in self.runners[0].plan(nsteps)]
+        if nsteps > sum(chunks):
+            chunks.append(nsteps - sum(chunks))          # partial period: eager
+        for k in chunks:
+            self.runners[0].run(k)
+            for r, s in zip(self.runners[1:], self.streams[1:]):
+                with torch.cuda.stream(s):
+                    r.run(k)
         for s in self.streams[1:]:
             cur.wait_stream(s)
 

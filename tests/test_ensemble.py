@@ -48,16 +48,16 @@ def test_ensemble_native_concurrent_members_bitwise():
     grid = CubedSphereGrid(24)
     L = TileLayout(24, 2, 1, ng=2)
     ens = Ensemble(lambda: ShallowWater("tc5"), L, 2, amplitude=1e-4, grid=grid, device="cuda", backend="hip",
-                   steps_per_graph=6)
+                   steps_per_graph=4)
     assert ens.native
     for m, e in enumerate(ens.engines):
         ens0_state[m] = e.tiles_view().clone()
-    ens.prepare(6)
-    ens.run(6)
+    ens.prepare(10)
+    ens.run(10)                         # chunks 4, 4, 2, interleaved across the members
     torch.cuda.synchronize()
     got = ens.states().cpu()
     for m in range(2):
-        alone = _alone(grid, L, ens, m, 6, "cuda", "hip")
+        alone = _alone(grid, L, ens, m, 10, "cuda", "hip")
         assert torch.equal(got[m], alone), float((got[m] - alone).abs().max())
     ens.close()
 

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--N", type=int, default=96)
+    ap.add_argument("--tpe", type=int, default=2)
+    ap.add_argument("--spg", type=int, default=0, help="steps per graph (0: the whole timed run)")
     a = ap.parse_args()
     import torch
     from stsphere.ensemble import Ensemble
@@ -32,12 +34,14 @@ def main():
     from stsphere.parallel.layout import TileLayout
 
     grid = CubedSphereGrid(a.N)
-    L = TileLayout(a.N, 2, 1, ng=2)
+    L = TileLayout(a.N, a.tpe, 1, ng=2)
+    spg = a.spg or a.steps
     cells = 6 * a.N * a.N
-    res = {"N": a.N, "steps": a.steps, "dtype": "fp64", "model": "SWE TC5, SSPRK3, MC-PLR"}
+    res = {"N": a.N, "steps": a.steps, "tiles_per_edge": a.tpe, "steps_per_graph": spg, "dtype": "fp64",
+           "model": "SWE TC5, SSPRK3, MC-PLR"}
     for M in [int(m) for m in a.members.split(",")]:
         ens = Ensemble(lambda: ShallowWater("tc5"), L, M, amplitude=1e-4, grid=grid, device="cuda",
-                       backend="hip", steps_per_graph=a.steps)
+                       backend="hip", steps_per_graph=spg)
         init = [e.tiles_view().clone() for e in ens.engines]
         ens.prepare(a.steps)
         ens.prepare(a.warmup)
