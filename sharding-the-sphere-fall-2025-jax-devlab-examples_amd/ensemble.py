@@ -10,8 +10,9 @@ native runner (one hipGraph per chunk length) and HIP stream, and the
 members' graphs run concurrently: one member's launch gaps and drain phases
 are filled by another's blocks.  Measured at C96 fp64 (tools/ensemble_probe.py,
 profiles/r2_ensemble), every member bitwise equal to the same member run alone:
-one member 16.3 us/step (3.39e9 cell-updates/s); two members 23.6-23.9 us per
-member step, 4.63-4.69e9 aggregate (1.38x).  Three or more members share the
+one member 16.3 us/step (3.39e9 cell-updates/s); two members 22.5-23.9 us per
+member step, 4.63-4.91e9 aggregate (1.38-1.45x; `python -m stsphere ensemble
+configs/reference_6dev.yaml --members 2`: 4.81-4.83e9 against 3.27e9, 1.48x).  Three or more members share the
 process's 4 hardware queues (GPU_MAX_HW_QUEUES) with the runners' own streams
 and lose (3.2-4.1e9 for three, 2.7e9 for four), so two members per process is
 the useful setting at C96.
