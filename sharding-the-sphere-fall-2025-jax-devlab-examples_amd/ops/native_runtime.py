@@ -195,8 +195,9 @@ class NativeStepper:
         d.use_graph = 1 if self._cxx_graph else 0
         self.graph_periods = max(1, steps_per_graph // period)
         d.graph_periods = self.graph_periods
-        self._graphs = {}          # periods -> torch.cuda.CUDAGraph
-        self._primed = set()       # graph lengths replayed at least once
+        self._graphs = {}          # (periods, copy) -> torch.cuda.CUDAGraph
+        self._primed = set()       # (periods, copy) replayed at least once
+        self._next_copy = {}       # periods -> copy the next replay of that length uses
         self._pool0 = list(e.pool)  # construction order = the op list's buffer pointers
         self.stats = {"graph_steps": 0, "eager_steps": 0, "replays": 0}
         self._warmed = False
@@ -274,17 +275,22 @@ class NativeStepper:
         if self.xgmi is not None:
             self.xgmi.prime()          # re-deliver the remote ghosts of the restored state (collective)
 
-    def _graph(self, periods: int):
+    def _graph(self, periods: int, copy: int = 0):
         """hipGraph of exactly ``periods`` integrator periods (recorded once,
-        cached by length; recorded launches carry the current dt)."""
-        g = self._graphs.get(periods)
+        cached by length; recorded launches carry the current dt).  Two
+        copies per length: a graph exec launched again while its previous
+        launch is still running holds the host until that launch is done, so
+        back-to-back chunks of one length alternate between the copies and
+        the host stays a chunk ahead of the GPU (profiles/r2_ensemble)."""
+        key = (periods, copy)
+        g = self._graphs.get(key)
         if g is None:
             self._warm()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=self.stream):
                 self._check(self.L.stsp_rt_run(self.h, periods * self.period), "capture")   # recorded, not executed
-            self._graphs[periods] = g
-            self._primed.discard(periods)
+            self._graphs[key] = g
+            self._primed.discard(key)
         return g
 
     def plan(self, nsteps: int) -> List[int]:
@@ -308,14 +314,16 @@ class NativeStepper:
             return
         todo = []
         for c in self.plan(nsteps):
-            self._graph(c)
-            if c not in self._primed:
-                todo.append(c)
+            for copy in (0, 1):
+                key = (c, copy)
+                self._graph(c, copy)
+                if key not in self._primed and key not in todo:
+                    todo.append(key)
         if prime and todo:
             saved = self._save()
-            for c in todo:
-                self._graphs[c].replay()
-                self._primed.add(c)
+            for key in todo:
+                self._graphs[key].replay()
+                self._primed.add(key)
             torch.cuda.synchronize(self.e.device)
             self._restore(saved)
 
@@ -327,8 +335,10 @@ class NativeStepper:
         # replay on torch's current stream: measured 17.2 us/step at C96 there
         # against 20-21 us/step when the same graph is launched on a side stream
         for c in self.plan(nsteps):
-            self._graph(c).replay()
-            self._primed.add(c)
+            copy = self._next_copy.get(c, 0)
+            self._graph(c, copy).replay()
+            self._primed.add((c, copy))
+            self._next_copy[c] = 1 - copy
             self.stats["graph_steps"] += c * self.period
             self.stats["replays"] += 1
 
@@ -363,6 +373,7 @@ class NativeStepper:
         self._check(self.L.stsp_rt_set_dt(self.h, dt), "set_dt")
         self._graphs = {}     # recorded launches carry the old dt
         self._primed = set()
+        self._next_copy = {}
 
     def close(self) -> None:
         self._graphs = {}
