@@ -129,8 +129,8 @@ def run_ensemble(config, members: int, amplitude: float, days=None, nsteps=None)
     cells = 6 * c.grid.N ** 2
     return {"members": members, "steps": nsteps, "dt": ens.dt, "wall_s": wall,
             "aggregate_cell_updates_per_s": members * cells * nsteps / max(wall, 1e-12),
-            "native": ens.native, "h_mean": after["mean"], "h_spread_rms_initial": before["spread_rms"],
-            "h_spread_rms_final": after["spread_rms"]}
+            "native": ens.native, "field0_mean": after["mean"], "field0_spread_rms_initial": before["spread_rms"],
+            "field0_spread_rms_final": after["spread_rms"]}
 
 
 if __name__ == "__main__":

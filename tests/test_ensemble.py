@@ -69,6 +69,6 @@ def test_ensemble_cli_from_config_cpu():
                        "sharding-the-sphere-fall-2025-jax-devlab-examples_amd", "configs", "plumbing_cpu.yaml")
     r = run_ensemble(cfg, 2, 1e-3, nsteps=2)
     assert r["members"] == 2 and r["steps"] == 2 and not r["native"]
-    assert r["h_spread_rms_initial"] > 0 and np.isfinite(r["h_spread_rms_final"])
+    assert r["field0_spread_rms_initial"] > 0 and np.isfinite(r["field0_spread_rms_final"])
     r1 = run_ensemble(cfg, 1, 1e-3, nsteps=1)
-    assert r1["h_spread_rms_initial"] == 0.0
+    assert r1["field0_spread_rms_initial"] == 0.0
