@@ -56,7 +56,9 @@ def parse(argv=None):
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--integrator", default="ssprk3")
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
-    ap.add_argument("--runtime", default="auto", choices=["auto", "persistent", "native", "graph", "eager"])
+    ap.add_argument("--runtime", default="auto", choices=["auto", "fused", "native", "graph", "eager"],
+                    help="fused: one launch per SSP-RK3 step (temporal blocking, one rank); native: one launch "
+                         "per RK stage (C++ op list, any rank count); auto: fused where it applies")
     ap.add_argument("--steps-per-graph", type=int, default=0,
                     help="steps recorded per graph (0 = the whole timed run in one graph)")
     ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "rccl"],
@@ -65,6 +67,9 @@ def parse(argv=None):
     ap.add_argument("--partition", default="auto")
     ap.add_argument("--dt", type=float, default=None)
     ap.add_argument("--block", default=None, help="stage block shape BXxBY (default: chosen per grid)")
+    ap.add_argument("--timeout", type=float, default=float(os.environ.get("STSP_BENCH_TIMEOUT", "480")),
+                    help="--gpus N > 1 (self-launched): kill every rank and print a status=timeout JSON line "
+                         "after this many seconds (0 = no deadline)")
     ap.add_argument("--no-verify", action="store_true",
                     help="N > 1: skip the bitwise comparisons with a one-GPU run")
     return ap.parse_args(argv)
@@ -78,18 +83,86 @@ def free_port() -> int:
     return p
 
 
+def _phase(name: str) -> None:
+    """Record this rank's current phase (read by the launching parent when the
+    run overruns its deadline)."""
+    d = os.environ.get("STSP_PHASE_DIR")
+    if d:
+        try:
+            with open(os.path.join(d, f"rank{os.environ.get('RANK', '0')}.phase"), "w") as f:
+                f.write(f"{name} {time.time():.3f}\n")
+        except OSError:
+            pass
+
+
+def _fail_line(a, status: str, **extra) -> str:
+    """The one JSON line of a run that produced no measurement."""
+    out = {"metric": f"cell-updates/sec (whole node) at C{a.N}", "value": None, "unit": "cell-updates/s",
+           "n_gpus": a.gpus, "steps": a.steps, "warmup": a.warmup, "ms_per_step": None,
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": a.dtype,
+           "data": "synthetic", "status": status}
+    out.update(extra)
+    return json.dumps(out)
+
+
 def launch_ranks(a) -> int:
     """--gpus N > 1 without a distributed launch: start N fresh worker
     processes with torch.distributed.run (this parent never touches the GPU,
     and is never replaced by exec) and pass their output through; rank 0 prints
-    the JSON line.  Returns the launcher's exit code."""
+    the JSON line.  Returns the launcher's exit code.
+
+    Deadline: the workers run in their own process group; past ``--timeout``
+    seconds the whole group is killed and this parent prints one JSON line with
+    ``"status": "timeout"`` and the last phase each rank reached (each rank
+    writes its phase to a file in a scratch directory), then exits non-zero."""
+    import shutil
+    import signal
+    import tempfile
+    share = os.environ.get("STSP_SHARE_GPU") == "1"
+    if a.backend == "hip" and not share:
+        import torch   # device_count() does not initialise the GPU
+        have = torch.cuda.device_count()
+        if have < a.gpus:
+            print(_fail_line(a, "error", error=f"--gpus {a.gpus} but only {have} GPU(s) visible "
+                                               "(STSP_SHARE_GPU=1 rehearses several ranks on one GPU)"),
+                  flush=True)
+            return 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__),
            *sys.argv[1:]]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "1")
-    return subprocess.call(cmd, env=env)
+    pdir = tempfile.mkdtemp(prefix="stsp_phase_")
+    env["STSP_PHASE_DIR"] = pdir
+    t0 = time.time()
+    proc = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        return proc.wait(timeout=a.timeout if a.timeout > 0 else None)
+    except subprocess.TimeoutExpired:
+        phases = {}
+        for r in range(a.gpus):
+            try:
+                with open(os.path.join(pdir, f"rank{r}.phase")) as f:
+                    name, ts = f.read().split()
+                phases[str(r)] = {"phase": name, "since_s": round(time.time() - float(ts), 1)}
+            except (OSError, ValueError):
+                phases[str(r)] = {"phase": "not started", "since_s": None}
+        for sig, grace in ((signal.SIGTERM, 10), (signal.SIGKILL, 10)):
+            try:
+                os.killpg(proc.pid, sig)
+            except ProcessLookupError:
+                break
+            try:
+                proc.wait(timeout=grace)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+        print(_fail_line(a, "timeout", timeout_s=a.timeout, elapsed_s=round(time.time() - t0, 1), phases=phases),
+              flush=True)
+        return 124
+    finally:
+        shutil.rmtree(pdir, ignore_errors=True)
 
 
 def single_rank_reference(a, phys_factory, grid, dtype, device, dt, ng, nsteps, runtime, backend):
@@ -101,9 +174,13 @@ def single_rank_reference(a, phys_factory, grid, dtype, device, dt, ng, nsteps, 
     L1 = TileLayout(a.N, a.tiles_per_edge, 1, ng=ng)
     ref = Engine(phys_factory(), L1, 0, grid=grid, dtype=dtype, device=device, backend=backend,
                  integrator=a.integrator, dt=dt)
-    if runtime in ("native", "persistent") and backend == "hip":
+    if runtime in ("native", "fused") and backend == "hip":
         from stsphere.ops.native_runtime import NativeStepper
-        r = NativeStepper(ref, use_graph=True, steps_per_graph=max(nsteps, 1))
+        fk = None
+        if runtime == "fused":
+            from stsphere.ops.fused import FusedKernel
+            fk = FusedKernel(ref)
+        r = NativeStepper(ref, use_graph=True, steps_per_graph=max(nsteps, 1), fused=fk)
         r.run(nsteps)
         r.close()
     else:
@@ -138,6 +215,7 @@ def main():
     if device.type == "cuda":
         torch.cuda.set_device(device)
     if world > 1:
+        _phase("init_process_group")
         if device.type == "cuda" and not share:
             dist.init_process_group("nccl", device_id=device)
         else:
@@ -152,8 +230,14 @@ def main():
     runtime = a.runtime
     if runtime == "auto":
         runtime = "native" if (device.type == "cuda" and backend == "hip") else "eager"
+        if runtime == "native" and world == 1:
+            from stsphere.ops.fused import fused_supported
+            probe = Engine(phys_factory(), layout, rank, grid=grid, dtype=dtype, device="cpu", integrator=a.integrator)
+            if fused_supported(probe) is None:
+                runtime = "fused"
+            del probe
     comm = a.comm if world > 1 else "none"
-    if world > 1 and runtime not in ("native",):
+    if world > 1 and runtime not in ("native", "fused"):
         comm = "torch.distributed"
     elif comm == "auto":
         comm = "xgmi" if world > 1 else "none"
@@ -188,9 +272,11 @@ def main():
         eng = Engine(phys_factory(), layout, rank, grid=grid, dtype=dtype, device=device, transport=transport,
                      backend=backend, integrator=a.integrator, dt=a.dt, block=blk)
         runner, xg = None, None
-        if runtime == "persistent":
-            from stsphere.ops.persistent import PersistentStepper
-            runner = PersistentStepper(eng, timeout_s=2.0, max_steps_per_launch=max(a.steps, a.warmup, 1))
+        if runtime == "fused":
+            # one launch per SSP-RK3 step (temporal blocking, ops/fused.py), hipGraph replay
+            from stsphere.ops.fused import FusedKernel
+            from stsphere.ops.native_runtime import NativeStepper
+            runner = NativeStepper(eng, use_graph=True, steps_per_graph=spg, fused=FusedKernel(eng))
         elif runtime == "native":
             # C++ runtime, hipGraph replay; between GPUs either direct xGMI
             # stores from the stage kernels (graph-captured) or RCCL grouped
@@ -247,31 +333,47 @@ def main():
         return float(d.item())
 
     eng = runner = xg = None
+    fallback_reason = None
+    _phase("build")
     try:
         eng, runner, xg = build(comm)
         ok = True
     except Exception as exc:   # e.g. no IPC between these GPUs
         print(f"[bench] rank {rank}: {comm} setup failed: {exc}", file=sys.stderr, flush=True)
+        fallback_reason = f"rank {rank}: {comm} setup failed: {exc}"
         ok = False
     if comm == "xgmi" and not agree(ok):
         close(runner, xg)
+        fallback_reason = fallback_reason or "xgmi setup failed on another rank"
         comm = "rccl"
+        _phase("build_rccl")
         eng, runner, xg = build(comm)
     elif not ok:
         raise SystemExit(1)
+    _phase("warmup")
+    if os.environ.get("STSP_BENCH_HANG_RANK") == str(rank):   # test hook: a rank that never returns
+        while True:
+            time.sleep(1)
     ok = warm(eng, runner)
+    if not ok:
+        fallback_reason = f"rank {rank}: {comm} exchange timed out in warmup"
     warm_diff = None
     verify = world > 1 and not a.no_verify
     if verify and ok:
+        _phase("verify")
         warm_diff = diff_vs_1gpu(eng, a.warmup)
         ok = warm_diff == 0.0
+        if not ok:
+            fallback_reason = f"{comm}: warmup state differs from one GPU by {warm_diff:.3e}"
         if not ok and rank == 0:
             print(f"[bench] {comm}: warmup state differs from one GPU by {warm_diff:.3e}", file=sys.stderr, flush=True)
     if world > 1 and not agree(ok):
         if comm != "xgmi":
             raise SystemExit(f"[bench] rank {rank}: {comm} exchange failed its check")
         close(runner, xg)
+        fallback_reason = fallback_reason or f"{comm} check failed on another rank"
         comm = "rccl"                    # fall back from a fresh state
+        _phase("build_rccl")
         eng, runner, xg = build(comm)
         if not warm(eng, runner):
             raise SystemExit(f"[bench] rank {rank}: rccl exchange failed")
@@ -281,6 +383,7 @@ def main():
                 raise SystemExit(f"[bench] rank {rank}: rccl state differs from one GPU by {warm_diff:.3e}")
     step = runner.run if runner is not None else eng.step
     stats0 = dict(getattr(runner, "stats", {}))
+    _phase("timed")
     sync()
     t0 = time.perf_counter()
     step(a.steps)
@@ -294,7 +397,8 @@ def main():
         elapsed = float(t.item())
     if hasattr(runner, "check"):
         runner.check()
-    graph_path = runtime == "native" and getattr(runner, "use_graph", False) and not getattr(runner, "_cxx_graph", False)
+    graph_path = runtime in ("native", "fused") and getattr(runner, "use_graph", False) \
+        and not getattr(runner, "_cxx_graph", False)
     if graph_path and (timed.get("eager_steps", 0) != 0 or timed.get("graph_steps", 0) != a.steps):
         raise SystemExit(f"[bench] timed region was not a pure graph replay: {timed}")
     diag = eng.diagnostics()
@@ -303,6 +407,7 @@ def main():
         dist.all_reduce(t)
         diag["mass"] = float(t.item())
     finite = bool(torch.isfinite(eng.tiles_view()).all().item())
+    _phase("final_verify")
     final_diff = diff_vs_1gpu(eng, a.warmup + a.steps) if verify else None
     cells = 6 * a.N * a.N
     cups = cells * a.steps / elapsed
@@ -344,6 +449,8 @@ def main():
             "finite": finite,
             "max_abs_diff_vs_1gpu_warmup": warm_diff,
             "max_abs_diff_vs_1gpu": final_diff,
+            "comm_fallback_reason": fallback_reason,
+            "status": "ok",
             "mass": diag.get("mass"),
         }
         print(json.dumps(out), flush=True)

@@ -438,28 +438,38 @@ class Solver:
             drain()
             p = pos()
             due = {k for k, v in iv.items() if p % v == 0 or p >= end}
+            ok, checked = True, False
             if "watchdog" in due:
                 with ph("watchdog"):
-                    ok = self._watchdog(pending, deferred and "checkpoint" not in due and p < end)
-                if not ok:
-                    saved = [s for s in ckpt.list_checkpoints(self.checkpoint_root())]
-                    if recoveries < 3 and saved:
-                        recoveries += 1
-                        pending.clear()
-                        self._wd_pending = None
-                        # go back further on each repeated failure (recent checkpoints may
-                        # already hold a growing instability)
-                        last = ckpt.step_dir(self.checkpoint_root(), saved[-min(recoveries, len(saved))])
-                        dt_cur = self.dt
-                        self._log(f"watchdog: non-finite state at step {self.step_count}; restarting from {last} "
-                                  f"with dt/2")
-                        self.restore_checkpoint(last)
-                        level += 1
-                        self.set_dt(dt_cur * 0.5)
-                        if abs(self.dt * (1 << level) - dt0) > 1e-9 * dt0:
-                            self.set_dt(dt0 / (1 << level))
-                        continue
-                    raise FloatingPointError(f"non-finite state detected at step {self.step_count}")
+                    sync_check = not (deferred and "checkpoint" not in due and p < end)
+                    ok = self._watchdog(pending, not sync_check)
+                    checked = sync_check
+            if ok and "checkpoint" in due and p % iv["checkpoint"] == 0 and "watchdog" in iv and not checked:
+                # a checkpoint between watchdog intervals: resolve the deferred
+                # check and test the state itself, so no checkpoint ever holds a
+                # state the watchdog would reject
+                with ph("watchdog"):
+                    drain(block=True)
+                    ok = self._watchdog(pending, False)
+            if not ok:
+                saved = [s for s in ckpt.list_checkpoints(self.checkpoint_root())]
+                if recoveries < 3 and saved:
+                    recoveries += 1
+                    pending.clear()
+                    self._wd_pending = None
+                    # go back further on each repeated failure (recent checkpoints may
+                    # already hold a growing instability)
+                    last = ckpt.step_dir(self.checkpoint_root(), saved[-min(recoveries, len(saved))])
+                    dt_cur = self.dt
+                    self._log(f"watchdog: non-finite state at step {self.step_count}; restarting from {last} "
+                              f"with dt/2")
+                    self.restore_checkpoint(last)
+                    level += 1
+                    self.set_dt(dt_cur * 0.5)
+                    if abs(self.dt * (1 << level) - dt0) > 1e-9 * dt0:
+                        self.set_dt(dt0 / (1 << level))
+                    continue
+                raise FloatingPointError(f"non-finite state detected at step {self.step_count}")
             if hist is not None and "history" in due and p % iv["history"] == 0:
                 with ph("history"):
                     self._snapshot_history(hist, p // iv["history"], pending, async_copy=deferred)

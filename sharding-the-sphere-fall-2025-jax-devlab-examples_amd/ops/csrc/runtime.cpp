@@ -12,6 +12,8 @@
 //       STAGE(interior blocks)           overlaps the transfer
 //       COMM_WAIT                        event: comm -> compute stream
 //       STAGE(boundary blocks)           remote ghosts from the receive buffer
+//   per step, fused (one rank, SSP-RK3 PLR shallow water):
+//       FUSED                            the whole step in one launch (fused_step.hip)
 //
 // The list is executed eagerly or captured once into a hipGraph (several steps
 // per graph) and replayed, which removes host launch overhead entirely
@@ -106,6 +108,14 @@ int run_op(Runtime* rt, const StspOp& op) {
       NC_CHECK(ncclGroupEnd());
       return 0;
     }
+    case STSP_OP_FUSED: {
+      const int rc = stsp_fused_launch(op.dtype, static_cast<const FusedDesc*>(op.fused), rt->stream);
+      if (rc != 0) {
+        rt->err = "fused step launch failed: " + std::to_string(rc);
+        return -3;
+      }
+      return 0;
+    }
     case STSP_OP_COMM_WAIT: {
       RT_CHECK(hipEventRecord(rt->ev_join, rt->comm_stream));
       RT_CHECK(hipStreamWaitEvent(rt->stream, rt->ev_join, 0));
@@ -132,8 +142,8 @@ int run_period(Runtime* rt, bool mark) {
       std::fflush(stderr);
     }
     if (mark) {
-      const char* names[] = {"?", "stage", "pack", "comm", "comm_wait"};
-      roctxRangePush(names[op.type >= 1 && op.type <= 4 ? op.type : 0]);
+      const char* names[] = {"?", "stage", "pack", "comm", "comm_wait", "fused_step"};
+      roctxRangePush(names[op.type >= 1 && op.type <= 5 ? op.type : 0]);
     }
     const int rc = run_op(rt, op);
     if (mark) roctxRangePop();
@@ -224,8 +234,10 @@ extern "C" const char* stsp_rt_last_error(void* p) {
 
 extern "C" int stsp_rt_set_dt(void* p, double dt) {
   auto* rt = static_cast<Runtime*>(p);
-  for (StspOp& op : rt->ops)
+  for (StspOp& op : rt->ops) {
     if (op.type == STSP_OP_STAGE) op.stage.dt = dt;
+    if (op.type == STSP_OP_FUSED && op.fused) static_cast<FusedDesc*>(op.fused)->dt = dt;
+  }
   drop_graph(rt);
   return 0;
 }

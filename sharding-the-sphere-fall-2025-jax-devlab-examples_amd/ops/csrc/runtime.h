@@ -6,7 +6,8 @@
 
 extern "C" {
 
-enum StspOpType { STSP_OP_STAGE = 1, STSP_OP_PACK = 2, STSP_OP_COMM_START = 3, STSP_OP_COMM_WAIT = 4 };
+enum StspOpType { STSP_OP_STAGE = 1, STSP_OP_PACK = 2, STSP_OP_COMM_START = 3, STSP_OP_COMM_WAIT = 4,
+                  STSP_OP_FUSED = 5 };
 
 #define STSP_MAX_PEERS 32
 
@@ -29,6 +30,9 @@ typedef struct StspOp {
   void* sendbuf;
   void* recvbuf;
   int slot_elems;  // elements per slot (= F)
+  // FUSED: one whole SSP-RK step (fused_step.hip); the descriptor is owned by
+  // the caller and must outlive the runtime (dt is rewritten by stsp_rt_set_dt)
+  void* fused;
 } StspOp;
 
 typedef struct StspRtDesc {

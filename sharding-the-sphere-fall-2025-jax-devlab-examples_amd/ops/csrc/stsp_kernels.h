@@ -87,6 +87,31 @@ int stsp_copy_index_launch(int dtype, const void* src, const int* sidx, void* ds
 // code[i] = peer << 24 | slot) into every peer's ring slot of stage `epoch`.
 int stsp_xg_prime_launch(int dtype, const void* q, int S, int F, const int* src, const int* code, int nent,
                          void* const* peer_ring, int ring, int epoch, hipStream_t stream);
+// One fused SSP-RK3 step of the shallow-water solver (fused_step.hip, ops/fused.py):
+// temporal blocking over a window of the block plus a ring of 2 NS cells.
+typedef struct FusedDesc {
+  const void* Q;        // [F][S] step input, padded layout
+  void* out;            // [F][S] step output: interior + same-rank ghost pushes
+  const void* cgeo;     // [S][8] per-cell record in the padded layout (1/A, centre, grad b, 0)
+  const int* src;       // [nb][W*W] padded offset of each window cell's source, -1 = not loaded
+  const int* org;       // [nb][4] X0, Y0, tile_local, xo | yo << 12 | region flags << 24
+  const void* len;      // [nb][2 H1 (H1+1)] face lengths (x-faces, then y-faces)
+  const void* nrm;      // [nb][2][5][W+1][3] line normals per region
+  const short* gidx;    // [nb][20 W] ghost entry of (reader region * 4 + side, pos), -1 none
+  const int* gtab;      // [nb][G][2] LDS index of the interpolation pair
+  const void* gw;       // [nb][G] interpolation weights
+  const int* ctab;      // [nb][C][8] corner faces: cu | cv << 8 | side_c << 16, du | dv << 8 | side_d << 16, fslot_c, fslot_d
+  const void* cgf;      // [nb][C][4] normal out of c, length
+  const int* ccnt;      // [nb]
+  const int* push;      // [T][4][mg][n] push map (same-rank ghost slot fed by a strip cell, or -1)
+  int G, C;
+  int nblocks, n, N, S, mg, pw;
+  int B, ns, limiter;
+  double a0[4], a1[4], a2[4];
+  double dt, g, omega2;
+} FusedDesc;
+int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stream);
+int stsp_fused_limits(int* gmax, int* cmax);
 // Direct xGMI halo build constants: protocol (0 counters, 1 tagged granules), ring slots.
 int stsp_xg_protocol(void);
 int stsp_xg_slots(void);

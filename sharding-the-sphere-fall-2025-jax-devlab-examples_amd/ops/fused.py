@@ -1,0 +1,952 @@
+"""Fused time step (temporal blocking): one launch per SSP-RK step.
+
+The launch-per-stage path (``stage_kernel.hip``) pays a dependent kernel
+boundary and a window round trip per RK stage, three per SSP-RK3 step.  The
+reference composes its whole halo exchange into one compiled program for the
+same reason (PY:238-246; PDF s.10 "Why two JITs?").  Here a whole step is one
+launch: every block loads its ``B x B`` cells plus a ring ``R = ns * 2`` wide
+(``ns`` stages, PLR reads 2 cells per stage), then advances the ring through
+the earlier stages by redundant recompute, so no block waits for another
+inside the step.
+
+Ring cells beyond a cube edge belong to another panel.  They are updated in
+their own panel's frame, exactly as that panel's own tile computes them in the
+stage-by-stage scheme (models/base.py::reconstruct):
+
+* a cell next to a panel edge reads its neighbour across the edge as the
+  other panel's edge cells **interpolated onto its own grid line** (the
+  Putman-Lin ghost, ``panel_edge_tables``).  Those values live in per-block
+  *ghost strips* keyed by (reader region, side, along-edge position); the
+  table entry names the two window cells and the weight;
+* at a cube corner the window's diagonal quadrant has no cells.  The faces of
+  the panel-edge cells that point into it are the third cube edge; they are
+  listed as *corner faces* (cell, side, partner cell, partner side) and get
+  the flux computed from both panels' reconstructions, as FV3's direction-split
+  corner fill does.
+
+Everything the kernel needs beyond the state is precomputed here, on the host,
+from the same tables the oracle uses (ghost sources, ``pe_base`` / ``pe_t``,
+the edge normals and lengths), so the fused step reproduces the stage-by-stage
+step to rounding.  ``fused_step_torch`` is the PyTorch rendering of the kernel
+(same tables, same phases) and is checked against ``Engine.step`` on CPU;
+``ops/csrc/fused_step.hip`` is the gfx950 kernel.
+
+Window coordinates: cell ``(u, v)``, ``u`` along x (columns), ``v`` along y
+(rows), ``u, v in [0, W)``, ``W = B + 2 R``; panel coordinates
+``(X0 + u, Y0 + v)`` in the block's panel (outside ``[0, N)`` = another panel).
+Stage ``s`` (1-based) updates the square ``[lo_s, hi_s)`` with
+``lo_s = R - 2 (ns - s)``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..models.base import panel_edge_tables
+from ..parallel.layout import TileLayout, ghost_xy
+from ..parallel.topology import neighbor_cells
+
+REG_P, REG_W, REG_E, REG_S, REG_N = 0, 1, 2, 3, 4
+NREG = 5
+# window sides: 0 = -x, 1 = +x, 2 = -y, 3 = +y
+SIDE_VEC = ((-1, 0), (1, 0), (0, -1), (0, 1))
+NG_PLR = 2
+
+
+def region(X, Y, N):
+    """Region code of extended-panel coordinates: P inside, W/E/S/N across one
+    panel edge, -1 beyond a cube corner (no cell)."""
+    X = np.asarray(X)
+    Y = np.asarray(Y)
+    inx = (X >= 0) & (X < N)
+    iny = (Y >= 0) & (Y < N)
+    r = np.full(np.broadcast(X, Y).shape, -1, dtype=np.int64)
+    r[inx & iny] = REG_P
+    r[(X < 0) & iny] = REG_W
+    r[(X >= N) & iny] = REG_E
+    r[(Y < 0) & inx] = REG_S
+    r[(Y >= N) & inx] = REG_N
+    return r
+
+
+def frame_map(N: int, face: int, reg: int) -> Tuple[int, np.ndarray]:
+    """(panel of region ``reg`` around ``face``, 2x2 integer matrix M) with
+    M @ (du, dv) = the step in that panel's own (i, j) index frame for a step
+    (du, dv) in ``face``'s extended index frame."""
+    h = N // 2
+    if reg == REG_P:
+        p = (h, h)
+    elif reg == REG_W:
+        p = (-2, h)
+    elif reg == REG_E:
+        p = (N, h)
+    elif reg == REG_S:
+        p = (h, -2)
+    else:
+        p = (h, N)
+    X = np.array([p[0], p[0] + 1, p[0]])
+    Y = np.array([p[1], p[1], p[1] + 1])
+    F, I, J = neighbor_cells(N, face, X, Y)
+    assert F[0] == F[1] == F[2] >= 0
+    M = np.array([[I[1] - I[0], I[2] - I[0]], [J[1] - J[0], J[2] - J[0]]], dtype=np.int64)
+    return int(F[0]), M
+
+
+def _side_of(di: int, dj: int) -> int:
+    """Tile side index (0 W, 1 E, 2 S, 3 N) of an index-frame unit step."""
+    return {(-1, 0): 0, (1, 0): 1, (0, -1): 2, (0, 1): 3}[(int(di), int(dj))]
+
+
+@dataclass
+class FusedDims:
+    B: int
+    ns: int
+    R: int
+    W: int
+    L1: int      # first window row/column updated by stage 1
+    H1: int      # cells per row updated by stage 1
+
+    @classmethod
+    def make(cls, B: int, ns: int) -> "FusedDims":
+        R = NG_PLR * ns
+        W = B + 2 * R
+        L1 = R - NG_PLR * (ns - 1)
+        H1 = B + 2 * NG_PLR * (ns - 1)
+        return cls(B, ns, R, W, L1, H1)
+
+    def stage_range(self, s: int) -> Tuple[int, int]:
+        """[lo, hi) of window rows/columns that stage s (1-based) updates."""
+        lo = self.R - NG_PLR * (self.ns - s)
+        return lo, self.W - lo
+
+    @property
+    def nfx(self) -> int:        # x-faces of the stage-1 set: rows H1, lines H1+1
+        return self.H1 * (self.H1 + 1)
+
+
+class FusedPlan:
+    """Per-block tables of the fused step for one rank (numpy; see module doc).
+
+    Arrays (nb = number of blocks, bid = (tile_local * nby + yb) * nbx + xb):
+      org   [nb, 4]  int32  X0, Y0 (panel coords of the window origin), tile_local, 0
+      src   [nb, W*W] int32 padded state offset of each window cell's source
+                            cell; -1 beyond a cube corner; <= -2: receive slot -2-src
+      reg   [nb, W*W] int8  region code (P W E S N, -1 none)
+      nrm   [nb, 2, 5, W+1, 3] float64  unit normal of grid line k (between
+                            columns / rows k-1 and k) of each region, oriented +u / +v
+      lx    [nb, H1, H1+1]  float64  length of x-face (row L1+r, line L1+c)
+      ly    [nb, H1+1, H1]  float64  length of y-face (line L1+r, column L1+c)
+      gtab  [nb, G, 4] int32 (strip = reg*4+side, pos, slot0, slot1), gt [nb, G] weights,
+            gcnt [nb]
+      ctab  [nb, C, 6] int32 (slot_c, side_c, slot_d, side_d, fslot_c, fslot_d),
+            cgeo [nb, C, 4] (normal out of c, length), ccnt [nb]
+    Face slots (fslot) index the stage-1 flux arrays: x-face (r, c) -> r (H1+1) + c,
+    y-face (r, c) -> H1 (H1+1) + r H1 + c; -1 = outside them.
+    """
+
+    def __init__(self, layout: TileLayout, rank: int, grid, B: int = 16, ns: int = 3,
+                 source=None):
+        self.layout = layout
+        self.rank = rank
+        self.grid = grid
+        N, n, t = layout.N, layout.n, layout.t
+        if n % B:
+            raise ValueError(f"fused step: tile size {n} is not a multiple of the block size {B}")
+        d = FusedDims.make(B, ns)
+        if d.R >= N:
+            raise ValueError(f"fused step: ring width {d.R} needs C{N} > {d.R}")
+        self.d = d
+        self.N, self.n, self.B, self.ns = N, n, B, ns
+        plan = layout.plan(rank)
+        self.tiles = list(plan.tiles)
+        self.T = len(self.tiles)
+        self.nbx = self.nby = n // B
+        self.nb = self.T * self.nbx * self.nby
+        # where a global cell lives: padded local offset (>= 0) or receive code
+        self._source = source or (lambda g: layout.local_flat(g))
+        self._lx = grid.x_edge_lengths()
+        self._ly = grid.y_edge_lengths()
+        self._mx = grid.x_edge_normals()
+        self._my = grid.y_edge_normals()
+        self._pe_cache: Dict[int, Tuple[np.ndarray, np.ndarray]] = {}
+        self._build()
+
+    # ---- helpers -----------------------------------------------------------
+    def _pe(self, tid: int):
+        if tid not in self._pe_cache:
+            b, t = panel_edge_tables(self.N, self.layout, [tid], 1)
+            self._pe_cache[tid] = (b[0, :, 0], t[0, :, 0])
+        return self._pe_cache[tid]
+
+    def _ghost_source(self, tid: int, side: int, pos: int) -> int:
+        """Global flat id of layer-0 ghost ``pos`` of tile ``tid``'s ``side``."""
+        L = self.layout
+        f, I0, J0 = L.tile_origin(tid)
+        x, y = ghost_xy(side, 0, np.array([pos]), self.n)
+        F, I, J = neighbor_cells(self.N, f, I0 + x, J0 + y)
+        assert F[0] >= 0
+        return int(L.global_flat(F[0], I[0], J[0]))
+
+    def _face_normal(self, face, i, j, di, dj, plus: bool) -> np.ndarray:
+        """Unit normal pointing along index step (di, dj) of the face on the
+        (di, dj) side of cell (i, j) if plus, else on the -(di, dj) side."""
+        if plus:
+            if di == 1:
+                return self._mx[face, i + 1]
+            if di == -1:
+                return -self._mx[face, i]
+            if dj == 1:
+                return self._my[face, j + 1]
+            return -self._my[face, j]
+        # face on the -(di, dj) side, normal still along +(di, dj)
+        if di == 1:
+            return self._mx[face, i]
+        if di == -1:
+            return -self._mx[face, i + 1]
+        if dj == 1:
+            return self._my[face, j]
+        return -self._my[face, j + 1]
+
+    def _face_length(self, face, i, j, di, dj, plus: bool) -> float:
+        if not plus:
+            di, dj = -di, -dj
+        if di == 1:
+            return float(self._lx[face, j, i + 1])
+        if di == -1:
+            return float(self._lx[face, j, i])
+        if dj == 1:
+            return float(self._ly[face, j + 1, i])
+        return float(self._ly[face, j, i])
+
+    def fslot(self, u: int, v: int, side: int) -> int:
+        """Stage-1 flux-array slot of the face on ``side`` of window cell (u, v)."""
+        d = self.d
+        L1, H1 = d.L1, d.H1
+        if side in (0, 1):
+            k = u + (side == 1)
+            r, c = v - L1, k - L1
+            if 0 <= r < H1 and 0 <= c <= H1:
+                return r * (H1 + 1) + c
+            return -1
+        k = v + (side == 3)
+        r, c = k - L1, u - L1
+        if 0 <= r <= H1 and 0 <= c < H1:
+            return H1 * (H1 + 1) + r * H1 + c
+        return -1
+
+    # ---- build ---------------------------------------------------------------
+    def _build(self):
+        L, d, N, n, B = self.layout, self.d, self.N, self.n, self.B
+        W, R, L1, H1 = d.W, d.R, d.L1, d.H1
+        nb = self.nb
+        self.org = np.zeros((nb, 4), dtype=np.int32)
+        self.src = np.full((nb, W * W), -1, dtype=np.int32)
+        self.reg = np.full((nb, W * W), -1, dtype=np.int8)
+        self.nrm = np.zeros((nb, 2, NREG, W + 1, 3))
+        self.lx = np.zeros((nb, H1, H1 + 1))
+        self.ly = np.zeros((nb, H1 + 1, H1))
+        gl: List[List[Tuple[int, int, int, int, float]]] = []
+        cl: List[List[Tuple[Tuple[int, ...], Tuple[float, ...]]]] = []
+        uu, vv = np.meshgrid(np.arange(W), np.arange(W))          # [v, u]
+        self._need: List[List[set]] = []
+        maps: Dict[Tuple[int, int], Tuple[int, np.ndarray]] = {}
+        for li, tid in enumerate(self.tiles):
+            face, I0, J0 = L.tile_origin(tid)
+            for r_ in (REG_P, REG_W, REG_E, REG_S, REG_N):
+                if (face, r_) not in maps:
+                    maps[(face, r_)] = frame_map(N, face, r_)
+            for yb in range(self.nby):
+                for xb in range(self.nbx):
+                    bid = (li * self.nby + yb) * self.nbx + xb
+                    X0, Y0 = I0 + xb * B - R, J0 + yb * B - R
+                    self.org[bid] = (X0, Y0, li, 0)
+                    X, Y = X0 + uu, Y0 + vv
+                    rg = region(X, Y, N)
+                    F, I, J = neighbor_cells(N, face, X.reshape(-1), Y.reshape(-1))
+                    F, I, J = F.reshape(W, W), I.reshape(W, W), J.reshape(W, W)
+                    valid = rg >= 0
+                    assert ((F >= 0) == valid).all()
+                    g = np.where(valid, L.global_flat(F, I, J), -1)
+                    self.reg[bid] = rg.reshape(-1)
+                    srcv = np.full(W * W, -1, dtype=np.int64)
+                    gv = g.reshape(-1)
+                    m = gv >= 0
+                    srcv[m] = self._source(gv[m])
+                    assert (srcv[m] != -1).all()
+                    self.src[bid] = srcv
+                    gslot = {int(x): k for k, x in enumerate(gv) if x >= 0}
+                    self._block_geometry(bid, face, rg, F, I, J, maps)
+                    gx, cx = self._block_stencils(bid, face, rg, F, I, J, g, gslot, maps, X0, Y0)
+                    gl.append(gx)
+                    cl.append(cx)
+        G = max(1, max(len(x) for x in gl))
+        C = max(1, max(len(x) for x in cl))
+        self.gtab = np.zeros((nb, G, 4), dtype=np.int32)
+        self.gt = np.zeros((nb, G))
+        self.gcnt = np.zeros(nb, dtype=np.int32)
+        self.ctab = np.full((nb, C, 6), -1, dtype=np.int32)
+        self.cgeo = np.zeros((nb, C, 4))
+        self.ccnt = np.zeros(nb, dtype=np.int32)
+        for b in range(nb):
+            self.gcnt[b] = len(gl[b])
+            for k, (strip, pos, s0, s1, w) in enumerate(gl[b]):
+                self.gtab[b, k] = (strip, pos, s0, s1)
+                self.gt[b, k] = w
+            self.ccnt[b] = len(cl[b])
+            for k, (ints, flts) in enumerate(cl[b]):
+                self.ctab[b, k] = ints
+                self.cgeo[b, k] = flts
+        # cells each stage must update (stage 0: the cells the window load must
+        # provide), per block
+        self.need = np.zeros((nb, d.ns + 1, W * W), dtype=bool)
+        for b in range(nb):
+            for s_, cells in enumerate(self._need[b]):
+                self.need[b, s_, sorted(cells)] = True
+        del self._need
+        # strip lookup per block: [nb, 20 strips, W] -> ghost entry index or -1
+        self.gidx = np.full((nb, NREG * 4, W), -1, dtype=np.int32)
+        for b in range(nb):
+            for k in range(self.gcnt[b]):
+                s, p = self.gtab[b, k, 0], self.gtab[b, k, 1]
+                self.gidx[b, s, p] = k
+
+    def _cell_frame(self, face, rg, F, I, J, u, v, maps):
+        """(panel, i, j, M) of window cell (u, v)."""
+        pf, M = maps[(face, int(rg[v, u]))]
+        assert pf == F[v, u]
+        return int(F[v, u]), int(I[v, u]), int(J[v, u]), M
+
+    def _block_geometry(self, bid, face, rg, F, I, J, maps):
+        """Line normals and stage-1 face lengths of one block (vectorised).
+
+        Per cell and axis: the normal and length of its face on the +axis side
+        (``plus``) and on the -axis side (``minus``), both oriented +axis in the
+        window, taken in the cell's own panel frame.  A face is described by its
+        lower cell if that exists, else by its upper cell."""
+        d = self.d
+        W, L1, H1 = d.W, d.L1, d.H1
+        valid = rg >= 0
+        Np = np.zeros((2, W, W, 3))
+        Nm = np.zeros((2, W, W, 3))
+        Lp = np.zeros((2, W, W))
+        Lm = np.zeros((2, W, W))
+        N = self.N
+        for r_ in range(NREG):
+            m = rg == r_
+            if not m.any():
+                continue
+            _, M = maps[(face, r_)]
+            f, i, j = F[m], I[m], J[m]
+            for axis in (0, 1):
+                di, dj = M @ (np.array([1, 0]) if axis == 0 else np.array([0, 1]))
+                if di == 1:
+                    Np[axis][m] = self._mx[f, i + 1]
+                    Nm[axis][m] = self._mx[f, i]
+                    Lp[axis][m] = self._lx[f, j, i + 1]
+                    Lm[axis][m] = self._lx[f, j, i]
+                elif di == -1:
+                    Np[axis][m] = -self._mx[f, i]
+                    Nm[axis][m] = -self._mx[f, i + 1]
+                    Lp[axis][m] = self._lx[f, j, i]
+                    Lm[axis][m] = self._lx[f, j, i + 1]
+                elif dj == 1:
+                    Np[axis][m] = self._my[f, j + 1]
+                    Nm[axis][m] = self._my[f, j]
+                    Lp[axis][m] = self._ly[f, j + 1, i]
+                    Lm[axis][m] = self._ly[f, j, i]
+                else:
+                    Np[axis][m] = -self._my[f, j]
+                    Nm[axis][m] = -self._my[f, j + 1]
+                    Lp[axis][m] = self._ly[f, j, i]
+                    Lm[axis][m] = self._ly[f, j + 1, i]
+        # line normals: line k between cells k-1 and k (k = 0 .. W)
+        for axis in (0, 1):
+            # lower cell (k-1) and upper cell (k) along the axis, for k = 0..W
+            pad_r = np.full((W, 1), -1)
+            if axis == 0:
+                ra = np.concatenate([pad_r, rg], 1)          # [w, k]: region of (k-1, w)
+                rb = np.concatenate([rg, pad_r], 1)          # region of (k, w)
+                na = np.concatenate([np.zeros((W, 1, 3)), Np[0]], 1)
+                nbm = np.concatenate([Nm[0], np.zeros((W, 1, 3))], 1)
+            else:
+                ra = np.concatenate([pad_r.T, rg], 0).T      # [w=u, k]
+                rb = np.concatenate([rg, pad_r.T], 0).T
+                na = np.concatenate([np.zeros((1, W, 3)), Np[1]], 0).transpose(1, 0, 2)
+                nbm = np.concatenate([Nm[1], np.zeros((1, W, 3))], 0).transpose(1, 0, 2)
+            rf = np.where(ra >= 0, ra, rb)
+            val = np.where((ra >= 0)[..., None], na, nbm)
+            ww, kk = np.nonzero(rf >= 0)
+            self.nrm[bid, axis, rf[ww, kk], kk] = val[ww, kk]
+        # stage-1 face lengths
+        r = np.arange(H1)[:, None]
+        c = np.arange(H1 + 1)[None, :]
+        va, ua, ub = L1 + r, L1 + c - 1, L1 + c
+        ok_a = valid[va, ua]
+        self.lx[bid] = np.where(ok_a, Lp[0][va, ua], Lm[0][va, ub])
+        # y-faces [line L1 + c', column L1 + r'] stored [c', r']
+        ua2, vb2 = L1 + r, L1 + c                             # column, upper row
+        ok_a = valid[vb2 - 1, ua2]
+        ly = np.where(ok_a, Lp[1][vb2 - 1, ua2], Lm[1][vb2, ua2])   # [r' col, c' line]
+        self.ly[bid] = ly.T
+        self.lx[bid][~(valid[va, ua] | valid[va, ub])] = 0.0
+
+    def _across(self, face, rg, F, I, J, u, v, side, maps):
+        """Global id of the real cell across ``side`` of window cell (u, v) in
+        the cell's own frame, the cell's owning tile, tile side and strip pos."""
+        L = self.layout
+        f, i, j, M = self._cell_frame(face, rg, F, I, J, u, v, maps)
+        di, dj = M @ np.array(SIDE_VEC[side])
+        F2, I2, J2 = neighbor_cells(self.N, f, np.array([i + di]), np.array([j + dj]))
+        assert F2[0] >= 0
+        gid = int(L.global_flat(F2[0], I2[0], J2[0]))
+        tid, ti, tj = L.locate(np.array([L.global_flat(f, i, j)]))
+        return gid, int(tid[0]), _side_of(di, dj), (int(tj[0]) if abs(di) == 1 else int(ti[0]))
+
+    def _block_stencils(self, bid, face, rg, F, I, J, g, gslot, maps, X0, Y0):
+        """Dependency closure of the block's step, ghost-strip entries and
+        cube-corner faces.
+
+        Working back from the block's cells (stage ns), the cells stage s - 1
+        must provide are those the stage-s update of every needed cell reads:
+        its partners across its four faces and the reconstruction stencils of
+        both sides of each face, in each cell's own frame, where a stencil that
+        crosses a panel edge reads the two cells of the interpolation pair.
+        Only what is needed is tabulated, and everything needed must lie in the
+        window (asserted)."""
+        d = self.d
+        W, N = d.W, self.N
+        memo_desc: Dict[Tuple[int, int], tuple] = {}
+        memo_part: Dict[Tuple[int, int], Optional[Tuple[int, int]]] = {}
+
+        def uv(slot):
+            return slot % W, slot // W
+
+        def rg_at(u, v):
+            if 0 <= u < W and 0 <= v < W:
+                return int(rg[v, u])
+            return int(region(X0 + u, Y0 + v, N))
+
+        def desc(c, side):
+            """Neighbour of cell c across `side` in c's own frame:
+            ('slot', s) | ('interp', s0, s1, t, strip, pos); s / s0 / s1 None
+            when outside the window."""
+            key = (c, side)
+            if key in memo_desc:
+                return memo_desc[key]
+            u, v = uv(c)
+            du, dv = SIDE_VEC[side]
+            u2, v2 = u + du, v + dv
+            r_, r2 = int(rg[v, u]), rg_at(u2, v2)
+            inside = 0 <= u2 < W and 0 <= v2 < W
+            if r2 == r_:
+                out = ("slot", v2 * W + u2 if inside else None)
+            else:
+                gid, tid, tside, pos = self._across(face, rg, F, I, J, u, v, side, maps)
+                if inside and r2 >= 0:
+                    assert gslot.get(gid) == v2 * W + u2, "index-space ghost is not the window neighbour"
+                assert self._ghost_source(tid, tside, pos) == gid
+                base, frac = self._pe(tid)
+                b0 = int(base[tside, pos])
+                s0 = gslot.get(self._ghost_source(tid, tside, b0))
+                s1 = gslot.get(self._ghost_source(tid, tside, b0 + 1))
+                out = ("interp", s0, s1, float(frac[tside, pos]), r_ * 4 + side, v if side < 2 else u)
+            memo_desc[key] = out
+            return out
+
+        def partner(c, side):
+            """(slot, side) of the cell on the other side of c's face `side`."""
+            key = (c, side)
+            if key in memo_part:
+                return memo_part[key]
+            u, v = uv(c)
+            du, dv = SIDE_VEC[side]
+            u2, v2 = u + du, v + dv
+            r2 = rg_at(u2, v2)
+            out = None
+            if r2 >= 0:
+                if 0 <= u2 < W and 0 <= v2 < W:
+                    out = (v2 * W + u2, side ^ 1)
+            else:   # beyond a cube corner: the real neighbour in c's frame
+                gid, _, _, _ = self._across(face, rg, F, I, J, u, v, side, maps)
+                sd = gslot.get(gid)
+                if sd is not None:
+                    ud, vd = uv(sd)
+                    gc = int(g[v, u])
+                    for s2 in range(4):
+                        if rg_at(ud + SIDE_VEC[s2][0], vd + SIDE_VEC[s2][1]) >= 0:
+                            continue
+                        g2, _, _, _ = self._across(face, rg, F, I, J, ud, vd, s2, maps)
+                        if g2 == gc:
+                            out = (sd, s2)
+                            break
+                    assert out is not None
+            memo_part[key] = out
+            return out
+
+        ghosts = {}
+        corners = {}
+
+        def stencil(x, axis, acc):
+            for s_ in (2 * axis, 2 * axis + 1):
+                dsc = desc(x, s_)
+                if dsc[0] == "slot":
+                    assert dsc[1] is not None, "stencil outside the window"
+                    acc.add(dsc[1])
+                else:
+                    _, s0, s1, t_, strip, pos = dsc
+                    assert s0 is not None and s1 is not None, "panel-edge interpolation pair outside the window"
+                    acc.add(s0)
+                    acc.add(s1)
+                    ghosts[(strip, pos)] = (s0, s1, t_)
+
+        ns = d.ns
+        R, B = d.R, d.B
+        # a cell whose cross of radius 2 lies in the window and in its own
+        # region depends on exactly that cross (no panel edge within reach)
+        reg_ok = np.zeros((W, W), dtype=bool)
+        inner = rg[2:W - 2, 2:W - 2]
+        same = inner >= 0
+        for k in (-2, -1, 1, 2):
+            same &= rg[2:W - 2, 2 + k:W - 2 + k] == inner
+            same &= rg[2 + k:W - 2 + k, 2:W - 2] == inner
+        reg_ok[2:W - 2, 2:W - 2] = same
+        need = [set() for _ in range(ns + 1)]
+        need[ns] = {v * W + u for v in range(R, R + B) for u in range(R, R + B)}
+        for s in range(ns, 0, -1):
+            lo, hi = d.stage_range(s)
+            nm = np.zeros(W * W, dtype=bool)
+            nm[list(need[s])] = True
+            nm = nm.reshape(W, W)
+            rmask = nm & reg_ok
+            dil = rmask.copy()
+            for k in (-2, -1, 1, 2):
+                dil[:, max(k, 0):W + min(k, 0)] |= rmask[:, max(-k, 0):W + min(-k, 0)]
+                dil[max(k, 0):W + min(k, 0), :] |= rmask[max(-k, 0):W + min(-k, 0), :]
+            acc = set(np.flatnonzero(dil).tolist())
+            for c in np.flatnonzero(nm & ~reg_ok).tolist():
+                u, v = uv(c)
+                assert lo <= u < hi and lo <= v < hi and rg[v, u] >= 0
+                acc.add(c)
+                for side in range(4):
+                    p = partner(c, side)
+                    assert p is not None, "face partner outside the window"
+                    acc.add(p[0])
+                    stencil(c, side // 2, acc)
+                    stencil(p[0], p[1] // 2, acc)
+                    du, dv = SIDE_VEC[side]
+                    if rg_at(u + du, v + dv) < 0:
+                        key = frozenset([(c, side), p])
+                        if key not in corners:
+                            corners[key] = ((c, side), p)
+            need[s - 1] = acc
+        for s in range(ns, 0, -1):
+            lo, hi = d.stage_range(s)
+            for c in need[s]:
+                u, v = uv(c)
+                assert lo <= u < hi and lo <= v < hi and rg[v, u] >= 0
+        for c in need[0]:
+            u, v = uv(c)
+            assert rg[v, u] >= 0
+        self._need.append(need)
+        gout = [(strip, pos, s0, s1, t_) for (strip, pos), (s0, s1, t_) in sorted(ghosts.items())]
+        cout = []
+        for (c, side_c), (sd, side_d) in corners.values():
+            uc, vc = uv(c)
+            ud, vd = uv(sd)
+            f, i, j, M = self._cell_frame(face, rg, F, I, J, uc, vc, maps)
+            di, dj = M @ np.array(SIDE_VEC[side_c])
+            m = self._face_normal(f, i, j, di, dj, True)          # out of c
+            ln = self._face_length(f, i, j, di, dj, True)
+            cout.append(((c, side_c, sd, side_d, self.fslot(uc, vc, side_c), self.fslot(ud, vd, side_d)),
+                         (float(m[0]), float(m[1]), float(m[2]), ln)))
+        return gout, cout
+
+
+# ---------------------------------------------------------------------------
+# PyTorch rendering of the fused kernel (same tables, same phases)
+# ---------------------------------------------------------------------------
+
+def _half_slope(dl, dr, lim):
+    if lim == 0:
+        return 0.25 * (dl + dr)
+    same = dl * dr > 0
+    if lim == 1:
+        s = torch.sign(dl) * torch.minimum(dl.abs(), dr.abs())
+    elif lim == 2:
+        c = 0.5 * (dl + dr)
+        s = torch.sign(c) * torch.minimum(torch.minimum(2 * dl.abs(), 2 * dr.abs()), c.abs())
+    elif lim == 3:
+        s = 2 * dl * dr / torch.where(same, dl + dr, torch.ones_like(dl))
+    else:
+        raise ValueError(f"fused step: limiter {lim} is not a PLR limiter")
+    return 0.5 * torch.where(same, s, torch.zeros_like(s))
+
+
+def _swe_flux(wl, wr, cl, cr, m, L, g):
+    """Rusanov flux (models/swe.py::_flux), fields on dim 0, m [3, ...]."""
+    hL, hR = wl[0], wr[0]
+    vnL = (wl[1:] * m).sum(0)
+    vnR = (wr[1:] * m).sum(0)
+    sL = (cl[1:4] * m).sum(0).abs() + cl[4]
+    sR = (cr[1:4] * m).sum(0).abs() + cr[4]
+    c = torch.maximum(sL, sR)
+    Fh = 0.5 * (hL * vnL + hR * vnR) - 0.5 * c * (hR - hL)
+    Fm = 0.5 * (hL * wl[1:] * vnL + hR * wr[1:] * vnR + 0.5 * g * (hL * hL + hR * hR) * m) \
+        - 0.5 * c * (hR * wr[1:] - hL * wl[1:])
+    return torch.cat([Fh[None], Fm], 0) * L
+
+
+class FusedTorch:
+    """The fused step in PyTorch, on a SWE ``Engine`` (CPU or GPU): validates the
+    host tables against the stage-by-stage oracle and documents the kernel."""
+
+    def __init__(self, engine, plan: FusedPlan, coefs=None):
+        e = engine
+        self.e = e
+        self.p = plan
+        dev, dt = e.device, e.dtype
+        P = plan
+        d = P.d
+        W = d.W
+        nb = P.nb
+        self.d = d
+        t = lambda a, ty=dt: torch.as_tensor(np.ascontiguousarray(a), dtype=ty, device=dev)
+        self.src = t(P.src, torch.long)
+        self.reg = t(P.reg.astype(np.int64), torch.long).view(nb, W, W)
+        self.nrm = t(P.nrm)                                   # [nb,2,5,W+1,3]
+        self.lx, self.ly = t(P.lx), t(P.ly)
+        # cell records gathered through the padded layout
+        tens = e.tens
+        T, n, ng = e.plan.T, e.plan.n, e.plan.ng
+        Pw = n + 2 * ng
+        cg = torch.zeros((T, Pw, Pw, 8), dtype=dt, device=dev)
+        cg[:, ng:ng + n, ng:ng + n] = tens["cgeo"]
+        self.cgeo_pad = cg.view(-1, 8)
+        self.g = float(e.physics.g)
+        self.omega2 = 2.0 * float(e.physics.omega)
+        self.lim = int(e.physics.limiter)
+        ints = e.integ
+        self.coefs = coefs or [(s.a0, s.a1, s.a2) for s in ints.stages]
+        assert len(self.coefs) == d.ns
+        # substitution index per (cell, side): ghost entry or -1
+        gidx = torch.as_tensor(P.gidx, dtype=torch.long, device=dev)      # [nb,20,W]
+        reg = self.reg
+        sub = torch.full((nb, 4, W, W), -1, dtype=torch.long, device=dev)
+        vv, uu = torch.meshgrid(torch.arange(W, device=dev), torch.arange(W, device=dev), indexing="ij")
+        for side in range(4):
+            du, dv = SIDE_VEC[side]
+            u2, v2 = uu + du, vv + dv
+            inside = (u2 >= 0) & (u2 < W) & (v2 >= 0) & (v2 < W)
+            r2 = torch.full_like(reg, -2)
+            r2[:, inside] = reg[:, v2[inside], u2[inside]]
+            diff = (reg >= 0) & (r2 != reg) & (r2 != -2)
+            pos = vv if side < 2 else uu
+            strip = reg.clamp(min=0) * 4 + side
+            k = gidx[torch.arange(nb, device=dev)[:, None, None], strip, pos[None].expand(nb, W, W)]
+            sub[:, side] = torch.where(diff, k, torch.full_like(k, -1))
+        self.sub = sub
+        self.gt_ = torch.as_tensor(P.gtab, dtype=torch.long, device=dev)
+        self.gw = t(P.gt)
+        self.ctab = torch.as_tensor(P.ctab, dtype=torch.long, device=dev)
+        self.cgf = t(P.cgeo)
+        self.need = torch.as_tensor(P.need, device=dev).view(nb, d.ns + 1, W, W)
+
+    def _prims(self, q):
+        h = q[0]
+        safe = torch.where(h != 0, h, torch.ones_like(h))
+        w = torch.stack([h, q[1] / safe, q[2] / safe, q[3] / safe])
+        c = torch.sqrt(self.g * torch.clamp(h, min=0.0))
+        return w, c
+
+    def step(self):
+        e, P, d = self.e, self.p, self.d
+        W, L1, H1, nb = d.W, d.L1, d.H1, P.nb
+        F = 4
+        Q0 = e.pool[0]
+        srcc = self.src.clamp(min=0)
+        valid = self.need[:, 0]
+        q = Q0[:, srcc].view(F, nb, W, W) * valid
+        X = q.clone()
+        geo = self.cgeo_pad[srcc].view(nb, W, W, 8) * valid[..., None]
+        invA = geo[..., 0]
+        r = geo[..., 1:4].permute(3, 0, 1, 2)
+        gb = geo[..., 4:7].permute(3, 0, 1, 2)
+        bidx = torch.arange(nb, device=q.device)
+        for s in range(1, d.ns + 1):
+            a0, a1, a2 = self.coefs[s - 1]
+            w, c = self._prims(q)
+            wc = torch.cat([w, c[None]], 0)                        # [5,nb,W,W]
+            # ghost strip values of this stage
+            wf = w.reshape(F, nb, W * W)
+            s0 = self.gt_[:, :, 2]
+            s1 = self.gt_[:, :, 3]
+            x0 = torch.gather(wf, 2, s0[None].expand(F, -1, -1))
+            x1 = torch.gather(wf, 2, s1[None].expand(F, -1, -1))
+            G = x0 + self.gw[None] * (x1 - x0)                      # [F,nb,Gmax]
+
+            def nbr(side):
+                du, dv = SIDE_VEC[side]
+                sh = torch.roll(w, shifts=(-dv, -du), dims=(2, 3))
+                k = self.sub[:, side]
+                gv = torch.gather(G, 2, k.clamp(min=0).reshape(1, nb, -1).expand(F, -1, -1)).view(F, nb, W, W)
+                return torch.where(k[None] >= 0, gv, sh)
+
+            wm_x, wp_x, wm_y, wp_y = nbr(0), nbr(1), nbr(2), nbr(3)
+            hx = _half_slope(w - wm_x, wp_x - w, self.lim)
+            hy = _half_slope(w - wm_y, wp_y - w, self.lim)
+            # stage-1 face set (compact): x-face (r, c) between (L1+c-1, L1+r) and (L1+c, L1+r)
+            rows = slice(L1, L1 + H1)
+            a_x = slice(L1 - 1, L1 + H1)
+            b_x = slice(L1, L1 + H1 + 1)
+            wl = (w + hx)[:, :, rows, a_x]
+            wr = (w - hx)[:, :, rows, b_x]
+            cl = wc[:, :, rows, a_x]
+            cr = wc[:, :, rows, b_x]
+            ra = self.reg[:, rows, a_x]
+            rb = self.reg[:, rows, b_x]
+            rf = torch.where(ra >= 0, ra, rb).clamp(min=0)
+            lines = torch.arange(L1, L1 + H1 + 1, device=q.device)
+            mx = self.nrm[bidx[:, None, None], 0, rf, lines[None, None, :].expand(nb, H1, H1 + 1)]   # [nb,H1,H1+1,3]
+            FX = _swe_flux(wl, wr, cl, cr, mx.permute(3, 0, 1, 2), self.lx, self.g)
+            FX = torch.where(((ra >= 0) & (rb >= 0))[None], FX, torch.zeros_like(FX))
+            wl = (w + hy)[:, :, a_x, rows]
+            wr = (w - hy)[:, :, b_x, rows]
+            cl = wc[:, :, a_x, rows]
+            cr = wc[:, :, b_x, rows]
+            ra = self.reg[:, a_x, rows]
+            rb = self.reg[:, b_x, rows]
+            rf = torch.where(ra >= 0, ra, rb).clamp(min=0)
+            my = self.nrm[bidx[:, None, None], 1, rf, lines[None, :, None].expand(nb, H1 + 1, H1)]
+            FY = _swe_flux(wl, wr, cl, cr, my.permute(3, 0, 1, 2), self.ly, self.g)
+            FY = torch.where(((ra >= 0) & (rb >= 0))[None], FY, torch.zeros_like(FY))
+            # cube-corner faces
+            flat = torch.cat([FX.reshape(F, nb, -1), FY.reshape(F, nb, -1)], 2)
+            for b in range(nb):
+                for k in range(int(P.ccnt[b])):
+                    sc, side_c, sd, side_d, fc, fd = [int(x) for x in self.ctab[b, k]]
+                    uc, vc, ud, vd = sc % W, sc // W, sd % W, sd // W
+                    ax_c, ax_d = side_c // 2, side_d // 2
+                    hc = (hx if ax_c == 0 else hy)[:, b, vc, uc]
+                    hd = (hx if ax_d == 0 else hy)[:, b, vd, ud]
+                    fl = w[:, b, vc, uc] + (hc if side_c % 2 else -hc)
+                    fr = w[:, b, vd, ud] + (hd if side_d % 2 else -hd)
+                    m = self.cgf[b, k, :3][:, None]
+                    Fk = _swe_flux(fl[:, None], fr[:, None], wc[:, b, vc, uc][:, None], wc[:, b, vd, ud][:, None],
+                                   m, self.cgf[b, k, 3], self.g)[:, 0]
+                    if fc >= 0:
+                        flat[:, b, fc] = Fk if side_c % 2 else -Fk
+                    if fd >= 0:
+                        flat[:, b, fd] = -Fk if side_d % 2 else Fk
+            nfx = H1 * (H1 + 1)
+            FX = flat[:, :, :nfx].view(F, nb, H1, H1 + 1)
+            FY = flat[:, :, nfx:].view(F, nb, H1 + 1, H1)
+            # cell update on the stage range
+            lo, hi = d.stage_range(s)
+            cs = slice(lo - L1, hi - L1)
+            ce = slice(lo - L1 + 1, hi - L1 + 1)
+            win = slice(lo, hi)
+            iA = invA[:, win, win]
+            div = (FX[:, :, cs, ce] - FX[:, :, cs, cs]) + (FY[:, :, ce, cs] - FY[:, :, cs, cs])
+            dq = -div * iA
+            qs = q[:, :, win, win]
+            rr = r[:, :, win, win]
+            hcell = qs[0]
+            M = qs[1:4]
+            fcor = self.omega2 * rr[2]
+            cor = torch.stack([rr[1] * M[2] - rr[2] * M[1], rr[2] * M[0] - rr[0] * M[2], rr[0] * M[1] - rr[1] * M[0]])
+            # curvature balance from this block's face normals and lengths
+            mxw = self.nrm[:, 0]                                   # [nb,5,W+1,3]
+            myw = self.nrm[:, 1]
+            regw = self.reg
+            # per-cell face normals: region rule "lower cell if it exists, else upper"
+            def face_m(axis, plus):
+                uu_ = torch.arange(lo, hi, device=q.device)
+                if axis == 0:
+                    k = uu_ + (1 if plus else 0)                    # line index
+                    ua = (k - 1).clamp(0, W - 1)
+                    ra_ = regw[:, lo:hi, :][:, :, ua]               # [nb, rows, cols]
+                    rb_ = regw[:, lo:hi, :][:, :, k.clamp(max=W - 1)]
+                    rf_ = torch.where(ra_ >= 0, ra_, rb_).clamp(min=0)
+                    return mxw[bidx[:, None, None], rf_, k[None, None, :].expand_as(rf_)].permute(3, 0, 1, 2)
+                k = uu_ + (1 if plus else 0)
+                va = (k - 1).clamp(0, W - 1)
+                ra_ = regw[:, :, lo:hi][:, va, :]
+                rb_ = regw[:, :, lo:hi][:, k.clamp(max=W - 1), :]
+                rf_ = torch.where(ra_ >= 0, ra_, rb_).clamp(min=0)
+                return myw[bidx[:, None, None], rf_, k[None, :, None].expand_as(rf_)].permute(3, 0, 1, 2)
+
+            Lw = self.lx[:, cs, cs]
+            Le = self.lx[:, cs, ce]
+            Ls = self.ly[:, cs, cs]
+            Ln = self.ly[:, ce, cs]
+            Sk = Le * face_m(0, True) - Lw * face_m(0, False) + Ln * face_m(1, True) - Ls * face_m(1, False)
+            sbal = 0.5 * self.g * Sk * iA
+            dq[1:] += -fcor * cor + (hcell * hcell) * sbal - self.g * hcell * gb[:, :, win, win]
+            out = a2 * e.dt * dq
+            if a1 != 0.0:
+                out = out + a1 * qs
+            if a0 != 0.0:
+                out = out + a0 * X[:, :, win, win]
+            dd = (out[1:4] * rr).sum(0)
+            out[1:4] = out[1:4] - dd * rr
+            ok = self.need[:, s, win, win][None]      # only what later stages read
+            q = q.clone()
+            q[:, :, win, win] = torch.where(ok, out, qs)
+        # own cells -> output buffer (pool[1]), then swap
+        R, B = d.R, d.B
+        own = q[:, :, R:R + B, R:R + B]
+        dst = self.src.view(nb, W, W)[:, R:R + B, R:R + B]
+        Q1 = e.pool[1]
+        Q1[:, dst.reshape(-1)] = own.reshape(F, -1)
+        e.refresh_halos(Q1)
+        e.pool[0], e.pool[1] = e.pool[1], e.pool[0]
+        e.time += e.dt
+        e.step_count += 1
+
+
+# ---------------------------------------------------------------------------
+# Device tables + descriptors of the gfx950 kernel (fused_step.hip)
+# ---------------------------------------------------------------------------
+
+def fused_supported(engine, B: int = 16) -> Optional[str]:
+    """None if ``engine`` can take the fused step, else the reason it cannot."""
+    from ..models.swe import ShallowWater
+    e = engine
+    if not isinstance(e.physics, ShallowWater):
+        return "fused step: shallow water only"
+    if int(e.physics.limiter) not in (0, 1, 2, 3):
+        return "fused step: PLR limiters only (PPM runs stage by stage)"
+    if e.integ.name != "ssprk3":
+        return "fused step: SSP-RK3 only"
+    if e.layout.num_ranks != 1 or e.plan.num_recv or e.plan.num_send:
+        return "fused step: one rank only (multi-rank runs stage by stage)"
+    if e.plan.n % B:
+        return f"fused step: tile size {e.plan.n} is not a multiple of {B}"
+    if e.layout.N <= NG_PLR * 3:
+        return f"fused step: C{e.layout.N} is too small for the ring"
+    if e.plan.ng < NG_PLR:
+        return "fused step: needs a ghost ring of 2"
+    return None
+
+
+class FusedKernel:
+    """Device tables and the two ping-pong descriptors (pool[0] -> pool[1] and
+    back) of the gfx950 fused step for a one-rank SWE ``Engine`` (HIP backend).
+    Every index the kernel dereferences is checked here, on the host."""
+
+    def __init__(self, engine, B: int = 16):
+        from . import native
+        why = fused_supported(engine, B)
+        if why:
+            raise RuntimeError(why)
+        e = engine
+        self.e = e
+        self.lib = native.require_native()
+        P = FusedPlan(e.layout, e.rank, e.grid, B=B, ns=3)
+        self.plan = P
+        d = P.d
+        W, WS, nb = d.W, d.W + 1, P.nb
+        dev, dt = e.device, e.dtype
+        gmax, cmax = ctypes_limits(self.lib)
+        G, C = P.gtab.shape[1], P.ctab.shape[1]
+        if G > gmax or C > cmax:
+            raise RuntimeError(f"fused step: {G} ghost entries / {C} corner faces exceed the kernel's {gmax} / {cmax}")
+        S = e.plan.S
+        # ---- host-side contract checks ----------------------------------------
+        assert P.src.shape == (nb, W * W) and int(P.src.max()) < S and int(P.src.min()) >= -1
+        nfl = 2 * d.nfx
+        ld = lambda s: (s // W) * WS + s % W
+        for b in range(nb):
+            k = int(P.gcnt[b])
+            assert (P.gtab[b, :k, 2:4] >= 0).all() and (P.gtab[b, :k, 2:4] < W * W).all()
+            for j in range(int(P.ccnt[b])):
+                assert -1 <= P.ctab[b, j, 4] < nfl and -1 <= P.ctab[b, j, 5] < nfl
+        gi = P.gidx.astype(np.int16)
+        assert int(P.gidx.max()) < G
+        gpair = np.zeros((nb, G, 2), dtype=np.int32)
+        gpair[..., 0] = ld(P.gtab[..., 2])
+        gpair[..., 1] = ld(P.gtab[..., 3])
+        ct = np.zeros((nb, C, 8), dtype=np.int32)
+        for b in range(nb):
+            for j in range(int(P.ccnt[b])):
+                sc, side_c, sd, side_d, fc, fd = (int(x) for x in P.ctab[b, j])
+                ct[b, j, 0] = (sc % W) | ((sc // W) << 8) | (side_c << 16)
+                ct[b, j, 1] = (sd % W) | ((sd // W) << 8) | (side_d << 16)
+                ct[b, j, 2], ct[b, j, 3] = fc, fd
+        org = P.org.copy()
+        for b in range(nb):
+            regs = set(int(x) for x in np.unique(P.reg[b]) if x >= 0)
+            flags = sum(1 << r for r in regs)
+            li, rem = divmod(b, P.nbx * P.nby)
+            yb, xb = divmod(rem, P.nbx)
+            org[b, 3] = (xb * B) | ((yb * B) << 12) | (flags << 24)
+        src = P.src.copy()
+        src[~P.need[:, 0]] = -1          # load only what the step reads
+        T_, n, ng = e.plan.T, e.plan.n, e.plan.ng
+        pw = n + 2 * ng
+        cg = torch.zeros((T_, pw, pw, 8), dtype=dt, device=dev)
+        cg[:, ng:ng + n, ng:ng + n] = e.tens["cgeo"]
+        t = lambda a, ty=dt: torch.as_tensor(np.ascontiguousarray(a), dtype=ty, device=dev)
+        self.tens = {
+            "cgeo": cg.reshape(-1, 8).contiguous(),
+            "src": t(src, torch.int32), "org": t(org, torch.int32),
+            "len": t(np.concatenate([P.lx.reshape(nb, -1), P.ly.reshape(nb, -1)], 1)),
+            "nrm": t(P.nrm), "gidx": t(gi, torch.int16), "gtab": t(gpair, torch.int32), "gw": t(P.gt),
+            "ctab": t(ct, torch.int32), "cgf": t(P.cgeo), "ccnt": t(P.ccnt, torch.int32),
+            "push": torch.as_tensor(e.plan.push_map, dtype=torch.int32, device=dev).contiguous(),
+        }
+        assert self.tens["len"].shape == (nb, nfl)
+        assert int(e.plan.push_map.max(initial=-1)) < S
+        self.dcode = native.dtype_code(dt)
+        self.descs = [self._desc(0, 1), self._desc(1, 0)]
+
+    def _desc(self, qi: int, oi: int):
+        from . import native
+        e, P, tn = self.e, self.plan, self.tens
+        p = native.ptr
+        d = native.FusedDesc()
+        d.Q, d.out = p(e.pool[qi]), p(e.pool[oi])
+        for k in ("cgeo", "src", "org", "len", "nrm", "gidx", "gtab", "gw", "ctab", "cgf", "ccnt", "push"):
+            setattr(d, k, p(tn[k]))
+        d.G, d.C = P.gtab.shape[1], P.ctab.shape[1]
+        d.nblocks, d.n, d.N, d.S = P.nb, e.plan.n, e.layout.N, e.plan.S
+        d.mg, d.pw, d.B, d.ns = e.plan.ng, e.plan.P, P.B, P.ns
+        d.limiter = int(e.physics.limiter)
+        for k, st in enumerate(e.integ.stages):
+            d.a0[k], d.a1[k], d.a2[k] = st.a0, st.a1, st.a2
+        d.dt = e.dt
+        d.g = float(e.physics.g)
+        d.omega2 = 2.0 * float(e.physics.omega)
+        return d
+
+    def set_dt(self, dt: float) -> None:
+        for d in self.descs:
+            d.dt = dt
+
+    def launch(self, parity: int = 0, stream: Optional[int] = None) -> None:
+        """One fused step from pool[parity] into pool[1 - parity] (the
+        engine's pool list is not touched)."""
+        from . import native
+        rc = self.lib.stsp_fused_launch(self.dcode, self.descs[parity],
+                                        native.current_stream_handle() if stream is None else stream)
+        native.check(rc, "fused step")
+
+    def step(self, nsteps: int = 1) -> None:
+        """Eager fused steps on the engine (state in pool[0] afterwards)."""
+        e = self.e
+        for _ in range(nsteps):
+            self.launch(0)
+            e.pool[1], e.pool[0] = e.pool[0], e.pool[1]
+            self.descs = [self.descs[1], self.descs[0]]
+            e.time += e.dt
+            e.step_count += 1
+
+
+def ctypes_limits(L) -> Tuple[int, int]:
+    import ctypes
+    g, c = ctypes.c_int(0), ctypes.c_int(0)
+    L.stsp_fused_limits(ctypes.byref(g), ctypes.byref(c))
+    return g.value, c.value

@@ -43,6 +43,22 @@ class StageDesc(ctypes.Structure):
     ]
 
 
+class FusedDesc(ctypes.Structure):
+    """Mirror of FusedDesc (stsp_kernels.h): one fused SSP-RK3 step."""
+    _fields_ = [
+        ("Q", ctypes.c_void_p), ("out", ctypes.c_void_p), ("cgeo", ctypes.c_void_p), ("src", ctypes.c_void_p),
+        ("org", ctypes.c_void_p), ("len", ctypes.c_void_p), ("nrm", ctypes.c_void_p), ("gidx", ctypes.c_void_p),
+        ("gtab", ctypes.c_void_p), ("gw", ctypes.c_void_p), ("ctab", ctypes.c_void_p), ("cgf", ctypes.c_void_p),
+        ("ccnt", ctypes.c_void_p), ("push", ctypes.c_void_p),
+        ("G", ctypes.c_int), ("C", ctypes.c_int),
+        ("nblocks", ctypes.c_int), ("n", ctypes.c_int), ("N", ctypes.c_int), ("S", ctypes.c_int),
+        ("mg", ctypes.c_int), ("pw", ctypes.c_int), ("B", ctypes.c_int), ("ns", ctypes.c_int),
+        ("limiter", ctypes.c_int),
+        ("a0", ctypes.c_double * 4), ("a1", ctypes.c_double * 4), ("a2", ctypes.c_double * 4),
+        ("dt", ctypes.c_double), ("g", ctypes.c_double), ("omega2", ctypes.c_double),
+    ]
+
+
 def lib_path() -> str:
     return _build.lib_for(os.environ.get("STSP_VARIANT", ""))
 
@@ -69,6 +85,10 @@ def load(build_if_missing: bool = True):
         L.stsp_pack_launch.restype = ci
         L.stsp_copy_index_launch.argtypes = [ci, vp, vp, vp, vp, ci, ci, cl, cl, vp]
         L.stsp_copy_index_launch.restype = ci
+        L.stsp_fused_launch.argtypes = [ci, ctypes.POINTER(FusedDesc), vp]
+        L.stsp_fused_launch.restype = ci
+        L.stsp_fused_limits.argtypes = [ctypes.POINTER(ci), ctypes.POINTER(ci)]
+        L.stsp_fused_limits.restype = ci
         _declare_runtime(L)
         _declare_tt(L)
         _LIB = L

@@ -21,7 +21,7 @@ from . import native
 from .native import StageDesc
 
 MAX_PEERS = 32
-OP_STAGE, OP_PACK, OP_COMM_START, OP_COMM_WAIT = 1, 2, 3, 4
+OP_STAGE, OP_PACK, OP_COMM_START, OP_COMM_WAIT, OP_FUSED = 1, 2, 3, 4, 5
 
 _I32x = ctypes.c_int * MAX_PEERS
 
@@ -36,6 +36,7 @@ class StspOp(ctypes.Structure):
         ("npeers", ctypes.c_int), ("send_peer", _I32x), ("send_off", _I32x), ("send_cnt", _I32x),
         ("nrecv", ctypes.c_int), ("recv_peer", _I32x), ("recv_off", _I32x), ("recv_cnt", _I32x),
         ("sendbuf", ctypes.c_void_p), ("recvbuf", ctypes.c_void_p), ("slot_elems", ctypes.c_int),
+        ("fused", ctypes.c_void_p),
     ]
 
 
@@ -118,7 +119,7 @@ class NativeStepper:
 
     def __init__(self, engine, nccl_comm: Optional[int] = None, use_graph: bool = True,
                  steps_per_graph: int = 30, roctx: bool = False, stream: Optional[torch.cuda.Stream] = None,
-                 xgmi=None):
+                 xgmi=None, fused=None):
         from .hip_compute import HipCompute
         e = engine
         if not isinstance(e.compute, HipCompute):
@@ -140,12 +141,24 @@ class NativeStepper:
         self.send_idx = torch.as_tensor(plan.send_idx, dtype=torch.int32, device=e.device)
         assert (plan.send_idx.size == 0) or int(plan.send_idx.max()) < plan.S
         self.stream = stream or torch.cuda.Stream(device=e.device)
-        period = e.integ.period
+        # fused: ops/fused.py::FusedKernel, one launch per step (temporal
+        # blocking), ping-pong between pool[0] and pool[1]: the op list covers
+        # two steps
+        self.fused = fused
+        if fused is not None and (self.remote or xgmi is not None):
+            raise RuntimeError("the fused step runs on one rank only")
+        period = 2 if fused is not None else e.integ.period
         self.period = period
         ops: List[StspOp] = []
         pool = list(e.pool)
         saved_pool = e.pool
-        for _ in range(period):
+        for k in range(period if fused is not None else 0):
+            op = StspOp()
+            op.type = OP_FUSED
+            op.dtype = fused.dcode
+            op.fused = ctypes.addressof(fused.descs[k])
+            ops.append(op)
+        for _ in range(period if fused is None else 0):
             e.pool = pool
             for st in e.integ.stages:
                 if xgmi is not None:
@@ -364,12 +377,22 @@ class NativeStepper:
             e.time += full * e.dt
             e.step_count += full
         if nsteps - full:
-            e.step(nsteps - full)
+            if self.fused is not None:
+                # odd step count: one eager fused step, result copied back to pool[0]
+                cur = torch.cuda.current_stream(e.device)
+                self.fused.launch(0, int(cur.cuda_stream))
+                e.pool[0].copy_(e.pool[1])
+                e.time += e.dt
+                e.step_count += 1
+            else:
+                e.step(nsteps - full)
             self.stats["eager_steps"] += nsteps - full
             self._sync_pool()
 
     def set_dt(self, dt: float) -> None:
         self.e.dt = dt
+        if self.fused is not None:
+            self.fused.set_dt(dt)
         self._check(self.L.stsp_rt_set_dt(self.h, dt), "set_dt")
         self._graphs = {}     # recorded launches carry the old dt
         self._primed = set()

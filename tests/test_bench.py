@@ -38,3 +38,40 @@ def test_bench_self_launches_ranks_cpu(gpus, t):
     assert out["n_gpus"] == gpus
     assert out["max_abs_diff_vs_1gpu_warmup"] == 0.0 and out["max_abs_diff_vs_1gpu"] == 0.0
     assert out["config"]["comm"] == "torch.distributed"
+
+
+def test_bench_deadline_kills_hung_rank_cpu():
+    """A rank that never returns (test hook) is killed at --timeout: the parent
+    prints one status=timeout JSON line naming each rank's last phase and exits
+    non-zero, well inside the driver's own limit."""
+    import time
+    env = dict(os.environ, OMP_NUM_THREADS="1", STSP_BENCH_HANG_RANK="1")
+    env.pop("WORLD_SIZE", None)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "torch",
+                        "--N", "12", "--steps", "2", "--warmup", "1", "--timeout", "25"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=200)
+    assert r.returncode != 0
+    assert time.time() - t0 < 120
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout + r.stderr
+    out = json.loads(lines[0])
+    assert out["status"] == "timeout" and out["value"] is None
+    assert out["phases"]["1"]["phase"] == "warmup"
+    assert out["phases"]["0"]["phase"] in ("warmup", "verify")
+
+
+def test_bench_preflight_refuses_missing_gpus():
+    """--gpus N on the HIP backend with fewer visible GPUs: one status=error
+    line, no ranks started (this container has no GPU at all)."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("enough GPUs visible")
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("STSP_SHARE_GPU", None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["status"] == "error" and "GPU" in out["error"]

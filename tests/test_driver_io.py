@@ -104,6 +104,28 @@ def test_watchdog_recovers_from_checkpoint(tmp_path):
     assert out["steps_run"] > 40
 
 
+def test_checkpoints_between_watchdog_intervals_hold_finite_states(tmp_path):
+    """Checkpoint interval 2, watchdog interval 3 (not aligned): a checkpoint
+    that falls between watchdog checks tests the state first, so no saved
+    checkpoint ever holds a non-finite state and recovery always finds a good
+    one."""
+    c = _cfg(tmp_path, checkpoint_interval=2, keep_checkpoints=3)
+    c["runtime"] = {"watchdog_interval": 3}
+    s = S.Solver(c, verbose=False)
+    s.initialize()
+    s.set_dt(s.dt * 64)            # blows up within a few steps
+    try:
+        s.run(nsteps=30)
+    except FloatingPointError:
+        pass
+    root = os.path.join(str(tmp_path), "checkpoints")
+    steps = ckpt.list_checkpoints(root)
+    assert steps
+    for st in steps:
+        vals = ckpt.read_fields(ckpt.step_dir(root, st))
+        assert all(np.isfinite(v).all() for v in vals.values()), st
+
+
 def test_history_frames_follow_simulated_time_across_recovery(tmp_path):
     """After a watchdog rollback the replayed interval overwrites its own
     history frames (frames are indexed by simulated time, not by a counter)."""

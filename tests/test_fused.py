@@ -1,0 +1,173 @@
+"""Fused SSP-RK3 step (temporal blocking, ops/fused.py + ops/csrc/fused_step.hip)
+against the stage-by-stage PyTorch oracle.
+
+CPU: the PyTorch rendering of the fused algorithm (FusedTorch, the same host
+tables and phases as the kernel) reproduces Engine.step to rounding on grids
+whose windows cross one panel edge, two panel edges, and cube corners.
+GPU: the gfx950 kernel against the fp64 oracle (1e-11), fp32 (1e-4), graph
+replay vs eager (bitwise), and a corner-poison check."""
+import numpy as np
+import pytest
+import torch
+
+from stsphere.engine import Engine
+from stsphere.models.geometry import CubedSphereGrid
+from stsphere.models.swe import ShallowWater
+from stsphere.ops.fused import FusedPlan, FusedTorch, fused_supported, region
+from stsphere.parallel.layout import TileLayout
+
+
+def _relerr(a_eng, b_eng):
+    a = a_eng.tiles_view().reshape(4, -1).double()
+    b = b_eng.tiles_view().reshape(4, -1).double()
+    return ((a - b).abs().amax(1) / a.abs().amax(1)).max().item()
+
+
+@pytest.mark.parametrize("N,t,B,case,lim", [
+    (16, 1, 8, "tc5", 2),     # one panel edge per window side, cube corners
+    (24, 2, 4, "tc5", 2),     # two tiles per panel edge, tile-clipped interpolation
+    (12, 1, 4, "tc2", 1),     # windows that cross both opposite panel edges
+    (24, 1, 8, "tc6", 3),
+])
+def test_fused_torch_matches_stage_oracle(N, t, B, case, lim):
+    grid = CubedSphereGrid(N)
+    L = TileLayout(N, t, 1, ng=2)
+    ref = Engine(ShallowWater(case, limiter=lim), L, grid=grid)
+    fe = Engine(ShallowWater(case, limiter=lim), L, grid=grid, dt=ref.dt)
+    ft = FusedTorch(fe, FusedPlan(L, 0, grid, B=B, ns=3))
+    for _ in range(2):
+        ref.step(1)
+        ft.step()
+    assert _relerr(ref, fe) < 1e-12
+    assert fe.step_count == 2
+
+
+def test_fused_plan_invariants():
+    N, B = 32, 16
+    L = TileLayout(N, 2, 1, ng=2)
+    P = FusedPlan(L, 0, CubedSphereGrid(N), B=B, ns=3)
+    d = P.d
+    assert (d.W, d.R, d.L1, d.H1) == (28, 6, 2, 24)
+    W = d.W
+    for b in range(P.nb):
+        reg = P.reg[b].reshape(W, W)
+        X0, Y0 = P.org[b, 0], P.org[b, 1]
+        vv, uu = np.mgrid[0:W, 0:W]
+        assert (region(X0 + uu, Y0 + vv, N) == reg).all()
+        # every needed cell exists and is loaded; stage s needs lie in its square
+        assert (P.src[b][P.need[b, 0]] >= 0).all()
+        for s in range(1, d.ns + 1):
+            lo, hi = d.stage_range(s)
+            m = P.need[b, s].reshape(W, W)
+            assert not m[:lo].any() and not m[hi:].any() and not m[:, :lo].any() and not m[:, hi:].any()
+            assert (P.need[b, s] <= P.need[b, s - 1]).all()
+        # ghost entries name two window cells and a weight in [-1, 2]
+        k = int(P.gcnt[b])
+        assert ((P.gtab[b, :k, 2:] >= 0) & (P.gtab[b, :k, 2:] < W * W)).all()
+        assert (np.abs(P.gt[b, :k]) <= 2).all()
+    # cube-corner blocks have corner faces
+    assert P.ccnt.max() > 0
+
+
+def test_fused_supported_reasons():
+    L = TileLayout(24, 1, 1, ng=2)
+    e = Engine(ShallowWater("tc5", limiter=4), TileLayout(24, 1, 1, ng=3))
+    assert "PLR" in fused_supported(e)
+    e = Engine(ShallowWater("tc5"), L, integrator="rk4")
+    assert "SSP-RK3" in fused_supported(e)
+    e = Engine(ShallowWater("tc5"), L)
+    assert "multiple of 16" in fused_supported(e)
+    e = Engine(ShallowWater("tc5"), TileLayout(32, 2, 1, ng=2))
+    assert fused_supported(e) is None
+
+
+# ---------------------------------------------------------------------------
+# GPU: the gfx950 kernel
+# ---------------------------------------------------------------------------
+
+def _gpu_pair(N, t, dtype=torch.float64, case="tc5", lim=2):
+    grid = CubedSphereGrid(N)
+    L = TileLayout(N, t, 1, ng=2)
+    ref = Engine(ShallowWater(case, limiter=lim), L, grid=grid, dtype=torch.float64, device="cuda", backend="torch")
+    hip = Engine(ShallowWater(case, limiter=lim), L, grid=grid, dtype=dtype, device="cuda", backend="hip", dt=ref.dt)
+    return ref, hip
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,t,case,lim", [(32, 2, "tc5", 2), (48, 1, "tc5", 1), (96, 2, "tc5", 2),
+                                          (48, 3, "tc6", 3), (32, 1, "tc2", 0)])
+def test_fused_kernel_fp64_matches_oracle(N, t, case, lim):
+    from stsphere.ops.fused import FusedKernel
+    ref, hip = _gpu_pair(N, t, case=case, lim=lim)
+    fk = FusedKernel(hip)
+    for _ in range(3):
+        ref.step(1)
+        fk.step(1)
+        torch.cuda.synchronize()
+        assert _relerr(ref, hip) < 1e-11
+
+
+@pytest.mark.gpu
+def test_fused_kernel_matches_stage_kernel_and_halos():
+    """Fused vs the launch-per-stage kernel over 6 steps; the fused step also
+    leaves every same-rank ghost slot current (it pushes like the stage kernel)."""
+    from stsphere.ops.fused import FusedKernel
+    _, a = _gpu_pair(48, 3)
+    _, b = _gpu_pair(48, 3)
+    b.dt = a.dt
+    fk = FusedKernel(b)
+    a.step(6)
+    fk.step(6)
+    torch.cuda.synchronize()
+    assert _relerr(a, b) < 1e-11
+    q = b.pool[0]
+    assert torch.equal(q[:, b.halo_dst], q[:, b.halo_src])
+
+
+@pytest.mark.gpu
+def test_fused_kernel_fp32_close_to_fp64_oracle():
+    from stsphere.ops.fused import FusedKernel
+    ref, hip = _gpu_pair(48, 3, dtype=torch.float32)
+    fk = FusedKernel(hip)
+    ref.step(3)
+    fk.step(3)
+    torch.cuda.synchronize()
+    assert _relerr(ref, hip) < 1e-4
+
+
+@pytest.mark.gpu
+def test_fused_kernel_never_reads_corner_ghosts():
+    """Corner ghost blocks of the padded storage (no single source at a cube
+    corner) are poisoned with NaN: the fused window gathers every cell from its
+    source, so the state stays finite and equal to the unpoisoned run."""
+    from stsphere.ops.fused import FusedKernel
+    _, a = _gpu_pair(32, 2)
+    _, b = _gpu_pair(32, 2)
+    b.dt = a.dt
+    b.poison_corners()
+    fa, fb = FusedKernel(a), FusedKernel(b)
+    fa.step(3)
+    fb.step(3)
+    torch.cuda.synchronize()
+    assert torch.isfinite(b.tiles_view()).all()
+    assert torch.equal(a.tiles_view(), b.tiles_view())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nsteps", [6, 5])
+def test_fused_native_graph_equals_eager(nsteps):
+    """NativeStepper(fused=...) replays hipGraphs of fused launches (period 2,
+    odd counts end with one eager fused step): bitwise equal to eager steps."""
+    from stsphere.ops.fused import FusedKernel
+    from stsphere.ops.native_runtime import NativeStepper
+    _, a = _gpu_pair(32, 2)
+    _, b = _gpu_pair(32, 2)
+    b.dt = a.dt
+    FusedKernel(a).step(nsteps)
+    r = NativeStepper(b, use_graph=True, steps_per_graph=4, fused=FusedKernel(b))
+    r.run(nsteps)
+    torch.cuda.synchronize()
+    assert torch.equal(a.tiles_view(), b.tiles_view())
+    assert b.step_count == nsteps
+    assert r.stats["graph_steps"] == (nsteps // 2) * 2
+    r.close()
