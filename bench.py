@@ -230,14 +230,16 @@ def main():
     runtime = a.runtime
     if runtime == "auto":
         runtime = "native" if (device.type == "cuda" and backend == "hip") else "eager"
-        if runtime == "native" and world == 1:
+        if runtime == "native" and (world == 1 or a.comm in ("auto", "xgmi")):
             from stsphere.ops.fused import fused_supported
             probe = Engine(phys_factory(), layout, rank, grid=grid, dtype=dtype, device="cpu", integrator=a.integrator)
             if fused_supported(probe) is None:
                 runtime = "fused"
             del probe
     comm = a.comm if world > 1 else "none"
-    if world > 1 and runtime not in ("native", "fused"):
+    if world > 1 and runtime == "fused":
+        comm = "xgmi"                    # remote window cells through the fused kernel's xGMI ring
+    elif world > 1 and runtime not in ("native", "fused"):
         comm = "torch.distributed"
     elif comm == "auto":
         comm = "xgmi" if world > 1 else "none"
@@ -264,7 +266,7 @@ def main():
     def build(comm):
         transport = None
         if world > 1:
-            if runtime == "native":
+            if runtime in ("native", "fused"):
                 transport = NativeBuffers(layout.plan(rank), phys.F, dtype, device)
             else:
                 transport = TorchDistTransport(layout.plan(rank), phys.F, dtype, device)
@@ -273,10 +275,13 @@ def main():
                      backend=backend, integrator=a.integrator, dt=a.dt, block=blk)
         runner, xg = None, None
         if runtime == "fused":
-            # one launch per SSP-RK3 step (temporal blocking, ops/fused.py), hipGraph replay
+            # one launch per SSP-RK3 step (temporal blocking, ops/fused.py), hipGraph replay;
+            # between GPUs the remote window cells travel through the kernel's own xGMI ring
             from stsphere.ops.fused import FusedKernel
             from stsphere.ops.native_runtime import NativeStepper
-            runner = NativeStepper(eng, use_graph=True, steps_per_graph=spg, fused=FusedKernel(eng))
+            fk = FusedKernel(eng, timeout_s=2.0)      # collective with several ranks
+            xg = fk if world > 1 else None
+            runner = NativeStepper(eng, use_graph=True, steps_per_graph=spg, fused=fk)
         elif runtime == "native":
             # C++ runtime, hipGraph replay; between GPUs either direct xGMI
             # stores from the stage kernels (graph-captured) or RCCL grouped
@@ -346,6 +351,7 @@ def main():
         close(runner, xg)
         fallback_reason = fallback_reason or "xgmi setup failed on another rank"
         comm = "rccl"
+        runtime = "native" if runtime == "fused" else runtime
         _phase("build_rccl")
         eng, runner, xg = build(comm)
     elif not ok:
@@ -373,6 +379,7 @@ def main():
         close(runner, xg)
         fallback_reason = fallback_reason or f"{comm} check failed on another rank"
         comm = "rccl"                    # fall back from a fresh state
+        runtime = "native" if runtime == "fused" else runtime
         _phase("build_rccl")
         eng, runner, xg = build(comm)
         if not warm(eng, runner):

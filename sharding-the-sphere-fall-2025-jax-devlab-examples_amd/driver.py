@@ -194,6 +194,13 @@ class Solver:
             if int(attrs["N"]) != self.layout.N or list(attrs["fields"]) != list(self.fields):
                 raise ValueError(f"{path}: initial condition is C{attrs['N']} {attrs['fields']}, "
                                  f"run is C{self.layout.N} {self.fields}")
+            # the state must belong to this physics and case: TC2 and TC5 share the
+            # SWE fields but not the topography the engines were built with
+            want = {"physics": self.physics.name, "case": getattr(self.physics, "case", None)}
+            for k, v in want.items():
+                if k in attrs and attrs[k] != v:
+                    raise ValueError(f"{path}: initial condition was written for {k} {attrs[k]!r}, "
+                                     f"the run is {k} {v!r} (remove the file or fix io.initial_condition)")
             glob = np.stack([zarr_lite.read_array(path, f) for f in self.fields])
             for e in self.engines:
                 loc = np.stack([e.geo.gather_global(glob[k]) for k in range(len(self.fields))])

@@ -26,10 +26,19 @@
 // ops/fused.py::FusedTorch is the same algorithm in PyTorch; both are checked
 // against the stage-by-stage oracle (tests/test_fused.py).
 //
-// Work split (1024 threads): thread t < W^2 owns window cell t for the whole
-// step (its step-start and stage states stay in registers, primitives in LDS);
-// face tasks (x-faces, then y-faces, then corner faces) are spread over all
-// threads.  Per stage: faces -> barrier -> cell updates -> barrier.
+// Work split (1024 threads): thread t < W^2 owns one window cell for the whole
+// step (its step-start and stage states and its cell record stay in registers,
+// primitives in LDS).  Owners are ordered by stage square (the block first, then
+// the rings stage 2 and stage 1 add, then the outer ring), so the cells stage s
+// updates are threads [0, |square_s|): whole waves, no idle lanes.  Face tasks
+// (x-faces, then y-faces, then cube-corner faces) are spread over all threads.
+// Per stage: faces -> barrier -> cell updates -> barrier.
+//
+// Cross-panel stencils: a host table gives every window cell one 16-bit code per
+// side: -1 = the window neighbour in the cell's own frame, >= 0 = ghost entry
+// (interpolation pair + weight, evaluated on the fly from the current window),
+// -3 = no cell here (beyond a cube corner); faces touching a -3 cell are the
+// corner list's.
 #include "stage_common.h"
 
 
@@ -46,6 +55,7 @@ struct FD {
   static constexpr int NFX = H1 * (H1 + 1);
   static constexpr int NFL = 2 * NFX;
   static constexpr int NT = 1024;
+  static_assert(W * W <= NT, "one owner thread per window cell");
   static constexpr int GMAX = 256;
   static constexpr int CMAX = 32;
 };
@@ -57,6 +67,48 @@ __device__ __forceinline__ int fregion(int X, int Y, int N) {
   return iny ? (X < 0 ? 1 : 2) : -1;
 }
 
+// Cell t of the square annulus [lo, lo+L)^2 minus [lo+w, lo+L-w)^2: the w top
+// rows, the w bottom rows, then the side columns row by row.
+__device__ __forceinline__ void annulus(int t, int lo, int L, int w, int& u, int& v) {
+  if (t < w * L) {
+    u = lo + t % L; v = lo + t / L;
+    return;
+  }
+  t -= w * L;
+  if (t < w * L) {
+    u = lo + t % L; v = lo + L - w + t / L;
+    return;
+  }
+  t -= w * L;
+  const int r = t / (2 * w), c = t - r * 2 * w;
+  v = lo + w + r;
+  u = c < w ? lo + c : lo + L - 2 * w + c;
+}
+
+// Owner order: the block (square of stage NS), then the ring each earlier stage
+// adds, then the outer ring of width 2 (loaded, never updated).
+template <int NS, int B>
+__device__ __forceinline__ void owner_cell(int t, int& u, int& v) {
+  using D = FD<NS, B>;
+  constexpr int R = D::R;
+  if (t < B * B) {
+    u = R + t % B; v = R + t / B;
+    return;
+  }
+  int done = B * B;
+#pragma unroll
+  for (int k = 1; k <= NS; ++k) {             // ring k: width 2 around the square of side B + 4 (k - 1)
+    const int L = B + 4 * k;
+    const int n = L * L - (L - 4) * (L - 4);
+    if (t < done + n) {
+      annulus(t - done, R - 2 * k, L, 2, u, v);
+      return;
+    }
+    done += n;
+  }
+  u = -1; v = -1;
+}
+
 template <typename T>
 struct FArgs {
   const T* Q;
@@ -66,7 +118,7 @@ struct FArgs {
   const int* org;
   const T* len;
   const T* nrm;
-  const short* gidx;
+  const unsigned long long* code;
   const int* gtab;
   const T* gw;
   const int* ctab;
@@ -74,92 +126,230 @@ struct FArgs {
   const int* ccnt;
   const int* push;
   int G, C, nblocks, n, N, S, mg, pw;
+  int links[6];           // per face: 4 x (nbr face | nbr edge << 3 | reversed << 5), sides W E S N (6 bits each)
+  int local_src;          // 1: one rank holding every tile in id order -> window sources computed, no table
+  unsigned mdiv_n;        // ceil(2^32 / n) (exact for the coordinates used), 0 = divide
   T a0[4], a1[4], a2[4];
   T dt, g, omega2;
+  // direct xGMI exchange (XG)
+  int ring, K;
+  const unsigned long long* recv;
+  T* const* peer_ring;
+  const int* xpush;
+  int* epoch;
+  int* err;
+  long long timeout_ticks;
+  unsigned long long* stamps;
 };
 
-template <typename T, int LIM, int NS, int B>
+// phase stamp (profiling): lane 0 of every wave, when a.stamps is set
+#define FSTAMP(k)                                                                                \
+  do {                                                                                           \
+    if (a.stamps) {                                                                              \
+      __builtin_amdgcn_sched_barrier(0);                                                         \
+      if ((threadIdx.x & 63) == 0)                                                               \
+        a.stamps[((long)bid * 16 + (threadIdx.x >> 6)) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+      __builtin_amdgcn_sched_barrier(0);                                                         \
+    }                                                                                            \
+  } while (0)
+
+// Padded-storage offset of the cell at extended-panel coordinates (X, Y) of face
+// f, for one rank holding all 6 t^2 tiles in id order (tile = face t^2 + tj t + ti);
+// -1 beyond a cube corner.  The cube-edge crossing is models/topology.py's
+// neighbor_cell: across side k of face f lies face g's edge e2, positions
+// reversed or not (the reference's T / R / TR table, PY:114-139).
+__device__ __forceinline__ int window_src(int f, int X, int Y, int N, int n, int pw, int mg, unsigned md,
+                                          const int (&links)[6]) {
+  const bool inx = (unsigned)X < (unsigned)N, iny = (unsigned)Y < (unsigned)N;
+  if (!inx && !iny) return -1;
+  int g = f, I = X, J = Y;
+  if (!(inx && iny)) {
+    int side, depth, pos;
+    if (X < 0) { side = 0; depth = -X; pos = Y; }
+    else if (X >= N) { side = 1; depth = X - N + 1; pos = Y; }
+    else if (Y < 0) { side = 2; depth = -Y; pos = X; }
+    else { side = 3; depth = Y - N + 1; pos = X; }
+    const int lk = (links[f] >> (6 * side)) & 63;
+    g = lk & 7;
+    const int e2 = (lk >> 3) & 3;
+    const int p2 = (lk >> 5) ? N - 1 - pos : pos;
+    if (e2 == 0) { I = depth - 1; J = p2; }
+    else if (e2 == 1) { I = N - depth; J = p2; }
+    else if (e2 == 2) { I = p2; J = depth - 1; }
+    else { I = p2; J = N - depth; }
+  }
+  const int t = N / n;
+  const int ti = md ? (int)__umulhi((unsigned)I, md) : I / n;
+  const int tj = md ? (int)__umulhi((unsigned)J, md) : J / n;
+  const int tid = (g * t + tj) * t + ti;
+  return (tid * pw + (J - tj * n) + mg) * pw + (I - ti * n) + mg;
+}
+
+// neighbour code of a window cell on one side (-1 window neighbour, >= 0 ghost
+// entry, -3 no cell)
+__device__ __forceinline__ int ncode(unsigned long long c, int side) {
+  return (int)(short)(unsigned short)(c >> (16 * side));
+}
+
+template <typename T, int LIM, int NS, int B, bool XG>
 __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   using D = FD<NS, B>;
   constexpr int W = D::W, WS = D::WS, WW = D::WW, R = D::R, L1 = D::L1, H1 = D::H1;
   constexpr int NFX = D::NFX, NFL = D::NFL, NT = D::NT;
-  __shared__ T s_w[5][W][WS];            // primitives h, vx, vy, vz and sound speed
-  __shared__ T s_fl[4][NFL];             // face fluxes (stage-1 face set, compact)
-  __shared__ T s_len[NFL];               // face lengths
-  __shared__ T s_nrm[2][5][W + 1][3];    // line normals per region (oriented +u / +v)
-  __shared__ short s_gi[20 * W];         // ghost entry per (strip, pos)
-  __shared__ short s_gs[D::GMAX][2];     // interpolation pair (LDS window index)
-  __shared__ T s_gt[D::GMAX];
+  constexpr int NN = 2 * 5 * 3 * (W + 1);
+  __shared__ T s_w[5][W][WS];              // primitives h, vx, vy, vz and sound speed
+  __shared__ T s_fl[4][NFL];               // face fluxes (stage-1 face set, compact)
+  __shared__ T s_len[NFL];                 // face lengths
+  __shared__ T s_nrm[2][5][3][W + 1];      // line normals per region, component-major
+  __shared__ unsigned long long s_code[W * W];   // neighbour codes (edge blocks)
+  __shared__ short s_gs[D::GMAX][2];       // ghost entry: interpolation pair (LDS window index)
+  __shared__ T s_gt[D::GMAX];              //              and weight
   __shared__ int s_ct[D::CMAX][4];
   __shared__ T s_cg[D::CMAX][4];
+  // step-start state of the cells stages 2.. update (owners [0, NX2)): the
+  // a0 X term of SSP-RK3; in LDS rather than registers (register pressure)
+  constexpr int NX2 = NS > 1 ? (B + 4 * (NS - 2)) * (B + 4 * (NS - 2)) : 1;
+  __shared__ T s_x[4][NX2];
 
   const int tid = threadIdx.x;
   const int bid = xcd_remap(blockIdx.x, a.nblocks);
   const int N = a.N;
   const int* og = a.org + bid * 4;
   const int X0 = og[0], Y0 = og[1], tile = og[2], ow = og[3];
-  const int xo = ow & 0xFFF, yo = (ow >> 12) & 0xFFF, flags = (ow >> 24) & 0x1F;
+  const int xo = ow & 0xFFF, yo = (ow >> 12) & 0xFFF, flags = (ow >> 24) & 0x1F;   // face: bits 29..31
   const bool edge = (flags & 0x1E) != 0;                 // a side region is present (block-uniform)
   const T* wf = &s_w[0][0][0];
+  FSTAMP(0);
 
-  // ---- 0. prologue: tables -> LDS, window state + cell records -> registers ----
-  const int u = tid % W, v = tid / W;
+  // ---- 0. prologue: every global load first, then the LDS writes --------------
+  int u = -1, v = -1;
   const bool owner = tid < W * W;
+  if (owner) owner_cell<NS, B>(tid, u, v);
+  const int wi = v * WS + u;                             // this owner's LDS window index
+  int xe = 0;                                            // steps this block has completed (XG)
+  if constexpr (XG) xe = a.epoch[bid];
   int src = -1;
-  if (owner) src = a.src[(long)bid * W * W + tid];
-  {
-    const T* ln = a.len + (long)bid * NFL;
-    for (int k = tid; k < NFL; k += NT) s_len[k] = ln[k];
-    const T* nr = a.nrm + (long)bid * (2 * 5 * (W + 1) * 3);
-    T* sn = &s_nrm[0][0][0][0];
-    constexpr int NN = 2 * 5 * (W + 1) * 3;
-    for (int k = tid; k < NN; k += NT) {
-      const int r_ = (k / ((W + 1) * 3)) % 5;
-      if (r_ == 0 || ((flags >> r_) & 1)) sn[k] = nr[k];
-    }
-    if (edge) {
-      const short* gi = a.gidx + (long)bid * 20 * W;
-      for (int k = tid; k < 20 * W; k += NT) s_gi[k] = gi[k];
-      const int* gt = a.gtab + (long)bid * a.G * 2;
-      const T* gw = a.gw + (long)bid * a.G;
-      for (int k = tid; k < a.G; k += NT) {
-        s_gs[k][0] = (short)gt[2 * k];
-        s_gs[k][1] = (short)gt[2 * k + 1];
-        s_gt[k] = gw[k];
-      }
-    }
+  if (owner) {
+    if (a.local_src)    // computed: no dependent table load in front of the window load
+      src = window_src((int)((unsigned)ow >> 29), X0 + u, Y0 + v, N, a.n, a.pw, a.mg, a.mdiv_n, a.links);
+    else
+      src = a.src[(long)bid * W * W + v * W + u];
   }
-  const int ncor = edge ? a.ccnt[bid] : 0;
-  if (tid < ncor) {
-    const int* ct = a.ctab + ((long)bid * a.C + tid) * 8;
-    const T* cg = a.cgf + ((long)bid * a.C + tid) * 4;
+  // tables into registers
+  constexpr int LPT = (NFL + NT - 1) / NT;
+  T lnv[LPT];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { s_ct[tid][k] = ct[k]; s_cg[tid][k] = cg[k]; }
+  for (int k = 0; k < LPT; ++k) {
+    const int j = tid + k * NT;
+    lnv[k] = j < NFL ? a.len[(long)bid * NFL + j] : T(0);
   }
-  // own window cell
-  T X[4], Q[4];
-  T iA = T(0), r0 = T(0), r1 = T(0), r2 = T(0), gb0 = T(0), gb1 = T(0), gb2 = T(0);
-  const bool loaded = src >= 0;
-  const bool in1 = (u >= L1) & (u < L1 + H1) & (v >= L1) & (v < L1 + H1);
-  if (loaded) {
+  T nrv = T(0);
+  const int nr_reg = (tid / (3 * (W + 1))) % 5;
+  const bool nr_ld = tid < NN && (nr_reg == 0 || ((flags >> nr_reg) & 1));
+  static_assert(NN <= NT, "one normal component per thread");
+  if (nr_ld) nrv = a.nrm[(long)bid * NN + tid];
+  unsigned long long cdv = 0;
+  int gs0 = 0, gs1 = 0;
+  T gtv = T(0);
+  int ncor = 0;
+  int ct4[4] = {0, 0, 0, 0};
+  T cg4[4] = {T(0), T(0), T(0), T(0)};
+  if (edge) {
+    if (owner) cdv = a.code[(long)bid * W * W + v * W + u];
+    if (tid < a.G) {
+      gs0 = a.gtab[((long)bid * a.G + tid) * 2];
+      gs1 = a.gtab[((long)bid * a.G + tid) * 2 + 1];
+      gtv = a.gw[(long)bid * a.G + tid];
+    }
+    ncor = a.ccnt[bid];
+    if (tid < ncor) {
+      const int* ct = a.ctab + ((long)bid * a.C + tid) * 8;
+      const T* cg = a.cgf + ((long)bid * a.C + tid) * 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { ct4[k] = ct[k]; cg4[k] = cg[k]; }
+    }
+  }
+  // own window cell: state (+ record for the cells stage 1 updates)
+  T Q[4];
+  T iA = T(0), r0 = T(0), r1 = T(0), r2 = T(0), gb0 = T(0), gb1 = T(0), gb2 = T(0), S0 = T(0), S1 = T(0),
+    S2 = T(0);
+  const bool loaded = src >= 0 || (XG && src <= -2);
+  const bool in1 = tid < (B + 4 * (NS - 1)) * (B + 4 * (NS - 1));   // updated by stage 1
+  if (XG && src <= -2) {
+    // another rank's cell: spin on its granules in ring slot xe % SLOTS until
+    // every tag carries this step (xe + 1); a timeout sets err and falls through
+    constexpr int G = sizeof(T) / 4;
+    const gu64* rp = (const gu64*)(a.recv) + (long)(xe % STSP_XG_SLOTS) * a.ring + (long)(-2 - src) * (4 * G);
+    const unsigned want = (unsigned)xe + 1u;
+    unsigned long long gr[4 * G];
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < 4 * G; ++k) {
+        gr[k] = __hip_atomic_load(rp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok &= (unsigned)(gr[k] >> 32) == want;
+      }
+      if (ok) break;
+      if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
+        __hip_atomic_store((gu32*)a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      if constexpr (G == 2)
+        Q[f] = __builtin_bit_cast(T, (gr[2 * f + 1] << 32) | (gr[2 * f] & 0xFFFFFFFFull));
+      else
+        Q[f] = __builtin_bit_cast(T, (unsigned)gr[f]);
+    }
+  } else if (loaded) {
     const unsigned S = (unsigned)a.S;
 #pragma unroll
     for (int f = 0; f < 4; ++f) Q[f] = *o32(a.Q, (unsigned)src + f * S);
-    if (in1) {
-      T rec[8];
-      load_rec8<T>(o32(a.cgeo, (unsigned)src * 8u), rec);
-      iA = rec[0]; r0 = rec[1]; r1 = rec[2]; r2 = rec[3];
-      gb0 = rec[4]; gb1 = rec[5]; gb2 = rec[6];
-    }
   } else {
 #pragma unroll
     for (int f = 0; f < 4; ++f) Q[f] = T(0);
   }
+  if (loaded && in1) {
+    // record: 1/A, centre (3), grad b (3), curvature sum S = sum(L m) (3), 0, 0;
+    // remote cells' records follow the S local ones
+    const unsigned ci = src >= 0 ? (unsigned)src : (unsigned)(a.S + (-2 - src));
+    T rec[12];
+    const T* rp = o32(a.cgeo, ci * 12u);
+    T r8[8];
+    load_rec8<T>(rp, r8);
 #pragma unroll
-  for (int f = 0; f < 4; ++f) X[f] = Q[f];
+    for (int k = 0; k < 8; ++k) rec[k] = r8[k];
+    rec[8] = rp[8]; rec[9] = rp[9];
+    iA = rec[0]; r0 = rec[1]; r1 = rec[2]; r2 = rec[3];
+    gb0 = rec[4]; gb1 = rec[5]; gb2 = rec[6];
+    S0 = rec[7]; S1 = rec[8]; S2 = rec[9];
+  }
+  if (tid < NX2) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) s_x[f][tid] = Q[f];
+  }
+  // tables -> LDS
+#pragma unroll
+  for (int k = 0; k < LPT; ++k) {
+    const int j = tid + k * NT;
+    if (j < NFL) s_len[j] = lnv[k];
+  }
+  if (nr_ld) (&s_nrm[0][0][0][0])[tid] = nrv;
+  if (edge) {
+    if (owner) s_code[v * W + u] = cdv;
+    if (tid < a.G) { s_gs[tid][0] = (short)gs0; s_gs[tid][1] = (short)gs1; s_gt[tid] = gtv; }
+    if (tid < ncor) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { s_ct[tid][k] = ct4[k]; s_cg[tid][k] = cg4[k]; }
+    }
+  }
   auto put = [&](const T (&q)[4]) {
     const T inv = q[0] != T(0) ? trcp(q[0]) : T(0);
-    T* p = &s_w[0][v][u];
+    T* p = &s_w[0][0][0] + wi;
     p[0] = q[0];
     p[WW] = q[1] * inv;
     p[2 * WW] = q[2] * inv;
@@ -167,12 +357,12 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
     p[4 * WW] = tsqrt(a.g * tmax(q[0], T(0)));
   };
   if (owner) put(Q);
+  FSTAMP(1);
   __syncthreads();
+  FSTAMP(2);
 
-  // ghost-strip value of field f for (strip, pos), or `dflt` when untabulated
-  auto ghost = [&](int strip, int pos, int f, T dflt) -> T {
-    const int e = s_gi[strip * W + pos];
-    if (e < 0) return dflt;
+  // value of field f of ghost entry e (Putman-Lin interpolation, current window)
+  auto ghost = [&](int e, int f) -> T {
     const T x0 = wf[f * WW + s_gs[e][0]], x1 = wf[f * WW + s_gs[e][1]];
     return x0 + s_gt[e] * (x1 - x0);
   };
@@ -200,18 +390,18 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
           st = WS;
         }
         const int ib = fv * WS + fu, ia = ib - st;
-        int ra = 0, rb = 0, ram = 0, rbp = 0;
+        const int sm = ax ? 2 : 0;                           // side index of -axis; +axis = sm + 1
+        int eam = -1, eap = -1, ebm = -1, ebp = -1, ra = 0;
+        bool ok = true;
         if (edge) {
-          const int X = X0 + fu, Y = Y0 + fv;
-          const int dx = ax ? 0 : 1, dy = ax ? 1 : 0;
-          rb = fregion(X, Y, N);
-          ra = fregion(X - dx, Y - dy, N);
-          ram = fregion(X - 2 * dx, Y - 2 * dy, N);
-          rbp = fregion(X + dx, Y + dy, N);
+          const int ci = fv * W + fu, cj = ci - (ax ? W : 1);   // window indices of b and a
+          const unsigned long long ca = s_code[cj], cb = s_code[ci];
+          eam = ncode(ca, sm); eap = ncode(ca, sm + 1);
+          ebm = ncode(cb, sm); ebp = ncode(cb, sm + 1);
+          ok = eam != -3 && ebm != -3;                         // both cells exist
+          ra = fregion(X0 + fu - (ax ? 0 : 1), Y0 + fv - (ax ? 1 : 0), N);
         }
-        if (ra >= 0 && rb >= 0) {
-          const int pos = ax ? fu : fv;
-          const int sm = ax ? 2 : 0;                         // side index of -axis; +axis = sm + 1
+        if (ok) {
           T wl[4], wr[4], cl[5], cr[5];
 #pragma unroll
           for (int f = 0; f < 5; ++f) { cl[f] = wf[f * WW + ia]; cr[f] = wf[f * WW + ib]; }
@@ -220,19 +410,17 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
             T am = wf[f * WW + ia - st], bp = wf[f * WW + ib + st];
             T ap = cr[f], bm = cl[f];
             if (edge) {
-              if (ram != ra) am = ghost(ra * 4 + sm, pos, f, am);
-              if (rb != ra) {
-                ap = ghost(ra * 4 + sm + 1, pos, f, ap);
-                bm = ghost(rb * 4 + sm, pos, f, bm);
-              }
-              if (rbp != rb) bp = ghost(rb * 4 + sm + 1, pos, f, bp);
+              if (eam >= 0) am = ghost(eam, f);
+              if (eap >= 0) ap = ghost(eap, f);
+              if (ebm >= 0) bm = ghost(ebm, f);
+              if (ebp >= 0) bp = ghost(ebp, f);
             }
             wl[f] = cl[f] + half_slope<LIM>(cl[f] - am, ap - cl[f]);
             wr[f] = cr[f] - half_slope<LIM>(cr[f] - bm, bp - cr[f]);
           }
-          const T* m = &s_nrm[ax ? 1 : 0][ra][k][0];
+          const T* m = &s_nrm[ax ? 1 : 0][ra][0][k];
           T fl[4];
-          swe_flux<T>(wl, wr, cl, cr, m[0], m[1], m[2], s_len[fslot], a.g, fl);
+          swe_flux<T>(wl, wr, cl, cr, m[0], m[W + 1], m[2 * (W + 1)], s_len[fslot], a.g, fl);
 #pragma unroll
           for (int f = 0; f < 4; ++f) s_fl[f][fslot] = fl[f];
         }
@@ -245,21 +433,19 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
         for (int q = 0; q < 2; ++q) {
           const int e = q ? ed : ec;
           const int cu = e & 0xFF, cv = (e >> 8) & 0xFF, side = (e >> 16) & 3;
-          const int axs = side >> 1, plus = side & 1;
-          const int st = axs ? WS : 1;
+          const int plus = side & 1;
+          const int st = (side >> 1) ? WS : 1;
           const int ic = cv * WS + cu;
-          const int rc = fregion(X0 + cu, Y0 + cv, N);
-          const int du = axs ? 0 : 1, dv = axs ? 1 : 0;
-          const int rin = plus ? fregion(X0 + cu - du, Y0 + cv - dv, N) : fregion(X0 + cu + du, Y0 + cv + dv, N);
-          const int pos = axs ? cu : cv;
+          const unsigned long long cd = s_code[cv * W + cu];
+          const int eac = ncode(cd, side), ein = ncode(cd, side ^ 1);
 #pragma unroll
           for (int f = 0; f < 5; ++f) cc[q][f] = wf[f * WW + ic];
 #pragma unroll
           for (int f = 0; f < 4; ++f) {
             const T c0 = cc[q][f];
-            const T across = ghost(rc * 4 + side, pos, f, c0);
+            const T across = eac >= 0 ? ghost(eac, f) : c0;
             T inward = wf[f * WW + (plus ? ic - st : ic + st)];
-            if (rin != rc) inward = ghost(rc * 4 + (side ^ 1), pos, f, inward);
+            if (ein >= 0) inward = ghost(ein, f);
             fv2[q][f] = plus ? c0 + half_slope<LIM>(c0 - inward, across - c0)
                              : c0 - half_slope<LIM>(c0 - across, inward - c0);
           }
@@ -276,43 +462,28 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
       }
     }
     __syncthreads();
-    // ---- cell updates ------------------------------------------------------------
-    const bool upd = loaded & (u >= lo) & (u < hi) & (v >= lo) & (v < hi);
+    FSTAMP(3 + 2 * s);
+    // ---- cell updates: owners [0, |square_s|) -----------------------------------
+    const bool upd = loaded && tid < nr * nr;
     if (upd) {
-      const int xw = (v - L1) * (H1 + 1) + (u - L1), xe = xw + 1;
+      const int xw = (v - L1) * (H1 + 1) + (u - L1), xe_ = xw + 1;
       const int ys = NFX + (v - L1) * H1 + (u - L1), yn = ys + H1;
       T dq[4];
 #pragma unroll
-      for (int f = 0; f < 4; ++f) dq[f] = -((s_fl[f][xe] - s_fl[f][xw]) + (s_fl[f][yn] - s_fl[f][ys])) * iA;
-      int rc = 0, rw = 0, rs = 0;
-      if (edge) {
-        rc = fregion(X0 + u, Y0 + v, N);
-        rw = fregion(X0 + u - 1, Y0 + v, N);
-        rs = fregion(X0 + u, Y0 + v - 1, N);
-        if (rw < 0) rw = rc;
-        if (rs < 0) rs = rc;
-      }
-      const T Lw = s_len[xw], Le = s_len[xe], Ls = s_len[ys], Ln = s_len[yn];
-      const T* mw = &s_nrm[0][rw][u][0];
-      const T* me = &s_nrm[0][rc][u + 1][0];
-      const T* ms = &s_nrm[1][rs][v][0];
-      const T* mn = &s_nrm[1][rc][v + 1][0];
+      for (int f = 0; f < 4; ++f) dq[f] = -((s_fl[f][xe_] - s_fl[f][xw]) + (s_fl[f][yn] - s_fl[f][ys])) * iA;
       const T h = Q[0];
       const T fcor = a.omega2 * r2;
       const T cor[3] = {r1 * Q[3] - r2 * Q[2], r2 * Q[1] - r0 * Q[3], r0 * Q[2] - r1 * Q[1]};
       const T pb = T(0.5) * a.g * h * h * iA, gh = a.g * h;
-      const T gbv[3] = {gb0, gb1, gb2};
+      const T gbv[3] = {gb0, gb1, gb2}, Sv[3] = {S0, S1, S2};
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const T Sk = Le * me[k] - Lw * mw[k] + Ln * mn[k] - Ls * ms[k];
-        dq[1 + k] += -fcor * cor[k] + pb * Sk - gh * gbv[k];
-      }
+      for (int k = 0; k < 3; ++k) dq[1 + k] += -fcor * cor[k] + pb * Sv[k] - gh * gbv[k];
       const T c0 = a.a0[s], c1 = a.a1[s], c2 = a.a2[s] * a.dt;
       T o[4];
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
         T base = c1 * Q[f];
-        if (c0 != T(0)) base += c0 * X[f];
+        if (c0 != T(0)) base += c0 * s_x[f][tid];        // a0 != 0 only in stages >= 2: tid < NX2
         o[f] = c2 * dq[f] + base;
       }
       const T dd = o[1] * r0 + o[2] * r1 + o[3] * r2;
@@ -322,10 +493,11 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
       if (s + 1 < NS) put(Q);
     }
     if (s + 1 < NS) __syncthreads();
+    FSTAMP(4 + 2 * s);
   }
 
-  // ---- 4. the block's cells -> output, plus same-rank ghost pushes -----------
-  if (owner && (u >= R) & (u < R + B) & (v >= R) & (v < R + B)) {
+  // ---- 4. the block's cells (owners [0, B^2)) -> output, same-rank pushes ------
+  if (tid < B * B) {
     const unsigned S = (unsigned)a.S;
 #pragma unroll
     for (int f = 0; f < 4; ++f) *o32(a.out, (unsigned)src + f * S) = Q[f];
@@ -344,7 +516,33 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
         for (int f = 0; f < 4; ++f) *o32(a.out, (unsigned)pt[k] + f * S) = Q[f];
       }
     }
+    if constexpr (XG) {   // cells other ranks read: straight into their rings, tag xe + 2
+      constexpr int G = sizeof(T) / 4;
+      const int* xp = a.xpush + ((long)bid * B * B + (v - R) * B + (u - R)) * a.K;
+      for (int k = 0; k < a.K; ++k) {
+        const int code = xp[k];
+        if (code < 0) break;
+        gu64* dst = ((gu64*)(a.peer_ring[code >> 24])) + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring +
+                    (long)(code & 0xFFFFFF) * (4 * G);
+        const unsigned long long tag = (unsigned long long)((unsigned)xe + 2u) << 32;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          if constexpr (G == 2) {
+            const unsigned long long b = __builtin_bit_cast(unsigned long long, Q[f]);
+            __hip_atomic_store(dst + 2 * f, tag | (b & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(dst + 2 * f + 1, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          } else {
+            __hip_atomic_store(dst + f, tag | __builtin_bit_cast(unsigned, Q[f]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
+      }
+    }
   }
+  if constexpr (XG) {
+    if (tid == 0) a.epoch[bid] = xe + 1;
+  }
+  FSTAMP(3 + 2 * NS);
 }
 
 template <typename T, int NS, int B>
@@ -354,30 +552,54 @@ int launch_fused(const FusedDesc* d, hipStream_t s) {
   if (d->pw != d->n + 2 * d->mg || d->mg < 2 || d->n % B) return -3;
   FArgs<T> a;
   a.Q = (const T*)d->Q; a.out = (T*)d->out; a.cgeo = (const T*)d->cgeo; a.src = d->src; a.org = d->org;
-  a.len = (const T*)d->len; a.nrm = (const T*)d->nrm; a.gidx = d->gidx; a.gtab = d->gtab; a.gw = (const T*)d->gw;
+  a.len = (const T*)d->len; a.nrm = (const T*)d->nrm; a.code = (const unsigned long long*)d->code; a.gtab = d->gtab;
+  a.gw = (const T*)d->gw;
   a.ctab = d->ctab; a.cgf = (const T*)d->cgf; a.ccnt = d->ccnt; a.push = d->push;
   a.G = d->G; a.C = d->C; a.nblocks = d->nblocks; a.n = d->n; a.N = d->N; a.S = d->S; a.mg = d->mg; a.pw = d->pw;
   for (int k = 0; k < 4; ++k) {
     a.a0[k] = (T)d->a0[k]; a.a1[k] = (T)d->a1[k]; a.a2[k] = (T)d->a2[k];
   }
   a.dt = (T)d->dt; a.g = (T)d->g; a.omega2 = (T)d->omega2;
+  a.ring = d->ring; a.K = d->K; a.recv = (const unsigned long long*)d->recv; a.peer_ring = (T* const*)d->peer_ring;
+  a.xpush = d->xpush; a.epoch = d->epoch; a.err = d->err; a.timeout_ticks = d->timeout_ticks;
+  a.stamps = d->stamps;
+  for (int k = 0; k < 6; ++k) a.links[k] = d->links[k];
+  a.local_src = d->local_src;
+  a.mdiv_n = magic_div((unsigned)d->n, (unsigned long long)d->N + 1);
+  if (d->xg && (!STSP_XG_TAG || !d->recv || !d->peer_ring || !d->xpush || !d->epoch || !d->err || d->ring <= 0 ||
+                d->K <= 0))
+    return -6;
   const dim3 grid(d->nblocks), block(D::NT);
+#define FUSED_LAUNCH(L_)                                                                          \
+  if (d->xg) hipLaunchKernelGGL((fused_step_kernel<T, L_, NS, B, true>), grid, block, 0, s, a);   \
+  else hipLaunchKernelGGL((fused_step_kernel<T, L_, NS, B, false>), grid, block, 0, s, a);
   switch (d->limiter) {
-    case 0: hipLaunchKernelGGL((fused_step_kernel<T, 0, NS, B>), grid, block, 0, s, a); break;
-    case 1: hipLaunchKernelGGL((fused_step_kernel<T, 1, NS, B>), grid, block, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((fused_step_kernel<T, 2, NS, B>), grid, block, 0, s, a); break;
-    case 3: hipLaunchKernelGGL((fused_step_kernel<T, 3, NS, B>), grid, block, 0, s, a); break;
+    case 0: FUSED_LAUNCH(0) break;
+    case 1: FUSED_LAUNCH(1) break;
+    case 2: FUSED_LAUNCH(2) break;
+    case 3: FUSED_LAUNCH(3) break;
     default: return -4;
   }
+#undef FUSED_LAUNCH
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
+// Block sizes: 16 (C96: tiles of 48, C48, C32) and 18 (C180 at tiles_per_edge 2:
+// tiles of 90; C720: 360, 180); the window of W = B + 12 cells must fit one
+// owner thread per cell (W^2 <= 1024).
 extern "C" int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stream) {
-  if (d->B != 16 || d->ns != 3) return -1;
-  if (dtype == 1) return launch_fused<double, 3, 16>(d, stream);
-  if (dtype == 0) return launch_fused<float, 3, 16>(d, stream);
+  if (d->ns != 3) return -1;
+  if (d->B == 16) {
+    if (dtype == 1) return launch_fused<double, 3, 16>(d, stream);
+    if (dtype == 0) return launch_fused<float, 3, 16>(d, stream);
+  } else if (d->B == 18) {
+    if (dtype == 1) return launch_fused<double, 3, 18>(d, stream);
+    if (dtype == 0) return launch_fused<float, 3, 18>(d, stream);
+  } else {
+    return -1;
+  }
   return -5;
 }
 

@@ -92,12 +92,12 @@ int stsp_xg_prime_launch(int dtype, const void* q, int S, int F, const int* src,
 typedef struct FusedDesc {
   const void* Q;        // [F][S] step input, padded layout
   void* out;            // [F][S] step output: interior + same-rank ghost pushes
-  const void* cgeo;     // [S][8] per-cell record in the padded layout (1/A, centre, grad b, 0)
+  const void* cgeo;     // [S (+ ring)][12] per-cell record in the padded layout (1/A, centre, grad b, sum L m, 0, 0)
   const int* src;       // [nb][W*W] padded offset of each window cell's source, -1 = not loaded
   const int* org;       // [nb][4] X0, Y0, tile_local, xo | yo << 12 | region flags << 24
   const void* len;      // [nb][2 H1 (H1+1)] face lengths (x-faces, then y-faces)
-  const void* nrm;      // [nb][2][5][W+1][3] line normals per region
-  const short* gidx;    // [nb][20 W] ghost entry of (reader region * 4 + side, pos), -1 none
+  const void* nrm;      // [nb][2][5][3][W+1] line normals per region, component-major
+  const void* code;     // [nb][W*W] u64: 4 x int16 neighbour codes per window cell and side (-1, entry, -3)
   const int* gtab;      // [nb][G][2] LDS index of the interpolation pair
   const void* gw;       // [nb][G] interpolation weights
   const int* ctab;      // [nb][C][8] corner faces: cu | cv << 8 | side_c << 16, du | dv << 8 | side_d << 16, fslot_c, fslot_d
@@ -109,6 +109,28 @@ typedef struct FusedDesc {
   int B, ns, limiter;
   double a0[4], a1[4], a2[4];
   double dt, g, omega2;
+  // several ranks (xg = 1, ops/fused.py::FusedExchangePlan): window cells with
+  // src <= -2 are read from this rank's receive ring, slot epoch % STSP_XG_SLOTS,
+  // entry -2 - src, as tagged granules; every step stores the block's cells that
+  // peers read into their rings (xpush codes peer << 24 | entry), tag epoch + 2
+  int xg;
+  int ring;                 // 8-byte granules per ring slot
+  const void* recv;         // this rank's ring (granules)
+  void* const* peer_ring;   // [world] ring bases (IPC-mapped)
+  const int* xpush;         // [nb][B*B][K] destination codes, -1 none
+  int K;
+  int* epoch;               // [nb] steps completed
+  int* err;                 // set to 1 on a wait timeout (every later wait falls through)
+  long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
+  // nullable: [nb][16 waves][16] s_memtime of every wave at the phase boundaries
+  // (prologue, then faces / updates of each stage, end); profiling only
+  unsigned long long* stamps;
+  // one rank holding every tile in id order: the kernel computes each window
+  // cell's storage offset from the cube topology (links: per face, sides W E S
+  // N, 6 bits each: nbr face | nbr edge << 3 | reversed << 5) instead of
+  // loading `src` (one dependent memory round trip less in the prologue)
+  int local_src;
+  int links[6];
 } FusedDesc;
 int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stream);
 int stsp_fused_limits(int* gmax, int* cmax);

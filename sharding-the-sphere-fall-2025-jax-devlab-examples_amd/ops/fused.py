@@ -244,6 +244,7 @@ class FusedPlan:
         nb = self.nb
         self.org = np.zeros((nb, 4), dtype=np.int32)
         self.src = np.full((nb, W * W), -1, dtype=np.int32)
+        self.gid = np.full((nb, W * W), -1, dtype=np.int64)
         self.reg = np.full((nb, W * W), -1, dtype=np.int8)
         self.nrm = np.zeros((nb, 2, NREG, W + 1, 3))
         self.lx = np.zeros((nb, H1, H1 + 1))
@@ -277,6 +278,7 @@ class FusedPlan:
                     srcv[m] = self._source(gv[m])
                     assert (srcv[m] != -1).all()
                     self.src[bid] = srcv
+                    self.gid[bid] = gv
                     gslot = {int(x): k for k, x in enumerate(gv) if x >= 0}
                     self._block_geometry(bid, face, rg, F, I, J, maps)
                     gx, cx = self._block_stencils(bid, face, rg, F, I, J, g, gslot, maps, X0, Y0)
@@ -603,7 +605,10 @@ class FusedTorch:
     """The fused step in PyTorch, on a SWE ``Engine`` (CPU or GPU): validates the
     host tables against the stage-by-stage oracle and documents the kernel."""
 
-    def __init__(self, engine, plan: FusedPlan, coefs=None):
+    def __init__(self, engine, plan: FusedPlan, coefs=None, remote_cells: Optional[np.ndarray] = None):
+        """``remote_cells``: global ids of the receive slots (several ranks,
+        ``FusedExchangePlan.need_remote[rank]``); ``step(recv)`` then takes
+        their values, [slots, F]."""
         e = engine
         self.e = e
         self.p = plan
@@ -625,6 +630,10 @@ class FusedTorch:
         cg = torch.zeros((T, Pw, Pw, 8), dtype=dt, device=dev)
         cg[:, ng:ng + n, ng:ng + n] = tens["cgeo"]
         self.cgeo_pad = cg.view(-1, 8)
+        self.S = self.cgeo_pad.shape[0]
+        if remote_cells is not None and len(remote_cells):
+            rec = torch.as_tensor(global_cell_records(e)[remote_cells][:, :8], dtype=dt, device=dev)
+            self.cgeo_pad = torch.cat([self.cgeo_pad, rec], 0)
         self.g = float(e.physics.g)
         self.omega2 = 2.0 * float(e.physics.omega)
         self.lim = int(e.physics.limiter)
@@ -661,14 +670,19 @@ class FusedTorch:
         c = torch.sqrt(self.g * torch.clamp(h, min=0.0))
         return w, c
 
-    def step(self):
+    def step(self, recv: Optional[torch.Tensor] = None):
         e, P, d = self.e, self.p, self.d
         W, L1, H1, nb = d.W, d.L1, d.H1, P.nb
         F = 4
         Q0 = e.pool[0]
-        srcc = self.src.clamp(min=0)
+        # local cells from the padded state, remote cells (src <= -2) from recv
+        rem = self.src <= -2
+        srcc = torch.where(rem, self.S + (-2 - self.src), self.src).clamp(min=0)
         valid = self.need[:, 0]
-        q = Q0[:, srcc].view(F, nb, W, W) * valid
+        full = Q0
+        if recv is not None and recv.numel():
+            full = torch.cat([Q0, recv.t().to(Q0.dtype)], 1)
+        q = full[:, srcc].view(F, nb, W, W) * valid
         X = q.clone()
         geo = self.cgeo_pad[srcc].view(nb, W, W, 8) * valid[..., None]
         invA = geo[..., 0]
@@ -799,6 +813,7 @@ class FusedTorch:
         R, B = d.R, d.B
         own = q[:, :, R:R + B, R:R + B]
         dst = self.src.view(nb, W, W)[:, R:R + B, R:R + B]
+        assert (dst >= 0).all()
         Q1 = e.pool[1]
         Q1[:, dst.reshape(-1)] = own.reshape(F, -1)
         e.refresh_halos(Q1)
@@ -811,7 +826,18 @@ class FusedTorch:
 # Device tables + descriptors of the gfx950 kernel (fused_step.hip)
 # ---------------------------------------------------------------------------
 
-def fused_supported(engine, B: int = 16) -> Optional[str]:
+FUSED_BLOCKS = (16, 18)      # block sizes the kernel is instantiated for
+
+
+def fused_block(n: int) -> Optional[int]:
+    """Block size of the fused kernel for tiles of n x n cells (None: none fits)."""
+    for B in FUSED_BLOCKS:
+        if n % B == 0:
+            return B
+    return None
+
+
+def fused_supported(engine, B: Optional[int] = None) -> Optional[str]:
     """None if ``engine`` can take the fused step, else the reason it cannot."""
     from ..models.swe import ShallowWater
     e = engine
@@ -821,10 +847,11 @@ def fused_supported(engine, B: int = 16) -> Optional[str]:
         return "fused step: PLR limiters only (PPM runs stage by stage)"
     if e.integ.name != "ssprk3":
         return "fused step: SSP-RK3 only"
-    if e.layout.num_ranks != 1 or e.plan.num_recv or e.plan.num_send:
-        return "fused step: one rank only (multi-rank runs stage by stage)"
-    if e.plan.n % B:
-        return f"fused step: tile size {e.plan.n} is not a multiple of {B}"
+    if e.layout.loopback:
+        return "fused step: no loopback layouts"
+    B = B or fused_block(e.plan.n)
+    if B is None or e.plan.n % B:
+        return f"fused step: tile size {e.plan.n} is not a multiple of {' or '.join(map(str, FUSED_BLOCKS))}"
     if e.layout.N <= NG_PLR * 3:
         return f"fused step: C{e.layout.N} is too small for the ring"
     if e.plan.ng < NG_PLR:
@@ -834,18 +861,35 @@ def fused_supported(engine, B: int = 16) -> Optional[str]:
 
 class FusedKernel:
     """Device tables and the two ping-pong descriptors (pool[0] -> pool[1] and
-    back) of the gfx950 fused step for a one-rank SWE ``Engine`` (HIP backend).
-    Every index the kernel dereferences is checked here, on the host."""
+    back) of the gfx950 fused step for a SWE ``Engine`` (HIP backend).  Every
+    index the kernel dereferences is checked here, on the host.
 
-    def __init__(self, engine, B: int = 16):
+    Several ranks: the window cells of other ranks arrive through the direct
+    xGMI ring (``FusedExchangePlan``; an ``IpcRing`` allocation per rank, mapped
+    by its peers): each step stores the cells peers read into their rings as
+    tagged granules and reads its own remote cells from its ring, so a
+    multi-GPU step is still one launch per rank and is graph-captured like a
+    one-GPU step.  ``prime()`` delivers the current state (collective)."""
+
+    def __init__(self, engine, B: Optional[int] = None, timeout_s: float = 2.0, group=None):
         from . import native
         why = fused_supported(engine, B)
         if why:
             raise RuntimeError(why)
+        B = B or fused_block(engine.plan.n)
         e = engine
         self.e = e
+        self.group = group
         self.lib = native.require_native()
-        P = FusedPlan(e.layout, e.rank, e.grid, B=B, ns=3)
+        world = e.layout.num_ranks
+        self.world = world
+        X = None
+        if world > 1:
+            X = FusedExchangePlan(e.layout, e.grid, B, ns=3)
+            P = X.plans[e.rank]
+        else:
+            P = FusedPlan(e.layout, e.rank, e.grid, B=B, ns=3)
+            P.src[~P.need[:, 0]] = -1          # load only what the step reads
         self.plan = P
         d = P.d
         W, WS, nb = d.W, d.W + 1, P.nb
@@ -855,17 +899,19 @@ class FusedKernel:
         if G > gmax or C > cmax:
             raise RuntimeError(f"fused step: {G} ghost entries / {C} corner faces exceed the kernel's {gmax} / {cmax}")
         S = e.plan.S
+        nring = X.ring_slots if X is not None else 0
         # ---- host-side contract checks ----------------------------------------
-        assert P.src.shape == (nb, W * W) and int(P.src.max()) < S and int(P.src.min()) >= -1
+        assert P.src.shape == (nb, W * W) and int(P.src.max()) < S and int(P.src.min()) >= -2 - (nring - 1)
+        assert (P.src[P.need[:, 0]] != -1).all()
         nfl = 2 * d.nfx
-        ld = lambda s: (s // W) * WS + s % W
+        ld = lambda s_: (s_ // W) * WS + s_ % W
         for b in range(nb):
             k = int(P.gcnt[b])
             assert (P.gtab[b, :k, 2:4] >= 0).all() and (P.gtab[b, :k, 2:4] < W * W).all()
             for j in range(int(P.ccnt[b])):
                 assert -1 <= P.ctab[b, j, 4] < nfl and -1 <= P.ctab[b, j, 5] < nfl
-        gi = P.gidx.astype(np.int16)
         assert int(P.gidx.max()) < G
+        code = neighbour_codes(P)
         gpair = np.zeros((nb, G, 2), dtype=np.int32)
         gpair[..., 0] = ld(P.gtab[..., 2])
         gpair[..., 1] = ld(P.gtab[..., 3])
@@ -882,26 +928,74 @@ class FusedKernel:
             flags = sum(1 << r for r in regs)
             li, rem = divmod(b, P.nbx * P.nby)
             yb, xb = divmod(rem, P.nbx)
-            org[b, 3] = (xb * B) | ((yb * B) << 12) | (flags << 24)
-        src = P.src.copy()
-        src[~P.need[:, 0]] = -1          # load only what the step reads
+            face = e.layout.tile_origin(e.plan.tiles[li])[0]
+            org[b, 3] = np.int32(np.uint32((xb * B) | ((yb * B) << 12) | (flags << 24) | (face << 29)).view(np.int32))
+        # cell records [S (+ ring)][12] in the padded layout: 1/A, centre, grad b,
+        # curvature sum S = sum(L m) over the cell's faces, 0, 0
+        rec_g = global_cell_records(e)
         T_, n, ng = e.plan.T, e.plan.n, e.plan.ng
         pw = n + 2 * ng
-        cg = torch.zeros((T_, pw, pw, 8), dtype=dt, device=dev)
-        cg[:, ng:ng + n, ng:ng + n] = e.tens["cgeo"]
+        cgn = np.zeros((T_, pw, pw, 12))
+        L_ = e.layout
+        jj, ii = np.mgrid[0:n, 0:n]
+        for li, tid in enumerate(e.plan.tiles):
+            f, I0, J0 = L_.tile_origin(tid)
+            cgn[li, ng:ng + n, ng:ng + n] = rec_g[L_.global_flat(f, I0 + ii, J0 + jj)]
+        cgn = cgn.reshape(-1, 12)
+        if X is not None:       # records of the remote cells, in ring-slot order
+            cgn = np.concatenate([cgn, rec_g[X.need_remote[e.rank]]], 0)
+        cg = torch.as_tensor(cgn, dtype=dt, device=dev)
         t = lambda a, ty=dt: torch.as_tensor(np.ascontiguousarray(a), dtype=ty, device=dev)
         self.tens = {
-            "cgeo": cg.reshape(-1, 8).contiguous(),
-            "src": t(src, torch.int32), "org": t(org, torch.int32),
+            "cgeo": cg.contiguous(),
+            "src": t(P.src, torch.int32), "org": t(org, torch.int32),
             "len": t(np.concatenate([P.lx.reshape(nb, -1), P.ly.reshape(nb, -1)], 1)),
-            "nrm": t(P.nrm), "gidx": t(gi, torch.int16), "gtab": t(gpair, torch.int32), "gw": t(P.gt),
+            "nrm": t(np.ascontiguousarray(np.moveaxis(P.nrm, -1, -2))),      # [nb,2,5,3,W+1]
+            "code": t(code.view(np.int64), torch.int64), "gtab": t(gpair, torch.int32), "gw": t(P.gt),
             "ctab": t(ct, torch.int32), "cgf": t(P.cgeo), "ccnt": t(P.ccnt, torch.int32),
             "push": torch.as_tensor(e.plan.push_map, dtype=torch.int32, device=dev).contiguous(),
         }
         assert self.tens["len"].shape == (nb, nfl)
         assert int(e.plan.push_map.max(initial=-1)) < S
         self.dcode = native.dtype_code(dt)
+        self.mem = None
+        if X is not None:
+            self._setup_exchange(X, timeout_s)
         self.descs = [self._desc(0, 1), self._desc(1, 0)]
+        if X is not None:
+            self.prime()
+
+    def _setup_exchange(self, X, timeout_s: float) -> None:
+        from .xgmi import IpcRing, _declare
+        e = self.e
+        L = _declare(self.lib)
+        if int(L.stsp_xg_protocol()) != 1:
+            raise RuntimeError("fused multi-rank step needs the tagged-granule protocol (STSP_XG_TAG=1)")
+        self._xlib = L
+        self.slots = int(L.stsp_xg_slots())
+        esize = torch.tensor([], dtype=e.dtype).element_size()
+        F = e.physics.F
+        self.ring = X.ring_slots * F * (esize // 4)
+        xpush, psrc, pcode = X.producer(e.rank)
+        assert psrc.size == 0 or int(psrc.max()) < e.plan.S
+        peers = sorted(set(int(c) >> XG_SLOT_BITS for c in pcode.tolist())
+                       | set(int(x) for x in np.unique(np.asarray(e.layout.owner)[
+                           e.layout.locate(X.need_remote[e.rank])[0]]).tolist()))
+        self.mem = IpcRing(L, e.device, self.world, e.rank, peers, self.slots * self.ring * 8, self.group)
+        pr = np.zeros(32, dtype=np.int64)
+        for p, b in self.mem.bases.items():
+            pr[p] = b
+        dev = e.device
+        self.tens.update({
+            "peer_ring": torch.as_tensor(pr, device=dev),
+            "xpush": torch.as_tensor(xpush, dtype=torch.int32, device=dev).contiguous(),
+            "epoch": torch.zeros(self.plan.nb, dtype=torch.int32, device=dev),
+            "err": torch.zeros(4, dtype=torch.int32, device=dev),
+            "prime_src": torch.as_tensor(psrc, dtype=torch.int32, device=dev),
+            "prime_code": torch.as_tensor(pcode, dtype=torch.int32, device=dev),
+        })
+        self.K = int(xpush.shape[2])
+        self.timeout_ticks = int(timeout_s * 1e8)
 
     def _desc(self, qi: int, oi: int):
         from . import native
@@ -909,7 +1003,7 @@ class FusedKernel:
         p = native.ptr
         d = native.FusedDesc()
         d.Q, d.out = p(e.pool[qi]), p(e.pool[oi])
-        for k in ("cgeo", "src", "org", "len", "nrm", "gidx", "gtab", "gw", "ctab", "cgf", "ccnt", "push"):
+        for k in ("cgeo", "src", "org", "len", "nrm", "code", "gtab", "gw", "ctab", "cgf", "ccnt", "push"):
             setattr(d, k, p(tn[k]))
         d.G, d.C = P.gtab.shape[1], P.ctab.shape[1]
         d.nblocks, d.n, d.N, d.S = P.nb, e.plan.n, e.layout.N, e.plan.S
@@ -920,7 +1014,59 @@ class FusedKernel:
         d.dt = e.dt
         d.g = float(e.physics.g)
         d.omega2 = 2.0 * float(e.physics.omega)
+        # one rank with every tile in id order: window sources computed in the kernel
+        d.local_src = 1 if (self.world == 1 and list(e.plan.tiles) == list(range(e.layout.num_tiles))) else 0
+        for f in range(6):
+            d.links[f] = face_links(f)
+        if self.mem is not None:
+            d.xg = 1
+            d.ring = self.ring
+            d.recv = self.mem.base
+            d.peer_ring = p(tn["peer_ring"])
+            d.xpush = p(tn["xpush"])
+            d.K = self.K
+            d.epoch = p(tn["epoch"])
+            d.err = p(tn["err"])
+            d.timeout_ticks = self.timeout_ticks
         return d
+
+    # ---- several ranks: delivery of the current state, error check ----------
+    def prime(self) -> None:
+        """Deliver the cells peers read of the current state (pool[0]) into
+        their ring slot for the next step.  Collective: all ranks, quiescent."""
+        if self.mem is None:
+            return
+        import torch.distributed as dist
+        from . import native
+        from .xgmi import agree
+        e = self.e
+        torch.cuda.synchronize(e.device)
+        ep = self.tens["epoch"]
+        e0 = int(ep[0].item())
+        if not bool((ep == e0).all()):
+            raise RuntimeError("fused xGMI epochs diverged across blocks")
+        dist_on = self.mem.distributed
+        if dist_on:
+            dist.barrier(group=self.group)      # nobody still reads the slot we are about to fill
+        tn = self.tens
+        rc = self._xlib.stsp_xg_prime_launch(self.dcode, native.ptr(e.pool[0]), e.plan.S, e.physics.F,
+                                             native.ptr(tn["prime_src"]), native.ptr(tn["prime_code"]),
+                                             int(tn["prime_src"].numel()), native.ptr(tn["peer_ring"]), self.ring,
+                                             e0, native.current_stream_handle())
+        torch.cuda.synchronize(e.device)
+        if not agree(rc == 0, dist_on, e.device, self.group):
+            raise RuntimeError(f"fused xGMI prime failed ({rc})")
+        if dist_on:
+            dist.barrier(group=self.group)
+
+    def check(self) -> None:
+        if self.mem is not None and int(self.tens["err"][0].item()) != 0:
+            raise RuntimeError("fused step: a peer's window cells did not arrive in time (poll timeout)")
+
+    def close(self) -> None:
+        if self.mem is not None:
+            self.mem.close()
+            self.mem = None
 
     def set_dt(self, dt: float) -> None:
         for d in self.descs:
@@ -945,8 +1091,165 @@ class FusedKernel:
             e.step_count += 1
 
 
+def face_links(face: int) -> int:
+    """Cube-edge links of a face for the kernel's window_src: sides W E S N,
+    6 bits each: neighbour face | its edge (0 W, 1 E, 2 S, 3 N) << 3 |
+    reversed << 5 (parallel/topology.py LINKS)."""
+    from ..parallel.topology import LINKS
+    code = 0
+    for k, ed in enumerate("WESN"):
+        lk = LINKS[(face, ed)]
+        c = lk.nbr_face | ("WESN".index(lk.nbr_edge) << 3) | (int(lk.reversed) << 5)
+        code |= c << (6 * k)
+    return code
+
+
+def global_cell_records(engine) -> np.ndarray:
+    """[6 N N, 12] cell records of every cell of the grid, indexed by global
+    flat id: 1/A, centre (3), grad b (3), the curvature sum S = sum(L m) over
+    the cell's four faces with outward normals (3; the kernel's curvature
+    balance is g h^2 / 2 * S / A, models/swe.py), 0, 0."""
+    e = engine
+    key = ("global_rec12", e.layout.N, e.physics.name, getattr(e.physics, "case", None))
+    cache = getattr(e.grid, "_cache", {})
+    if key in cache:
+        return cache[key]
+    from ..models.base import RankGeometry
+    L1 = TileLayout(e.layout.N, e.layout.t, 1, ng=e.layout.ng)
+    geo = RankGeometry(e.grid, L1, 0)
+    rec = e.physics.setup(geo, torch.float64, "cpu")["cgeo"].numpy()          # [T, n, n, 8]
+    g = e.grid
+    lx, ly, mx, my = g.x_edge_lengths(), g.y_edge_lengths(), g.x_edge_normals(), g.y_edge_normals()
+    Sv = (lx[:, :, 1:, None] * mx[:, None, 1:, :] - lx[:, :, :-1, None] * mx[:, None, :-1, :]
+          + ly[:, 1:, :, None] * my[:, 1:, None, :] - ly[:, :-1, :, None] * my[:, :-1, None, :])   # [6,N,N,3]
+    out = np.zeros((6 * L1.N * L1.N, 12))
+    n = L1.n
+    for li, tid in enumerate(L1.rank_tiles[0]):
+        f, I0, J0 = L1.tile_origin(tid)
+        jj, ii = np.mgrid[0:n, 0:n]
+        gid = L1.global_flat(f, I0 + ii, J0 + jj).reshape(-1)
+        out[gid, :7] = rec[li].reshape(-1, 8)[:, :7]
+        out[gid, 7:10] = Sv[f, J0:J0 + n, I0:I0 + n].reshape(-1, 3)
+    cache[key] = out
+    return out
+
+
+def neighbour_codes(P: "FusedPlan") -> np.ndarray:
+    """[nb, W*W] uint64: per window cell four int16 codes (sides -x, +x, -y,
+    +y): -1 = read the window neighbour (same region), >= 0 = ghost entry
+    (the neighbour in the cell's own frame is the interpolation pair of that
+    entry), -3 = no cell here (beyond a cube corner)."""
+    W = P.d.W
+    nb = P.nb
+    reg = P.reg.reshape(nb, W, W).astype(np.int64)
+    codes = np.full((nb, 4, W, W), -1, dtype=np.int64)
+    vv, uu = np.mgrid[0:W, 0:W]
+    for side in range(4):
+        du, dv = SIDE_VEC[side]
+        u2, v2 = uu + du, vv + dv
+        inside = (u2 >= 0) & (u2 < W) & (v2 >= 0) & (v2 < W)
+        pos = vv if side < 2 else uu
+        for b in range(nb):
+            r = reg[b]
+            r2 = np.full((W, W), -2)
+            r2[inside] = r[v2[inside], u2[inside]]
+            diff = (r >= 0) & (r2 != r)
+            strip = np.clip(r, 0, None) * 4 + side
+            e = P.gidx[b, strip, pos]
+            codes[b, side] = np.where(diff & (e >= 0), e, -1)
+    codes[np.broadcast_to((reg < 0)[:, None], codes.shape)] = -3
+    c16 = (codes & 0xFFFF).astype(np.uint64)
+    out = c16[:, 0] | (c16[:, 1] << np.uint64(16)) | (c16[:, 2] << np.uint64(32)) | (c16[:, 3] << np.uint64(48))
+    return out.reshape(nb, W * W)
+
+
 def ctypes_limits(L) -> Tuple[int, int]:
     import ctypes
     g, c = ctypes.c_int(0), ctypes.c_int(0)
     L.stsp_fused_limits(ctypes.byref(g), ctypes.byref(c))
     return g.value, c.value
+
+
+# ---------------------------------------------------------------------------
+# Several ranks: remote window cells through the direct xGMI ring
+# ---------------------------------------------------------------------------
+
+XG_SLOT_BITS = 24
+
+
+class FusedExchangePlan:
+    """Which window cells of the fused step live on other ranks, and who
+    stores them where (host side, numpy; tested on CPU).
+
+    Every rank builds every rank's ``FusedPlan`` (each covers only that rank's
+    blocks), so all ranks derive the same enumeration with no messages:
+
+    * consumer p: the remote cells its blocks need (``need[0]``), ordered by
+      owner rank then global id, are the slots of its receive ring; window cells
+      read them as ``src = -2 - slot``;
+    * producer r: for each of its cells needed by p, the code
+      ``p << 24 | slot``; the fused kernel stores the cell's new value there at
+      the end of every step (tagged granules), ``xpush[block][own cell][k]``.
+    """
+
+    def __init__(self, layout: TileLayout, grid, B: int, ns: int = 3):
+        L = layout
+        world = L.num_ranks
+        owner = np.asarray(L.owner)
+        self.world = world
+
+        def source_for(p):
+            def src(g):
+                tid, _, _ = L.locate(g)
+                loc = L.local_flat(g)
+                return np.where(owner[tid] == p, loc, -2)
+            return src
+
+        self.plans = [FusedPlan(L, p, grid, B=B, ns=ns, source=source_for(p)) for p in range(world)]
+        self.need_remote: List[np.ndarray] = []
+        for p, P in enumerate(self.plans):
+            m = P.need[:, 0] & (P.src == -2)
+            g = np.unique(P.gid[m])
+            tid, _, _ = L.locate(g)
+            order = np.lexsort((g, owner[tid]))
+            self.need_remote.append(g[order])
+        self.ring_slots = max(1, max(len(x) for x in self.need_remote))
+        if self.ring_slots >= (1 << XG_SLOT_BITS):
+            raise ValueError("receive ring too large for the push encoding")
+        for p, P in enumerate(self.plans):
+            slot = {int(x): k for k, x in enumerate(self.need_remote[p])}
+            rem = P.src == -2
+            idx = np.nonzero(rem)
+            P.src[idx] = [-2 - slot[int(x)] if int(x) in slot else -1 for x in P.gid[idx]]
+            # window cells nobody reads stay unloaded
+            P.src[~P.need[:, 0]] = -1
+
+    def producer(self, rank: int):
+        """(xpush [nb, B*B, K] int32, prime_src [M], prime_code [M]) for ``rank``."""
+        L = self.layout = self.plans[rank].layout
+        P = self.plans[rank]
+        B, n = P.B, P.n
+        owner = np.asarray(L.owner)
+        ent: Dict[int, List[int]] = {}
+        psrc, pcode = [], []
+        for p in range(self.world):
+            if p == rank:
+                continue
+            g = self.need_remote[p]
+            tid, i, j = L.locate(g)
+            mine = owner[tid] == rank
+            for k in np.nonzero(mine)[0]:
+                li = int(L._local_arr[tid[k]])
+                x, y = int(i[k]), int(j[k])
+                bid = (li * P.nby + y // B) * P.nbx + x // B
+                own = (y % B) * B + x % B
+                code = (p << XG_SLOT_BITS) | int(k)
+                ent.setdefault(bid * B * B + own, []).append(code)
+                psrc.append(int(L.local_flat(np.array([g[k]]))[0]))
+                pcode.append(code)
+        K = max(1, max((len(v) for v in ent.values()), default=1))
+        xpush = np.full((P.nb, B * B, K), -1, dtype=np.int64)
+        for key, codes in ent.items():
+            b, o = divmod(key, B * B)
+            xpush[b, o, :len(codes)] = codes
+        return (xpush.astype(np.int32), np.asarray(psrc, dtype=np.int32), np.asarray(pcode, dtype=np.int32))

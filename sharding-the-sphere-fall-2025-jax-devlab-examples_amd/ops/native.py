@@ -47,7 +47,7 @@ class FusedDesc(ctypes.Structure):
     """Mirror of FusedDesc (stsp_kernels.h): one fused SSP-RK3 step."""
     _fields_ = [
         ("Q", ctypes.c_void_p), ("out", ctypes.c_void_p), ("cgeo", ctypes.c_void_p), ("src", ctypes.c_void_p),
-        ("org", ctypes.c_void_p), ("len", ctypes.c_void_p), ("nrm", ctypes.c_void_p), ("gidx", ctypes.c_void_p),
+        ("org", ctypes.c_void_p), ("len", ctypes.c_void_p), ("nrm", ctypes.c_void_p), ("code", ctypes.c_void_p),
         ("gtab", ctypes.c_void_p), ("gw", ctypes.c_void_p), ("ctab", ctypes.c_void_p), ("cgf", ctypes.c_void_p),
         ("ccnt", ctypes.c_void_p), ("push", ctypes.c_void_p),
         ("G", ctypes.c_int), ("C", ctypes.c_int),
@@ -56,6 +56,10 @@ class FusedDesc(ctypes.Structure):
         ("limiter", ctypes.c_int),
         ("a0", ctypes.c_double * 4), ("a1", ctypes.c_double * 4), ("a2", ctypes.c_double * 4),
         ("dt", ctypes.c_double), ("g", ctypes.c_double), ("omega2", ctypes.c_double),
+        ("xg", ctypes.c_int), ("ring", ctypes.c_int), ("recv", ctypes.c_void_p), ("peer_ring", ctypes.c_void_p),
+        ("xpush", ctypes.c_void_p), ("K", ctypes.c_int), ("epoch", ctypes.c_void_p), ("err", ctypes.c_void_p),
+        ("timeout_ticks", ctypes.c_longlong), ("stamps", ctypes.c_void_p),
+        ("local_src", ctypes.c_int), ("links", ctypes.c_int * 6),
     ]
 
 

@@ -130,6 +130,11 @@ class NativeStepper:
         plan = e.plan
         self.remote = plan.num_recv > 0 or plan.num_send > 0
         self.xgmi = xgmi
+        self.fused = fused
+        if fused is not None:
+            if xgmi is not None:
+                raise RuntimeError("the fused step carries its own exchange")
+            self.remote = False      # remote window cells arrive inside the fused kernel
         if xgmi is not None:
             self.remote = False      # the exchange lives inside the stage kernels
         if self.remote and not nccl_comm:
@@ -144,9 +149,7 @@ class NativeStepper:
         # fused: ops/fused.py::FusedKernel, one launch per step (temporal
         # blocking), ping-pong between pool[0] and pool[1]: the op list covers
         # two steps
-        self.fused = fused
-        if fused is not None and (self.remote or xgmi is not None):
-            raise RuntimeError("the fused step runs on one rank only")
+
         period = 2 if fused is not None else e.integ.period
         self.period = period
         ops: List[StspOp] = []
@@ -254,6 +257,8 @@ class NativeStepper:
     def check(self) -> None:
         if self.xgmi is not None:
             self.xgmi.check()
+        if self.fused is not None:
+            self.fused.check()
 
     def _run_native(self, nsteps: int) -> None:
         """Eager op list on self.stream, ordered after and before torch's
@@ -287,6 +292,8 @@ class NativeStepper:
         torch.cuda.synchronize(self.e.device)
         if self.xgmi is not None:
             self.xgmi.prime()          # re-deliver the remote ghosts of the restored state (collective)
+        if self.fused is not None:
+            self.fused.prime()         # the same for the fused step's remote window cells
 
     def _graph(self, periods: int, copy: int = 0):
         """hipGraph of exactly ``periods`` integrator periods (recorded once,

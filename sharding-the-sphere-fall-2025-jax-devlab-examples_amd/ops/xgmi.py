@@ -187,7 +187,6 @@ class XgmiHalo:
     def __init__(self, engine, group=None, timeout_s: float = 2.0):
         from . import native
         from .hip_compute import HipCompute
-        import torch.distributed as dist
         e = engine
         if not isinstance(e.compute, HipCompute):
             raise RuntimeError("XgmiHalo needs an Engine with backend='hip'")
@@ -212,50 +211,11 @@ class XgmiHalo:
             self.ring = self.xp.ring_slots * F
             nbytes = CNT_BYTES + self.slots * self.ring * self.esize
         self.base = None
-        self.opened: List[int] = []
         peers = sorted(set(self.xp.plan.send_peers) | set(self.xp.plan.recv_peers))
-        bases = {self.rank: 0}
-        distributed = dist.is_available() and dist.is_initialized() and world > 1
-        if not distributed and any(p != self.rank for p in peers):
-            raise RuntimeError("remote peers but no initialised torch.distributed group to exchange IPC handles")
-        # Every step that can fail on one rank is followed by an all-ranks
-        # agreement, so all ranks leave through the same collective sequence
-        # (a rank that raised between collectives left its peers
-        # inside a different one).
-        err = None
-        hb = L.stsp_ipc_handle_bytes()
-        h = (ctypes.c_char * hb)()
-        try:
-            base = ctypes.c_void_p()
-            rc = L.stsp_xg_alloc(ctypes.c_size_t(nbytes), ctypes.byref(base))
-            if rc != 0:
-                raise RuntimeError(f"uncached allocation for the xGMI ring failed ({rc})")
-            self.base = base.value
-            bases[self.rank] = self.base
-            if distributed:
-                L.stsp_enable_peers(dev.index if dev.index is not None else torch.cuda.current_device())
-                rc = L.stsp_ipc_get(ctypes.c_void_p(self.base), h)
-                if rc != 0:
-                    raise RuntimeError(f"hipIpcGetMemHandle failed ({rc})")
-        except RuntimeError as exc:
-            err = exc
-        self._agreed(err, distributed)
-        if distributed:
-            allh = [None] * world
-            dist.all_gather_object(allh, bytes(h), group=group)
-            try:
-                for p in peers:
-                    if p == self.rank:
-                        continue
-                    ptr = ctypes.c_void_p()
-                    rc = L.stsp_ipc_open((ctypes.c_char * hb).from_buffer_copy(allh[p]), ctypes.byref(ptr))
-                    if rc != 0:
-                        raise RuntimeError(f"hipIpcOpenMemHandle of rank {p} failed ({rc})")
-                    self.opened.append(ptr.value)
-                    bases[p] = ptr.value
-            except RuntimeError as exc:
-                err = exc
-            self._agreed(err, distributed)
+        self.mem = IpcRing(L, dev, world, self.rank, peers, nbytes, group)
+        self.base = self.mem.base
+        bases = self.mem.bases
+        distributed = self.mem.distributed
         pr = np.zeros(MAX_WORLD, dtype=np.int64)
         pc = np.zeros(MAX_WORLD, dtype=np.int64)
         for p, b in bases.items():
@@ -279,14 +239,7 @@ class XgmiHalo:
     def _agreed(self, err, distributed: bool) -> None:
         """All-ranks agreement after a local step that may have failed: every
         rank raises (after releasing what it holds) if any rank failed."""
-        ok = err is None
-        if distributed:
-            import torch.distributed as dist
-            dev = self.e.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
-            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
-            ok = bool(t.item())
-        if not ok:
+        if not agree(err is None, distributed, self.e.device, self.group):
             self.close()
             raise err if err is not None else RuntimeError("xGMI setup failed on another rank")
 
@@ -352,20 +305,97 @@ class XgmiHalo:
             raise RuntimeError("direct xGMI halo: a peer's ghosts did not arrive in time (poll timeout)")
 
     def close(self) -> None:
-        L = self._lib
-        for p in self.opened:
-            L.stsp_ipc_close(ctypes.c_void_p(p))
-        self.opened = []
-        if getattr(self, "base", None):
-            torch.cuda.synchronize(self.e.device)
-            L.stsp_xg_free(ctypes.c_void_p(self.base))
-            self.base = None
+        if getattr(self, "mem", None) is not None:
+            self.mem.close()
+        self.base = None
 
     def __del__(self):
         try:
             self.close()
         except Exception:
             pass
+
+
+def agree(ok: bool, distributed: bool, device, group=None) -> bool:
+    """All-ranks AND of a local success flag (True without a process group)."""
+    if not distributed:
+        return ok
+    import torch.distributed as dist
+    dev = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
+class IpcRing:
+    """One uncached device allocation per rank, mapped by every peer through a
+    dmabuf IPC handle exchanged over torch.distributed (``bases[p]``: rank p's
+    allocation as seen from this process).  Every local step that can fail is
+    followed by an all-ranks agreement, so all ranks raise together (after
+    releasing what they hold) instead of leaving peers inside another
+    collective."""
+
+    def __init__(self, L, device, world: int, rank: int, peers, nbytes: int, group=None):
+        import torch.distributed as dist
+        self._lib = L
+        self.device = device
+        self.group = group
+        self.base = None
+        self.opened: List[int] = []
+        self.bases = {rank: 0}
+        distributed = dist.is_available() and dist.is_initialized() and world > 1
+        self.distributed = distributed
+        if not distributed and any(p != rank for p in peers):
+            raise RuntimeError("remote peers but no initialised torch.distributed group to exchange IPC handles")
+        err = None
+        hb = L.stsp_ipc_handle_bytes()
+        h = (ctypes.c_char * hb)()
+        try:
+            base = ctypes.c_void_p()
+            rc = L.stsp_xg_alloc(ctypes.c_size_t(nbytes), ctypes.byref(base))
+            if rc != 0:
+                raise RuntimeError(f"uncached allocation for the xGMI ring failed ({rc})")
+            self.base = base.value
+            self.bases[rank] = self.base
+            if distributed:
+                L.stsp_enable_peers(device.index if device.index is not None else torch.cuda.current_device())
+                rc = L.stsp_ipc_get(ctypes.c_void_p(self.base), h)
+                if rc != 0:
+                    raise RuntimeError(f"hipIpcGetMemHandle failed ({rc})")
+        except RuntimeError as exc:
+            err = exc
+        self._agreed(err)
+        if distributed:
+            allh = [None] * world
+            dist.all_gather_object(allh, bytes(h), group=group)
+            try:
+                for p in peers:
+                    if p == rank:
+                        continue
+                    ptr = ctypes.c_void_p()
+                    rc = L.stsp_ipc_open((ctypes.c_char * hb).from_buffer_copy(allh[p]), ctypes.byref(ptr))
+                    if rc != 0:
+                        raise RuntimeError(f"hipIpcOpenMemHandle of rank {p} failed ({rc})")
+                    self.opened.append(ptr.value)
+                    self.bases[p] = ptr.value
+            except RuntimeError as exc:
+                err = exc
+            self._agreed(err)
+
+    def _agreed(self, err) -> None:
+        if not agree(err is None, self.distributed, self.device, self.group):
+            self.close()
+            raise err if err is not None else RuntimeError("xGMI setup failed on another rank")
+
+    def close(self) -> None:
+        L = self._lib
+        for p in self.opened:
+            L.stsp_ipc_close(ctypes.c_void_p(p))
+        self.opened = []
+        if self.base:
+            torch.cuda.synchronize(self.device)
+            L.stsp_xg_free(ctypes.c_void_p(self.base))
+            self.base = None
 
 
 def _declare(L):

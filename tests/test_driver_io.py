@@ -193,6 +193,10 @@ def test_geometry_and_initial_condition_zarr_stages(tmp_path):
     assert np.array_equal(s3.gather_global()[0], ic[0] * 1.01)
     with pytest.raises(ValueError):
         S.Solver(dict(_cfg(tmp_path / "d", **io), grid={"N": 12}), verbose=False).initialize()
+    # same fields and grid, another SWE case (TC5 has topography): refused
+    with pytest.raises(ValueError, match="case"):
+        S.Solver(dict(_cfg(tmp_path / "e", **io), physics={"model": "swe", "case": "tc5"}),
+                 verbose=False).initialize()
 
 
 def test_plot_cli_products(tmp_path):

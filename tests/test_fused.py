@@ -28,6 +28,7 @@ def _relerr(a_eng, b_eng):
     (24, 2, 4, "tc5", 2),     # two tiles per panel edge, tile-clipped interpolation
     (12, 1, 4, "tc2", 1),     # windows that cross both opposite panel edges
     (24, 1, 8, "tc6", 3),
+    (36, 2, 18, "tc5", 2),    # the B = 18 kernel shape (C180 / C720 tiles)
 ])
 def test_fused_torch_matches_stage_oracle(N, t, B, case, lim):
     grid = CubedSphereGrid(N)
@@ -75,8 +76,9 @@ def test_fused_supported_reasons():
     assert "PLR" in fused_supported(e)
     e = Engine(ShallowWater("tc5"), L, integrator="rk4")
     assert "SSP-RK3" in fused_supported(e)
-    e = Engine(ShallowWater("tc5"), L)
-    assert "multiple of 16" in fused_supported(e)
+    e = Engine(ShallowWater("tc5"), TileLayout(20, 1, 1, ng=2))
+    assert "multiple of 16 or 18" in fused_supported(e)
+    assert fused_supported(Engine(ShallowWater("tc5"), TileLayout(36, 2, 1, ng=2))) is None   # B = 18
     e = Engine(ShallowWater("tc5"), TileLayout(32, 2, 1, ng=2))
     assert fused_supported(e) is None
 
@@ -95,7 +97,8 @@ def _gpu_pair(N, t, dtype=torch.float64, case="tc5", lim=2):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,t,case,lim", [(32, 2, "tc5", 2), (48, 1, "tc5", 1), (96, 2, "tc5", 2),
-                                          (48, 3, "tc6", 3), (32, 1, "tc2", 0)])
+                                          (48, 3, "tc6", 3), (32, 1, "tc2", 0), (36, 2, "tc5", 2),
+                                          (54, 1, "tc2", 1)])
 def test_fused_kernel_fp64_matches_oracle(N, t, case, lim):
     from stsphere.ops.fused import FusedKernel
     ref, hip = _gpu_pair(N, t, case=case, lim=lim)
@@ -171,3 +174,72 @@ def test_fused_native_graph_equals_eager(nsteps):
     assert b.step_count == nsteps
     assert r.stats["graph_steps"] == (nsteps // 2) * 2
     r.close()
+
+
+@pytest.mark.parametrize("N,t,R", [(32, 2, 2), (32, 2, 8), (48, 1, 6), (32, 2, 3)])
+def test_fused_exchange_ranks_equal_one_rank(N, t, R):
+    """Several ranks (FusedExchangePlan): each rank's window reads its remote
+    cells from a receive buffer filled in the slot order of the plan; every
+    rank steps with the PyTorch rendering of the kernel.  The assembled state
+    equals the one-rank fused step bit for bit, and every producer entry
+    delivers exactly the cell its consumer slot names."""
+    from stsphere.engine import assemble_global
+    from stsphere.ops.fused import FusedExchangePlan, XG_SLOT_BITS
+    grid = CubedSphereGrid(N)
+    L1 = TileLayout(N, t, 1, ng=2)
+    one = Engine(ShallowWater("tc5"), L1, grid=grid)
+    f1 = FusedTorch(one, FusedPlan(L1, 0, grid, B=16))
+    L = TileLayout(N, t, R, ng=2)
+    X = FusedExchangePlan(L, grid, 16)
+    engs = [Engine(ShallowWater("tc5"), L, r, grid=grid, dt=one.dt) for r in range(R)]
+    fts = [FusedTorch(engs[r], X.plans[r], remote_cells=X.need_remote[r]) for r in range(R)]
+    for r in range(R):        # producer codes deliver the consumer's slot cells
+        xpush, psrc, pcode = X.producer(r)
+        for s_, c in zip(psrc.tolist(), pcode.tolist()):
+            p, slot = c >> XG_SLOT_BITS, c & ((1 << XG_SLOT_BITS) - 1)
+            assert int(L.local_flat(X.need_remote[p][slot:slot + 1])[0]) == s_
+    for _ in range(2):
+        f1.step()
+        states = [e.pool[0] for e in engs]
+        recvs = []
+        for r in range(R):
+            g = X.need_remote[r]
+            tid, _, _ = L.locate(g)
+            own = np.asarray(L.owner)[tid]
+            off = L.local_flat(g)
+            rv = torch.stack([states[int(o)][:, int(k)] for o, k in zip(own, off)]) if len(g) else None
+            recvs.append(rv)
+        for r in range(R):
+            fts[r].step(recvs[r])
+    a = np.stack([one.global_field(f) for f in range(4)])
+    b = np.stack([assemble_global(L, {e.rank: e.tiles_view()[f].numpy() for e in engs}) for f in range(4)])
+    assert np.array_equal(a, b)
+
+
+def test_kernel_tables_cpu():
+    """Host tables the gfx950 kernel reads, checked on CPU: the neighbour
+    codes name every ghost entry of the block exactly where the PyTorch
+    rendering substitutes, cells beyond a cube corner are -3; the cell record's
+    curvature sum S reproduces the oracle's curvature balance (models/swe.py)."""
+    from stsphere.ops.fused import global_cell_records, neighbour_codes
+    N = 32
+    L = TileLayout(N, 2, 1, ng=2)
+    grid = CubedSphereGrid(N)
+    e = Engine(ShallowWater("tc5"), L, grid=grid)
+    P = FusedPlan(L, 0, grid, B=16)
+    ft = FusedTorch(e, P)
+    codes = neighbour_codes(P)
+    W = P.d.W
+    c = np.stack([((codes >> np.uint64(16 * k)) & np.uint64(0xFFFF)).astype(np.int64) for k in range(4)], 1)
+    c = np.where(c >= 0x8000, c - 0x10000, c).reshape(P.nb, 4, W, W)
+    sub = ft.sub.numpy()
+    reg = P.reg.reshape(P.nb, W, W)
+    valid = reg >= 0
+    assert (c[np.broadcast_to(~valid[:, None], c.shape)] == -3).all()
+    ok = np.broadcast_to(valid[:, None], c.shape)
+    assert np.array_equal(np.where(ok, c, -1), np.where(ok, sub, -1))
+    rec = global_cell_records(e)
+    loc = e.geo.gather_global(rec[:, 7:10].reshape(6, N, N, 3))          # [T,n,n,3]
+    sbal = e.tens["sbal"].permute(1, 2, 3, 0).numpy()                    # 0.5 g S / A
+    want = 0.5 * e.physics.g * loc / e.geo.area[..., None]
+    assert np.allclose(sbal, want, rtol=1e-12, atol=1e-12 * np.abs(want).max())

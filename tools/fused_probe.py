@@ -1,0 +1,102 @@
+#!/usr/bin/env python
+"""Fused-step probe: launch time (eager, back to back; and graph replay) and
+per-phase wave-0 stamps of every block (prologue, faces / updates of each
+stage), split into panel-edge and interior blocks.  One JSON line.
+
+    python tools/fused_probe.py --N 96 --t 2 --reps 50 --stamps
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--N", type=int, default=96)
+    ap.add_argument("--t", type=int, default=2)
+    ap.add_argument("--dtype", default="fp64")
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--stage", action="store_true", help="also time the launch-per-stage step")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    from stsphere.engine import Engine
+    from stsphere.models.geometry import CubedSphereGrid
+    from stsphere.models.swe import ShallowWater
+    from stsphere.ops.fused import FusedKernel
+    from stsphere.ops.native_runtime import NativeStepper
+    from stsphere.parallel.layout import TileLayout
+    dt = torch.float64 if a.dtype == "fp64" else torch.float32
+    L = TileLayout(a.N, a.t, 1, ng=2)
+    e = Engine(ShallowWater("tc5"), L, grid=CubedSphereGrid(a.N), dtype=dt, device="cuda", backend="hip")
+    fk = FusedKernel(e)
+    out = {"N": a.N, "t": a.t, "dtype": a.dtype, "blocks": fk.plan.nb, "B": fk.plan.B}
+    fk.step(4)
+    torch.cuda.synchronize()
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s0.record()
+    for _ in range(a.reps):
+        fk.launch(0)
+        fk.launch(1)
+    s1.record()
+    torch.cuda.synchronize()
+    out["eager_us_per_step"] = s0.elapsed_time(s1) * 1e3 / (2 * a.reps)
+    r = NativeStepper(e, use_graph=True, steps_per_graph=2 * a.reps, fused=fk)
+    r.prepare(2 * a.reps)
+    r.run(2 * a.reps)
+    torch.cuda.synchronize()
+    s0.record()
+    r.run(2 * a.reps)
+    s1.record()
+    torch.cuda.synchronize()
+    out["graph_us_per_step"] = s0.elapsed_time(s1) * 1e3 / (2 * a.reps)
+    if a.stage:
+        e2 = Engine(ShallowWater("tc5"), L, grid=CubedSphereGrid(a.N), dtype=dt, device="cuda", backend="hip")
+        r2 = NativeStepper(e2, use_graph=True, steps_per_graph=2 * a.reps)
+        r2.prepare(2 * a.reps)
+        r2.run(2 * a.reps)
+        torch.cuda.synchronize()
+        s0.record()
+        r2.run(2 * a.reps)
+        s1.record()
+        torch.cuda.synchronize()
+        out["stage_graph_us_per_step"] = s0.elapsed_time(s1) * 1e3 / (2 * a.reps)
+    if a.stamps:
+        nb = fk.plan.nb
+        st = torch.zeros((nb, 16, 16), dtype=torch.int64, device="cuda")
+        for d in fk.descs:
+            d.stamps = st.data_ptr()
+        for _ in range(3):
+            fk.launch(0)
+        torch.cuda.synchronize()
+        v = st.cpu().numpy().astype(np.int64)
+        for d in fk.descs:
+            d.stamps = 0
+        # stamps [block][wave][phase]: phase time of a block = its last wave's stamp
+        nw = 16
+        v = v.reshape(nb, nw, 16)
+        t0 = v[:, :, 0].min(1)
+        rel = v - t0[:, None, None]
+        blk = rel.max(1)                    # [nb, phase]: slowest wave of each block
+        edge = np.array([((int(x) >> 24) & 0x1E) != 0 for x in fk.plan.org[:, 3]])
+        names = ["start", "window_put", "window_bar"] + sum(
+            [[f"s{s}_faces", f"s{s}_upd"] for s in range(1, 4)], []) + ["end"]
+        ph = {}
+        for k, nm in enumerate(names):
+            ph[nm] = {"edge_mean": float(blk[edge, k].mean()) if edge.any() else None,
+                      "int_mean": float(blk[~edge, k].mean()) if (~edge).any() else None,
+                      "max": float(blk[:, k].max())}
+        out["phases_cycles"] = ph
+        out["start_spread"] = float(t0.max() - t0.min())
+        out["end_max"] = float((v[:, :, 9].max(1) - t0.min()).max())
+        out["edge_blocks"] = int(edge.sum())
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
