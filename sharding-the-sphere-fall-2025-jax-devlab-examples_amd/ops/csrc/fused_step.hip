@@ -41,6 +41,8 @@
 // corner list's.
 #include "stage_common.h"
 
+#include <type_traits>
+
 
 namespace {
 
@@ -49,14 +51,16 @@ struct FD {
   static constexpr int R = 2 * NS;
   static constexpr int W = B + 2 * R;
   static constexpr int WS = W + 1;                 // LDS row stride of the window
-  static constexpr int WW = W * WS;                // LDS field stride
+  static constexpr int GMAX = 160;                 // ghost entries per block (C96 corner blocks: 88)
+  static constexpr int GB = W * WS;                // LDS index of ghost entry 0 (after the window)
+  static constexpr int WW = GB + GMAX;             // LDS field stride: window, then ghost values
   static constexpr int L1 = R - 2 * (NS - 1);
   static constexpr int H1 = B + 4 * (NS - 1);
   static constexpr int NFX = H1 * (H1 + 1);
   static constexpr int NFL = 2 * NFX;
   static constexpr int NT = 1024;
   static_assert(W * W <= NT, "one owner thread per window cell");
-  static constexpr int GMAX = 256;
+  static_assert(GMAX <= NT, "one fix-up thread per ghost entry");
   static constexpr int CMAX = 32;
 };
 
@@ -113,11 +117,16 @@ template <typename T>
 struct FArgs {
   const T* Q;
   T* out;
-  const T* cgeo;
   const int* src;
   const int* org;
-  const T* len;
-  const T* nrm;
+  const int* rmap;        // [nb][5][8] per region: panel, I0, J0, m00, m01, m10, m11, 0 (window -> panel index)
+  const T* tanc;          // [N] tan of the cell-centre angles
+  const T* tane;          // [N+1] tan of the grid-line angles
+  const T* ainv;          // [N*N] 1/A by panel-local index (the same on every panel)
+  const T* sloc;          // [N*N][4] curvature sum S = sum(L m) in panel-local components (e_i, e_j, n), 0
+  const T* lxt;           // [N][N+1] x-edge lengths by panel-local index (y-edges: transposed)
+  const T* gbt;           // [S (+ ring)][4] grad b per cell in the padded layout, or null (no topography)
+  int frames[6];          // per panel: e_i, e_j, n as axis (2 bits each) and sign bits 6, 7, 8
   const unsigned long long* code;
   const int* gtab;
   const T* gw;
@@ -185,6 +194,23 @@ __device__ __forceinline__ int window_src(int f, int X, int Y, int N, int n, int
   return (tid * pw + (J - tj * n) + mg) * pw + (I - ti * n) + mg;
 }
 
+// panel-local components (along e_i, e_j, n) -> Cartesian, for a panel whose
+// frame vectors are signed coordinate axes (FACE_FRAMES, parallel/topology.py)
+template <typename T>
+__device__ __forceinline__ void to_global(int fr, T xi, T xj, T xn, T& o0, T& o1, T& o2) {
+  const int ai = fr & 3, aj = (fr >> 2) & 3;
+  if (fr & 64) xi = -xi;
+  if (fr & 128) xj = -xj;
+  if (fr & 256) xn = -xn;
+  o0 = ai == 0 ? xi : (aj == 0 ? xj : xn);
+  o1 = ai == 1 ? xi : (aj == 1 ? xj : xn);
+  o2 = ai == 2 ? xi : (aj == 2 ? xj : xn);
+}
+
+__device__ __forceinline__ int sel5(int r, int v0, int v1, int v2, int v3, int v4) {
+  return r == 0 ? v0 : r == 1 ? v1 : r == 2 ? v2 : r == 3 ? v3 : v4;
+}
+
 // neighbour code of a window cell on one side (-1 window neighbour, >= 0 ghost
 // entry, -3 no cell)
 __device__ __forceinline__ int ncode(unsigned long long c, int side) {
@@ -194,10 +220,12 @@ __device__ __forceinline__ int ncode(unsigned long long c, int side) {
 template <typename T, int LIM, int NS, int B, bool XG>
 __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   using D = FD<NS, B>;
-  constexpr int W = D::W, WS = D::WS, WW = D::WW, R = D::R, L1 = D::L1, H1 = D::H1;
+  constexpr int W = D::W, WS = D::WS, WW = D::WW, GB = D::GB, R = D::R, L1 = D::L1, H1 = D::H1;
   constexpr int NFX = D::NFX, NFL = D::NFL, NT = D::NT;
   constexpr int NN = 2 * 5 * 3 * (W + 1);
-  __shared__ T s_w[5][W][WS];              // primitives h, vx, vy, vz and sound speed
+  // primitives h, vx, vy, vz and sound speed of the window cells, then (fields
+  // 0-3) the values of the block's ghost entries, refreshed before each stage's faces
+  __shared__ T s_w[5 * WW];
   __shared__ T s_fl[4][NFL];               // face fluxes (stage-1 face set, compact)
   __shared__ T s_len[NFL];                 // face lengths
   __shared__ T s_nrm[2][5][3][W + 1];      // line normals per region, component-major
@@ -218,36 +246,53 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   const int X0 = og[0], Y0 = og[1], tile = og[2], ow = og[3];
   const int xo = ow & 0xFFF, yo = (ow >> 12) & 0xFFF, flags = (ow >> 24) & 0x1F;   // face: bits 29..31
   const bool edge = (flags & 0x1E) != 0;                 // a side region is present (block-uniform)
-  const T* wf = &s_w[0][0][0];
+  const T* wf = &s_w[0];
   FSTAMP(0);
 
   // ---- 0. prologue: every global load first, then the LDS writes --------------
+  // Per block only the state is unique data: the geometry comes from
+  // panel-independent tables (1/A, curvature sum, edge lengths, line tangents,
+  // L2-resident) through each region's window -> panel index map, and the cell
+  // centre is computed (gnomonic point of the cell-centre angles).
+  // region maps: block-uniform scalars (named, not an array: a per-lane pick
+  // from an array would be a dynamic index into scratch)
+  const int* rmb = a.rmap + bid * 40;
+#define RM_LOAD(k)                                                                             \
+  const int rm0_##k = __builtin_amdgcn_readfirstlane(rmb[k]),                                  \
+            rm1_##k = __builtin_amdgcn_readfirstlane(rmb[8 + k]),                              \
+            rm2_##k = __builtin_amdgcn_readfirstlane(rmb[16 + k]),                             \
+            rm3_##k = __builtin_amdgcn_readfirstlane(rmb[24 + k]),                             \
+            rm4_##k = __builtin_amdgcn_readfirstlane(rmb[32 + k]);
+  RM_LOAD(0) RM_LOAD(1) RM_LOAD(2) RM_LOAD(3) RM_LOAD(4) RM_LOAD(5) RM_LOAD(6)
+#undef RM_LOAD
+#define pick(r_, k) sel5((r_), rm0_##k, rm1_##k, rm2_##k, rm3_##k, rm4_##k)
   int u = -1, v = -1;
   const bool owner = tid < W * W;
   if (owner) owner_cell<NS, B>(tid, u, v);
   const int wi = v * WS + u;                             // this owner's LDS window index
   int xe = 0;                                            // steps this block has completed (XG)
   if constexpr (XG) xe = a.epoch[bid];
+  const int n = a.n;
+  // own cell: region, panel and panel-local index
+  int rc = owner ? fregion(X0 + u, Y0 + v, N) : -1;
+  int cg_ = 0, cI = 0, cJ = 0;
+  if (rc >= 0) {
+    cg_ = pick(rc, 0);
+    cI = pick(rc, 1) + pick(rc, 3) * u + pick(rc, 4) * v;
+    cJ = pick(rc, 2) + pick(rc, 5) * u + pick(rc, 6) * v;
+  }
   int src = -1;
-  if (owner) {
-    if (a.local_src)    // computed: no dependent table load in front of the window load
-      src = window_src((int)((unsigned)ow >> 29), X0 + u, Y0 + v, N, a.n, a.pw, a.mg, a.mdiv_n, a.links);
-    else
+  if (rc >= 0) {
+    if (a.local_src) {  // computed: no dependent table load in front of the window load
+      const int t = N / n;
+      const int ti = a.mdiv_n ? (int)__umulhi((unsigned)cI, a.mdiv_n) : cI / n;
+      const int tj = a.mdiv_n ? (int)__umulhi((unsigned)cJ, a.mdiv_n) : cJ / n;
+      src = (((cg_ * t + tj) * t + ti) * a.pw + (cJ - tj * n) + a.mg) * a.pw + (cI - ti * n) + a.mg;
+    } else {
       src = a.src[(long)bid * W * W + v * W + u];
+    }
   }
-  // tables into registers
-  constexpr int LPT = (NFL + NT - 1) / NT;
-  T lnv[LPT];
-#pragma unroll
-  for (int k = 0; k < LPT; ++k) {
-    const int j = tid + k * NT;
-    lnv[k] = j < NFL ? a.len[(long)bid * NFL + j] : T(0);
-  }
-  T nrv = T(0);
-  const int nr_reg = (tid / (3 * (W + 1))) % 5;
-  const bool nr_ld = tid < NN && (nr_reg == 0 || ((flags >> nr_reg) & 1));
-  static_assert(NN <= NT, "one normal component per thread");
-  if (nr_ld) nrv = a.nrm[(long)bid * NN + tid];
+  // edge / corner tables into registers
   unsigned long long cdv = 0;
   int gs0 = 0, gs1 = 0;
   T gtv = T(0);
@@ -269,7 +314,49 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
       for (int k = 0; k < 4; ++k) { ct4[k] = ct[k]; cg4[k] = cg[k]; }
     }
   }
-  // own window cell: state (+ record for the cells stage 1 updates)
+  // face lengths of the stage-1 face set: region of the face's lower cell (else
+  // upper), its panel-local edge through the region map, the shared length table
+  constexpr int LPT = (NFL + NT - 1) / NT;
+  T lnv[LPT];
+#pragma unroll
+  for (int k = 0; k < LPT; ++k) {
+    const int j = tid + k * NT;
+    lnv[k] = T(0);
+    if (j < NFL) {
+      const bool yf = j >= NFX;
+      const int jj = yf ? j - NFX : j;
+      const int r = yf ? jj / H1 : jj / (H1 + 1), c = yf ? jj - r * H1 : jj - r * (H1 + 1);
+      const int au = yf ? L1 + c : L1 + c - 1, av = yf ? L1 + r - 1 : L1 + r;   // lower cell
+      int rf = fregion(X0 + au, Y0 + av, N);
+      if (rf < 0) rf = fregion(X0 + au + (yf ? 0 : 1), Y0 + av + (yf ? 1 : 0), N);
+      if (rf >= 0) {
+        const int Ia = pick(rf, 1) + pick(rf, 3) * au + pick(rf, 4) * av;
+        const int Ja = pick(rf, 2) + pick(rf, 5) * au + pick(rf, 6) * av;
+        const int di = yf ? pick(rf, 4) : pick(rf, 3), dj = yf ? pick(rf, 6) : pick(rf, 5);
+        const int li = di != 0 ? Ja * (N + 1) + Ia + (di > 0) : Ia * (N + 1) + Ja + (dj > 0);
+        lnv[k] = a.lxt[li];
+      }
+    }
+  }
+  // line normals of the regions present: thread (axis, region, line) < 2 * 5 * (W + 1)
+  T nrm3[3] = {T(0), T(0), T(0)};
+  const int n_ax = tid / (5 * (W + 1)), n_r = (tid / (W + 1)) % 5, n_k = tid % (W + 1);
+  const bool n_do = tid < 2 * 5 * (W + 1) && (n_r == 0 || ((flags >> n_r) & 1));
+  T n_t = T(0);
+  int n_sign = 0, n_isj = 0;
+  if (n_do) {
+    // the line between window cells k-1 and k along the axis, as a panel line
+    const int au = n_ax ? 0 : n_k - 1, av = n_ax ? n_k - 1 : 0;
+    const int Ia = pick(n_r, 1) + pick(n_r, 3) * au + pick(n_r, 4) * av;
+    const int Ja = pick(n_r, 2) + pick(n_r, 5) * au + pick(n_r, 6) * av;
+    const int di = n_ax ? pick(n_r, 4) : pick(n_r, 3), dj = n_ax ? pick(n_r, 6) : pick(n_r, 5);
+    n_isj = di == 0;
+    n_sign = di != 0 ? di : dj;
+    int line = di != 0 ? Ia + (di > 0) : Ja + (dj > 0);
+    line = line < 0 ? 0 : (line > N ? N : line);       // lines outside the region are never read
+    n_t = a.tane[line];
+  }
+  // own window cell: state (+ geometry for the cells stage 1 updates)
   T Q[4];
   T iA = T(0), r0 = T(0), r1 = T(0), r2 = T(0), gb0 = T(0), gb1 = T(0), gb2 = T(0), S0 = T(0), S1 = T(0),
     S2 = T(0);
@@ -314,19 +401,21 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
     for (int f = 0; f < 4; ++f) Q[f] = T(0);
   }
   if (loaded && in1) {
-    // record: 1/A, centre (3), grad b (3), curvature sum S = sum(L m) (3), 0, 0;
-    // remote cells' records follow the S local ones
-    const unsigned ci = src >= 0 ? (unsigned)src : (unsigned)(a.S + (-2 - src));
-    T rec[12];
-    const T* rp = o32(a.cgeo, ci * 12u);
-    T r8[8];
-    load_rec8<T>(rp, r8);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) rec[k] = r8[k];
-    rec[8] = rp[8]; rec[9] = rp[9];
-    iA = rec[0]; r0 = rec[1]; r1 = rec[2]; r2 = rec[3];
-    gb0 = rec[4]; gb1 = rec[5]; gb2 = rec[6];
-    S0 = rec[7]; S1 = rec[8]; S2 = rec[9];
+    const int pi = cJ * N + cI;
+    iA = a.ainv[pi];
+    const T* sp = a.sloc + (long)pi * 4;
+    const T sx = sp[0], sy = sp[1], sz = sp[2];
+    const T ti = a.tanc[cI], tj = a.tanc[cJ];
+    if (a.gbt) {
+      const unsigned ci = src >= 0 ? (unsigned)src : (unsigned)(a.S + (-2 - src));
+      const T* gp = a.gbt + (long)ci * 4;
+      gb0 = gp[0]; gb1 = gp[1]; gb2 = gp[2];
+    }
+    const int fr = a.frames[cg_];
+    to_global(fr, sx, sy, sz, S0, S1, S2);
+    // cell centre: the gnomonic point n + tan(alpha) e_i + tan(beta) e_j, normalised
+    const T rn = trcp(tsqrt(T(1) + ti * ti + tj * tj));
+    to_global(fr, ti * rn, tj * rn, rn, r0, r1, r2);
   }
   if (tid < NX2) {
 #pragma unroll
@@ -338,7 +427,14 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
     const int j = tid + k * NT;
     if (j < NFL) s_len[j] = lnv[k];
   }
-  if (nr_ld) (&s_nrm[0][0][0][0])[tid] = nrv;
+  if (n_do) {
+    // unit normal of the panel line: (e - t n) / sqrt(1 + t^2), e = e_i (x-line) or
+    // e_j (y-line), oriented along the window axis
+    const T rn = T(n_sign) * trcp(tsqrt(T(1) + n_t * n_t));
+    to_global(a.frames[pick(n_r, 0)], n_isj ? T(0) : rn, n_isj ? rn : T(0), -n_t * rn, nrm3[0], nrm3[1], nrm3[2]);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) s_nrm[n_ax][n_r][c][n_k] = nrm3[c];
+  }
   if (edge) {
     if (owner) s_code[v * W + u] = cdv;
     if (tid < a.G) { s_gs[tid][0] = (short)gs0; s_gs[tid][1] = (short)gs1; s_gt[tid] = gtv; }
@@ -349,7 +445,7 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   }
   auto put = [&](const T (&q)[4]) {
     const T inv = q[0] != T(0) ? trcp(q[0]) : T(0);
-    T* p = &s_w[0][0][0] + wi;
+    T* p = &s_w[0] + wi;
     p[0] = q[0];
     p[WW] = q[1] * inv;
     p[2 * WW] = q[2] * inv;
@@ -361,69 +457,83 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   __syncthreads();
   FSTAMP(2);
 
-  // value of field f of ghost entry e (Putman-Lin interpolation, current window)
-  auto ghost = [&](int e, int f) -> T {
-    const T x0 = wf[f * WW + s_gs[e][0]], x1 = wf[f * WW + s_gs[e][1]];
-    return x0 + s_gt[e] * (x1 - x0);
-  };
-
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int lo = R - 2 * (NS - 1 - s), hi = W - lo;
     const int nr = hi - lo, nl = nr + 1, nx = nr * nl;
     const int ntask = 2 * nx + ncor;
+    // ---- ghost entries of this stage's input (edge blocks) ----------------------
+    // the Putman-Lin interpolation of the neighbour panel's edge cells onto each
+    // reader's grid line, one entry per thread; faces then read it like a cell
+    if (edge) {
+      if (tid < a.G) {
+        const int i0 = s_gs[tid][0], i1 = s_gs[tid][1];
+        const T t = s_gt[tid];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const T x0 = wf[f * WW + i0], x1 = wf[f * WW + i1];
+          s_w[f * WW + GB + tid] = x0 + t * (x1 - x0);
+        }
+      }
+      __syncthreads();
+    }
     // ---- faces ---------------------------------------------------------------
+    // EDGE: stencil neighbours come from the codes (window cell or ghost entry)
+    auto face_task = [&](int task, auto edge_c) {
+      constexpr bool EDGE = decltype(edge_c)::value;
+      const bool ax = task >= nx;                            // false: x-face, true: y-face
+      const int t2 = ax ? task - nx : task;
+      int fu, fv, k, fslot, st;
+      if (!ax) {
+        const int r = t2 / nl, c = t2 - r * nl;
+        fv = lo + r; k = lo + c; fu = k;                     // b = (k, fv), a = (k - 1, fv)
+        fslot = (fv - L1) * (H1 + 1) + (k - L1);
+        st = 1;
+      } else {
+        const int r = t2 / nr, c = t2 - r * nr;
+        k = lo + r; fu = lo + c; fv = k;                     // b = (fu, k), a = (fu, k - 1)
+        fslot = NFX + (k - L1) * H1 + (fu - L1);
+        st = WS;
+      }
+      const int ib = fv * WS + fu, ia = ib - st;
+      int iam = ia - st, iap = ib, ibm = ia, ibp = ib + st, ra = 0;
+      if constexpr (EDGE) {
+        const int sm = ax ? 2 : 0;                           // side index of -axis; +axis = sm + 1
+        const int ci = fv * W + fu, cj = ci - (ax ? W : 1);  // window indices of b and a
+        const unsigned long long ca = s_code[cj], cb = s_code[ci];
+        const int eam = ncode(ca, sm), eap = ncode(ca, sm + 1);
+        const int ebm = ncode(cb, sm), ebp = ncode(cb, sm + 1);
+        if (eam == -3 || ebm == -3) return;                  // a cell is missing: a corner face
+        if (eam >= 0) iam = GB + eam;
+        if (eap >= 0) iap = GB + eap;
+        if (ebm >= 0) ibm = GB + ebm;
+        if (ebp >= 0) ibp = GB + ebp;
+        ra = fregion(X0 + fu - (ax ? 0 : 1), Y0 + fv - (ax ? 1 : 0), N);
+      }
+      T wl[4], wr[4], cl[5], cr[5];
+#pragma unroll
+      for (int f = 0; f < 5; ++f) { cl[f] = wf[f * WW + ia]; cr[f] = wf[f * WW + ib]; }
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const T am = wf[f * WW + iam], bp = wf[f * WW + ibp];
+        T ap = cr[f], bm = cl[f];
+        if constexpr (EDGE) {
+          ap = wf[f * WW + iap];
+          bm = wf[f * WW + ibm];
+        }
+        wl[f] = cl[f] + half_slope<LIM>(cl[f] - am, ap - cl[f]);
+        wr[f] = cr[f] - half_slope<LIM>(cr[f] - bm, bp - cr[f]);
+      }
+      const T* m = &s_nrm[ax ? 1 : 0][ra][0][k];
+      T fl[4];
+      swe_flux<T>(wl, wr, cl, cr, m[0], m[W + 1], m[2 * (W + 1)], s_len[fslot], a.g, fl);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) s_fl[f][fslot] = fl[f];
+    };
     for (int task = tid; task < ntask; task += NT) {
       if (task < 2 * nx) {
-        const bool ax = task >= nx;                          // false: x-face, true: y-face
-        const int t2 = ax ? task - nx : task;
-        int fu, fv, k, fslot, st;
-        if (!ax) {
-          const int r = t2 / nl, c = t2 - r * nl;
-          fv = lo + r; k = lo + c; fu = k;                   // b = (k, fv), a = (k - 1, fv)
-          fslot = (fv - L1) * (H1 + 1) + (k - L1);
-          st = 1;
-        } else {
-          const int r = t2 / nr, c = t2 - r * nr;
-          k = lo + r; fu = lo + c; fv = k;                   // b = (fu, k), a = (fu, k - 1)
-          fslot = NFX + (k - L1) * H1 + (fu - L1);
-          st = WS;
-        }
-        const int ib = fv * WS + fu, ia = ib - st;
-        const int sm = ax ? 2 : 0;                           // side index of -axis; +axis = sm + 1
-        int eam = -1, eap = -1, ebm = -1, ebp = -1, ra = 0;
-        bool ok = true;
-        if (edge) {
-          const int ci = fv * W + fu, cj = ci - (ax ? W : 1);   // window indices of b and a
-          const unsigned long long ca = s_code[cj], cb = s_code[ci];
-          eam = ncode(ca, sm); eap = ncode(ca, sm + 1);
-          ebm = ncode(cb, sm); ebp = ncode(cb, sm + 1);
-          ok = eam != -3 && ebm != -3;                         // both cells exist
-          ra = fregion(X0 + fu - (ax ? 0 : 1), Y0 + fv - (ax ? 1 : 0), N);
-        }
-        if (ok) {
-          T wl[4], wr[4], cl[5], cr[5];
-#pragma unroll
-          for (int f = 0; f < 5; ++f) { cl[f] = wf[f * WW + ia]; cr[f] = wf[f * WW + ib]; }
-#pragma unroll
-          for (int f = 0; f < 4; ++f) {
-            T am = wf[f * WW + ia - st], bp = wf[f * WW + ib + st];
-            T ap = cr[f], bm = cl[f];
-            if (edge) {
-              if (eam >= 0) am = ghost(eam, f);
-              if (eap >= 0) ap = ghost(eap, f);
-              if (ebm >= 0) bm = ghost(ebm, f);
-              if (ebp >= 0) bp = ghost(ebp, f);
-            }
-            wl[f] = cl[f] + half_slope<LIM>(cl[f] - am, ap - cl[f]);
-            wr[f] = cr[f] - half_slope<LIM>(cr[f] - bm, bp - cr[f]);
-          }
-          const T* m = &s_nrm[ax ? 1 : 0][ra][0][k];
-          T fl[4];
-          swe_flux<T>(wl, wr, cl, cr, m[0], m[W + 1], m[2 * (W + 1)], s_len[fslot], a.g, fl);
-#pragma unroll
-          for (int f = 0; f < 4; ++f) s_fl[f][fslot] = fl[f];
-        }
+        if (edge) face_task(task, std::true_type{});
+        else face_task(task, std::false_type{});
       } else {
         // cube-corner face j: cell c's face on side_c meets cell d's face on side_d
         const int j = task - 2 * nx;
@@ -438,14 +548,14 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
           const int ic = cv * WS + cu;
           const unsigned long long cd = s_code[cv * W + cu];
           const int eac = ncode(cd, side), ein = ncode(cd, side ^ 1);
+          const int iac = eac >= 0 ? GB + eac : ic;
+          const int iin = ein >= 0 ? GB + ein : (plus ? ic - st : ic + st);
 #pragma unroll
           for (int f = 0; f < 5; ++f) cc[q][f] = wf[f * WW + ic];
 #pragma unroll
           for (int f = 0; f < 4; ++f) {
             const T c0 = cc[q][f];
-            const T across = eac >= 0 ? ghost(eac, f) : c0;
-            T inward = wf[f * WW + (plus ? ic - st : ic + st)];
-            if (ein >= 0) inward = ghost(ein, f);
+            const T across = wf[f * WW + iac], inward = wf[f * WW + iin];
             fv2[q][f] = plus ? c0 + half_slope<LIM>(c0 - inward, across - c0)
                              : c0 - half_slope<LIM>(c0 - across, inward - c0);
           }
@@ -545,14 +655,20 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   FSTAMP(3 + 2 * NS);
 }
 
+#undef pick
+
 template <typename T, int NS, int B>
 int launch_fused(const FusedDesc* d, hipStream_t s) {
   using D = FD<NS, B>;
   if (d->G > D::GMAX || d->C > D::CMAX || d->nblocks <= 0) return -2;
   if (d->pw != d->n + 2 * d->mg || d->mg < 2 || d->n % B) return -3;
   FArgs<T> a;
-  a.Q = (const T*)d->Q; a.out = (T*)d->out; a.cgeo = (const T*)d->cgeo; a.src = d->src; a.org = d->org;
-  a.len = (const T*)d->len; a.nrm = (const T*)d->nrm; a.code = (const unsigned long long*)d->code; a.gtab = d->gtab;
+  a.Q = (const T*)d->Q; a.out = (T*)d->out; a.src = d->src; a.org = d->org;
+  a.rmap = d->rmap; a.tanc = (const T*)d->tanc; a.tane = (const T*)d->tane; a.ainv = (const T*)d->ainv;
+  a.sloc = (const T*)d->sloc; a.lxt = (const T*)d->lxt; a.gbt = (const T*)d->gbt;
+  for (int k = 0; k < 6; ++k) a.frames[k] = d->frames[k];
+  if (!a.rmap || !a.tanc || !a.tane || !a.ainv || !a.sloc || !a.lxt) return -4;
+  a.code = (const unsigned long long*)d->code; a.gtab = d->gtab;
   a.gw = (const T*)d->gw;
   a.ctab = d->ctab; a.cgf = (const T*)d->cgf; a.ccnt = d->ccnt; a.push = d->push;
   a.G = d->G; a.C = d->C; a.nblocks = d->nblocks; a.n = d->n; a.N = d->N; a.S = d->S; a.mg = d->mg; a.pw = d->pw;

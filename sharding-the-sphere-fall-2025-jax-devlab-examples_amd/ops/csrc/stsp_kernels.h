@@ -92,11 +92,18 @@ int stsp_xg_prime_launch(int dtype, const void* q, int S, int F, const int* src,
 typedef struct FusedDesc {
   const void* Q;        // [F][S] step input, padded layout
   void* out;            // [F][S] step output: interior + same-rank ghost pushes
-  const void* cgeo;     // [S (+ ring)][12] per-cell record in the padded layout (1/A, centre, grad b, sum L m, 0, 0)
   const int* src;       // [nb][W*W] padded offset of each window cell's source, -1 = not loaded
-  const int* org;       // [nb][4] X0, Y0, tile_local, xo | yo << 12 | region flags << 24
-  const void* len;      // [nb][2 H1 (H1+1)] face lengths (x-faces, then y-faces)
-  const void* nrm;      // [nb][2][5][3][W+1] line normals per region, component-major
+  const int* org;       // [nb][4] X0, Y0, tile_local, xo | yo << 12 | region flags << 24 | face << 29
+  // geometry (ops/fused.py::kernel_geometry): per-block region maps and
+  // panel-independent tables, no per-cell records
+  const int* rmap;      // [nb][5][8] panel, I0, J0, m00, m01, m10, m11, 0
+  const void* tanc;     // [N]
+  const void* tane;     // [N+1]
+  const void* ainv;     // [N*N]
+  const void* sloc;     // [N*N][4]
+  const void* lxt;      // [N][N+1]
+  const void* gbt;      // [S (+ ring)][4] grad b, padded layout; null without topography
+  int frames[6];
   const void* code;     // [nb][W*W] u64: 4 x int16 neighbour codes per window cell and side (-1, entry, -3)
   const int* gtab;      // [nb][G][2] LDS index of the interpolation pair
   const void* gw;       // [nb][G] interpolation weights

@@ -72,27 +72,87 @@ def region(X, Y, N):
     return r
 
 
+def _region_point(N: int, reg: int) -> Tuple[int, int]:
+    h = N // 2
+    return {REG_P: (h, h), REG_W: (-2, h), REG_E: (N, h), REG_S: (h, -2)}.get(reg, (h, N))
+
+
 def frame_map(N: int, face: int, reg: int) -> Tuple[int, np.ndarray]:
     """(panel of region ``reg`` around ``face``, 2x2 integer matrix M) with
     M @ (du, dv) = the step in that panel's own (i, j) index frame for a step
     (du, dv) in ``face``'s extended index frame."""
-    h = N // 2
-    if reg == REG_P:
-        p = (h, h)
-    elif reg == REG_W:
-        p = (-2, h)
-    elif reg == REG_E:
-        p = (N, h)
-    elif reg == REG_S:
-        p = (h, -2)
-    else:
-        p = (h, N)
+    p = _region_point(N, reg)
     X = np.array([p[0], p[0] + 1, p[0]])
     Y = np.array([p[1], p[1], p[1] + 1])
     F, I, J = neighbor_cells(N, face, X, Y)
     assert F[0] == F[1] == F[2] >= 0
     M = np.array([[I[1] - I[0], I[2] - I[0]], [J[1] - J[0], J[2] - J[0]]], dtype=np.int64)
     return int(F[0]), M
+
+
+def region_affine(N: int, face: int, reg: int) -> Tuple[int, np.ndarray, np.ndarray]:
+    """(panel, c, M): the panel-local index of extended-panel coordinates
+    (X, Y) of region ``reg`` around ``face`` is c + M @ (X, Y) (the cube-edge
+    crossing of models/topology.py is an integer rotation / reflection)."""
+    F, M = frame_map(N, face, reg)
+    p = _region_point(N, reg)
+    _, I, J = neighbor_cells(N, face, np.array([p[0]]), np.array([p[1]]))
+    c = np.array([int(I[0]), int(J[0])], dtype=np.int64) - M @ np.array(p, dtype=np.int64)
+    return F, c, M
+
+
+def frame_code(face: int) -> int:
+    """Panel frame for the kernel's to_global: axis of e_i (bits 0-1), of e_j
+    (bits 2-3), sign bits of e_i, e_j, n (6, 7, 8); FACE_FRAMES rows are n, e_i, e_j."""
+    from ..parallel.topology import FACE_FRAMES
+    n, ei, ej = FACE_FRAMES[face]
+    ax = lambda v: int(np.argmax(np.abs(v)))
+    neg = lambda v: int(v[ax(v)] < 0)
+    assert len({ax(n), ax(ei), ax(ej)}) == 3
+    return ax(ei) | (ax(ej) << 2) | (neg(ei) << 6) | (neg(ej) << 7) | (neg(n) << 8)
+
+
+def kernel_geometry(layout: TileLayout, grid, P: "FusedPlan") -> Dict[str, np.ndarray]:
+    """Geometry the gfx950 kernel reconstructs per block instead of reading
+    per-cell records (fused_step.hip, prologue):
+
+      rmap  [nb, 5, 8] int32  per region: panel, I0, J0, m00, m01, m10, m11, 0 with
+                              panel index (I, J) = (I0, J0) + M @ (u, v) of window cell (u, v)
+      frames [6] int32        frame_code per panel
+      tanc [N], tane [N+1]    tan of the cell-centre / grid-line angles
+      ainv [N*N]              1/A by panel-local index (equal on every panel)
+      sloc [N*N, 4]           curvature sum S = sum(L m) over the cell's faces, in
+                              panel-local components (e_i, e_j, n), 0
+      lxt  [N, N+1]           x-edge lengths (j, i'); y-edge (j', i) = lxt[i, j']
+    """
+    N, B = layout.N, P.B
+    nb = P.nb
+    rmap = np.zeros((nb, NREG, 8), dtype=np.int64)
+    aff = {}
+    for b in range(nb):
+        li, rem = divmod(b, P.nbx * P.nby)
+        face = layout.tile_origin(P.tiles[li])[0]
+        X0, Y0 = int(P.org[b, 0]), int(P.org[b, 1])
+        for r in range(NREG):
+            if (face, r) not in aff:
+                aff[(face, r)] = region_affine(N, face, r)
+            F, c, M = aff[(face, r)]
+            I0, J0 = c + M @ np.array([X0, Y0])
+            rmap[b, r] = (F, I0, J0, M[0, 0], M[0, 1], M[1, 0], M[1, 1], 0)
+    lx, ly = grid.x_edge_lengths(), grid.y_edge_lengths()
+    mx, my = grid.x_edge_normals(), grid.y_edge_normals()
+    # panel 4 has the identity frame (n, e_i, e_j) = (x, y, z): local = (y, z, x)
+    f4 = 4
+    Sv = (lx[f4, :, 1:, None] * mx[f4, None, 1:, :] - lx[f4, :, :-1, None] * mx[f4, None, :-1, :]
+          + ly[f4, 1:, :, None] * my[f4, 1:, None, :] - ly[f4, :-1, :, None] * my[f4, :-1, None, :])   # [N,N,3]
+    sloc = np.zeros((N * N, 4))
+    sloc[:, 0], sloc[:, 1], sloc[:, 2] = Sv[..., 1].ravel(), Sv[..., 2].ravel(), Sv[..., 0].ravel()
+    return {
+        "rmap": rmap.astype(np.int32),
+        "frames": np.array([frame_code(f) for f in range(6)], dtype=np.int32),
+        "tanc": np.tan(grid.alpha_centers()), "tane": np.tan(grid.alpha_edges()),
+        "ainv": (1.0 / grid.areas()[0]).ravel(), "sloc": sloc, "lxt": lx[0].copy(),
+    }
 
 
 def _side_of(di: int, dj: int) -> int:
@@ -930,32 +990,38 @@ class FusedKernel:
             yb, xb = divmod(rem, P.nbx)
             face = e.layout.tile_origin(e.plan.tiles[li])[0]
             org[b, 3] = np.int32(np.uint32((xb * B) | ((yb * B) << 12) | (flags << 24) | (face << 29)).view(np.int32))
-        # cell records [S (+ ring)][12] in the padded layout: 1/A, centre, grad b,
-        # curvature sum S = sum(L m) over the cell's faces, 0, 0
-        rec_g = global_cell_records(e)
-        T_, n, ng = e.plan.T, e.plan.n, e.plan.ng
-        pw = n + 2 * ng
-        cgn = np.zeros((T_, pw, pw, 12))
-        L_ = e.layout
-        jj, ii = np.mgrid[0:n, 0:n]
-        for li, tid in enumerate(e.plan.tiles):
-            f, I0, J0 = L_.tile_origin(tid)
-            cgn[li, ng:ng + n, ng:ng + n] = rec_g[L_.global_flat(f, I0 + ii, J0 + jj)]
-        cgn = cgn.reshape(-1, 12)
-        if X is not None:       # records of the remote cells, in ring-slot order
-            cgn = np.concatenate([cgn, rec_g[X.need_remote[e.rank]]], 0)
-        cg = torch.as_tensor(cgn, dtype=dt, device=dev)
+        # geometry: shared panel tables + per-block region maps (kernel_geometry);
+        # grad b per cell [S (+ ring)][4] in the padded layout, only with topography
+        kg = kernel_geometry(e.layout, e.grid, P)
+        self.frames = [int(x) for x in kg["frames"]]
+        rm = kg["rmap"]
+        assert rm.shape == (nb, NREG, 8)
         t = lambda a, ty=dt: torch.as_tensor(np.ascontiguousarray(a), dtype=ty, device=dev)
         self.tens = {
-            "cgeo": cg.contiguous(),
+            "rmap": t(rm, torch.int32), "tanc": t(kg["tanc"]), "tane": t(kg["tane"]), "ainv": t(kg["ainv"]),
+            "sloc": t(kg["sloc"]), "lxt": t(kg["lxt"]),
             "src": t(P.src, torch.int32), "org": t(org, torch.int32),
-            "len": t(np.concatenate([P.lx.reshape(nb, -1), P.ly.reshape(nb, -1)], 1)),
-            "nrm": t(np.ascontiguousarray(np.moveaxis(P.nrm, -1, -2))),      # [nb,2,5,3,W+1]
             "code": t(code.view(np.int64), torch.int64), "gtab": t(gpair, torch.int32), "gw": t(P.gt),
             "ctab": t(ct, torch.int32), "cgf": t(P.cgeo), "ccnt": t(P.ccnt, torch.int32),
             "push": torch.as_tensor(e.plan.push_map, dtype=torch.int32, device=dev).contiguous(),
         }
-        assert self.tens["len"].shape == (nb, nfl)
+        rec_g = global_cell_records(e)
+        self.tens["gbt"] = None
+        if np.abs(rec_g[:, 4:7]).max() > 0.0:
+            T_, n, ng = e.plan.T, e.plan.n, e.plan.ng
+            pw = n + 2 * ng
+            gbn = np.zeros((T_, pw, pw, 4))
+            L_ = e.layout
+            jj, ii = np.mgrid[0:n, 0:n]
+            for li, tid in enumerate(e.plan.tiles):
+                f, I0, J0 = L_.tile_origin(tid)
+                gbn[li, ng:ng + n, ng:ng + n, :3] = rec_g[L_.global_flat(f, I0 + ii, J0 + jj), 4:7]
+            gbn = gbn.reshape(-1, 4)
+            if X is not None:       # remote cells, in ring-slot order
+                rg = np.zeros((len(X.need_remote[e.rank]), 4))
+                rg[:, :3] = rec_g[X.need_remote[e.rank], 4:7]
+                gbn = np.concatenate([gbn, rg], 0)
+            self.tens["gbt"] = t(gbn)
         assert int(e.plan.push_map.max(initial=-1)) < S
         self.dcode = native.dtype_code(dt)
         self.mem = None
@@ -1003,8 +1069,12 @@ class FusedKernel:
         p = native.ptr
         d = native.FusedDesc()
         d.Q, d.out = p(e.pool[qi]), p(e.pool[oi])
-        for k in ("cgeo", "src", "org", "len", "nrm", "code", "gtab", "gw", "ctab", "cgf", "ccnt", "push"):
+        for k in ("rmap", "tanc", "tane", "ainv", "sloc", "lxt", "src", "org", "code", "gtab", "gw", "ctab", "cgf",
+                  "ccnt", "push"):
             setattr(d, k, p(tn[k]))
+        d.gbt = p(tn["gbt"]) if tn["gbt"] is not None else 0
+        for f in range(6):
+            d.frames[f] = self.frames[f]
         d.G, d.C = P.gtab.shape[1], P.ctab.shape[1]
         d.nblocks, d.n, d.N, d.S = P.nb, e.plan.n, e.layout.N, e.plan.S
         d.mg, d.pw, d.B, d.ns = e.plan.ng, e.plan.P, P.B, P.ns

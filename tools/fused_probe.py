@@ -83,7 +83,14 @@ def main():
         t0 = v[:, :, 0].min(1)
         rel = v - t0[:, None, None]
         blk = rel.max(1)                    # [nb, phase]: slowest wave of each block
-        edge = np.array([((int(x) >> 24) & 0x1E) != 0 for x in fk.plan.org[:, 3]])
+        W = fk.plan.d.W
+        reg = fk.plan.reg.reshape(nb, W, W)
+        edge = (reg > 0).any(axis=(1, 2))
+        corner = (reg < 0).any(axis=(1, 2))
+        out["corner_blocks"] = int(corner.sum())
+        out["end_by_class"] = {"interior_max": float(blk[~edge, 9].max()) if (~edge).any() else None,
+                               "edge_max": float(blk[edge & ~corner, 9].max()) if (edge & ~corner).any() else None,
+                               "corner_max": float(blk[corner, 9].max()) if corner.any() else None}
         names = ["start", "window_put", "window_bar"] + sum(
             [[f"s{s}_faces", f"s{s}_upd"] for s in range(1, 4)], []) + ["end"]
         ph = {}
