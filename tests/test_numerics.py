@@ -177,7 +177,9 @@ def test_tc1_one_revolution_williamson_norms(alpha):
         assert nr["linf"] < 0.6 and nr["l1"] < 0.7
         errs.append(nr["l2"])
     assert errs[1] < 0.2, errs
-    assert convergence_order(errs, (24, 48)) > 1.2, errs
+    # measured orders C24 -> C48: 1.30 (alpha = 0, the bell runs along the
+    # panel edges' equator), 1.52 (alpha = pi/4)
+    assert convergence_order(errs, (24, 48)) > (1.2 if alpha == 0.0 else 1.42), errs
 
 
 def test_tc1_ppm_converges_c48_c96():
@@ -193,8 +195,66 @@ def test_tc1_ppm_converges_c48_c96():
         e.dt = 12 * DAY / n
         e.step(n)
         errs.append(williamson_norms(e.global_field(0), ph.exact(g, e.time), g.areas())["l2"])
-    assert convergence_order(errs, (48, 96)) >= 1.7, errs
+    assert convergence_order(errs, (48, 96)) >= 1.73, errs
     assert errs[1] < 0.025, errs
+
+
+def _restrict(h, A, r):
+    """Conservative restriction of a [6, N, N] cell-average field by r x r."""
+    M = h.shape[1] // r
+    hA = (h * A).reshape(6, M, r, M, r).sum((2, 4))
+    AA = A.reshape(6, M, r, M, r).sum((2, 4))
+    return hA / AA, AA
+
+
+def test_tc5_self_convergence_second_order():
+    """Williamson TC5 (flow over the mountain), 3 hours, MC-PLR + SSP-RK3 at
+    the bench's CFL: h of C24 / C48 / C96 against the C192 solution restricted
+    conservatively to each grid.  The reference holds no TC5 numbers (parity
+    unpinned), so self-convergence is the pin: order >= 1.8 from C24 to C96
+    and on the finest pair (C24 is pre-asymptotic: the mountain spans ~4
+    cells).  Measured (CPU fp64): 1.39e-3 (C24), 4.13e-4 (C48), 1.02e-4
+    (C96): orders 1.75, 2.01, overall 1.88."""
+    T = 3 * 3600.0
+    sol = {}
+    for N in (24, 48, 96, 192):
+        g = CubedSphereGrid(N)
+        e = Engine(ShallowWater("tc5"), TileLayout(N, 1, 1, ng=2), grid=g)
+        n = int(math.ceil(T / e.dt))
+        e.dt = T / n
+        e.step(n)
+        sol[N] = (e.global_field(0), g.areas())
+    href, Aref = sol[192]
+    errs = []
+    for N in (24, 48, 96):
+        hr, _ = _restrict(href, Aref, 192 // N)
+        h, A = sol[N]
+        errs.append(_l2(h, hr, A))
+    o1, o2 = math.log2(errs[0] / errs[1]), math.log2(errs[1] / errs[2])
+    assert o2 >= 1.9 and o1 >= 1.65 and (o1 + o2) / 2 >= 1.8, (errs, o1, o2)
+    assert errs[2] < 1.5e-4, errs
+
+
+def test_tc6_energy_dissipation_converges():
+    """Williamson TC6 (Rossby-Haurwitz wave 4), one day: total energy
+    (kinetic + potential, models/swe.py) only decays (Rusanov + limiter
+    dissipation), by < 5e-4 at C48, and the loss shrinks at >= 2.5 orders
+    per refinement; mass to roundoff.  Measured (CPU fp64): -2.69e-3 (C24),
+    -3.42e-4 (C48), order 2.97."""
+    drift = []
+    for N in (24, 48):
+        g = CubedSphereGrid(N)
+        e = Engine(ShallowWater("tc6"), TileLayout(N, 1, 1, ng=2), grid=g)
+        d0 = e.diagnostics()
+        n = int(math.ceil(DAY / e.dt))
+        e.dt = DAY / n
+        e.step(n)
+        d1 = e.diagnostics()
+        assert abs(d1["mass"] / d0["mass"] - 1) < 1e-12
+        drift.append(d1["energy"] / d0["energy"] - 1)
+    assert drift[0] < 0 and drift[1] < 0, drift
+    assert abs(drift[1]) < 5e-4, drift
+    assert math.log2(drift[0] / drift[1]) >= 2.5, drift
 
 
 def test_williamson_norms_definition():

@@ -94,9 +94,10 @@ def main():
         names = ["start", "window_put", "window_bar"] + sum(
             [[f"s{s}_faces", f"s{s}_upd"] for s in range(1, 4)], []) + ["end"]
         ph = {}
+        side = edge & ~corner
+        mean = lambda m, k: round(float(blk[m, k].mean()), 0) if m.any() else None
         for k, nm in enumerate(names):
-            ph[nm] = {"edge_mean": float(blk[edge, k].mean()) if edge.any() else None,
-                      "int_mean": float(blk[~edge, k].mean()) if (~edge).any() else None,
+            ph[nm] = {"int_mean": mean(~edge, k), "edge_mean": mean(side, k), "corner_mean": mean(corner, k),
                       "max": float(blk[:, k].max())}
         out["phases_cycles"] = ph
         out["start_spread"] = float(t0.max() - t0.min())
