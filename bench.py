@@ -26,7 +26,7 @@ Rank 0 prints one JSON line.  Order of events on every rank:
      timeout falls back to RCCL from a fresh state, a second mismatch aborts;
   5. barrier + synchronize, exactly K steps, synchronize + barrier; the time
      is the max over ranks; the runner's counters must show K graph-replayed
-     (or persistent) steps and no eager ones where a graph path was chosen.
+     steps and no eager ones where a graph path was chosen.
 """
 from __future__ import annotations
 
@@ -449,7 +449,6 @@ def main():
                 "comm": comm,
                 "block": list((eng.compute.bx, eng.compute.by)) if hasattr(eng.compute, "bx") else None,
                 "graph_replayed_steps": timed.get("graph_steps"),
-                "persistent_steps": timed.get("persistent_steps"),
                 "eager_steps": timed.get("eager_steps"),
             },
             "simulated_days_per_day": sdpd,

@@ -93,8 +93,8 @@ def get_integrator(name: str) -> Integrator:
 
 
 def step_kernel_compatible(integ: Integrator) -> bool:
-    """True if the persistent step kernel (ops/csrc/step_kernel.hip) can run
-    the integrator with its state in registers: period 1, no accumulator,
+    """True if a whole step can run in one kernel with the state held on
+    chip (the fused step, ops/csrc/fused_step.hip): period 1, no accumulator,
     at most 4 stages, every stage combines the step-start state (buffer 0)
     with the previous stage's output (the first stage's input is buffer 0),
     and the last stage writes buffer 0 (SSP-RK2, SSP-RK3)."""

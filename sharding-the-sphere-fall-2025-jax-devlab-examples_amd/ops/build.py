@@ -17,7 +17,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libstsp.so")
-SOURCES = ["stage_kernel.hip", "step_kernel.hip", "fused_step.hip", "tt_kernels.hip", "runtime.cpp"]
+SOURCES = ["stage_kernel.hip", "fused_step.hip", "tt_kernels.hip", "runtime.cpp"]
 HEADERS = ["stsp_kernels.h", "stage_common.h", "runtime.h"]
 ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
 # library variants: "" = production; "diag" = in-kernel phase stamps (-DSTSP_STAMPS);
@@ -28,8 +28,7 @@ VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgc": ["-DSTSP_XG_TAG=0"],
                  "unfused": ["-DSTSP_FUSE_FACES=0"], "pe0": ["-DSTSP_PE_WAVE=0"],
                  "pnotab": ["-DSTSP_PROBE_NOTAB=1"], "pnoslot": ["-DSTSP_PROBE_NOSLOT=1"],
                  "ownw0": ["-DSTSP_OWN_SKIP0=0"], "w9": ["-DSTSP_W10=0"], "swsqrt": ["-DSTSP_HW_SQRT=0"],
-                 "selslope": ["-DSTSP_SIGN_SLOPE=0"], "stepdbg": ["-DSTSP_STEP_DEBUG"], "wpe6": ["-DSTSP_WPE=6"], "wpe7": ["-DSTSP_WPE=7"],
-                 "stepdbg_bp": ["-DSTSP_STEP_DEBUG", "-DSTSP_STEP_BAND_PLAIN=1"]}
+                 "selslope": ["-DSTSP_SIGN_SLOPE=0"], "wpe6": ["-DSTSP_WPE=6"], "wpe7": ["-DSTSP_WPE=7"]}
 
 
 def lib_for(variant: str = "") -> str:

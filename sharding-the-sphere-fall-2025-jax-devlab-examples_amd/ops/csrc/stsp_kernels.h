@@ -62,24 +62,6 @@ typedef struct StageDesc {
 } StageDesc;
 
 int stsp_stage_launch(int phys, int dtype, int bx, int by, const StageDesc* d, hipStream_t stream);
-// Persistent step kernel (step_kernel.hip): nsteps whole time steps of a
-// period-1 integrator whose stages all combine the step-start state X with
-// the previous stage output (SSP-RK2 / SSP-RK3) in ONE launch; the block's
-// state stays in registers, its geometry is loaded once, and a stage boundary
-// is a granule hand-off of the halo ring between neighbouring blocks.
-typedef struct StepDesc {
-  StageDesc st;         // geometry, sizes, push map; X = Q = out = the state buffer
-  int nst;              // stages per step (<= 4)
-  int nsteps;
-  double a0[4], a1[4], a2[4];   // out = a0 X + a1 Q + a2 dt L(Q) per stage
-  void* xb;             // [2][S][F * (esize / 4)] 8-byte {tag, payload} granules
-  int* epoch;           // [nblocks] stages completed (tags only grow)
-  int* err;             // set to 1 on a hand-off timeout (every later wait falls through)
-  long long timeout_ticks;
-  long long* dbg;       // nullable: timeout diagnostics ([0] count, then 8-word records)
-} StepDesc;
-int stsp_step_launch(int phys, int dtype, int bx, int by, const StepDesc* d, hipStream_t stream);
-int stsp_step_max_blocks(int phys, int dtype, int bx, int by, int limiter);  // co-resident blocks on this device
 int stsp_pack_launch(int dtype, const void* q, int S, int F, const int* idx, int ns, void* send, hipStream_t stream);
 int stsp_copy_index_launch(int dtype, const void* src, const int* sidx, void* dst, const int* didx, int k,
                            int batch, long src_stride, long dst_stride, hipStream_t stream);

@@ -336,3 +336,13 @@ def test_kernel_geometry_reconstruction_cpu(N, t, B):
                     rn = (di if di != 0 else dj) / np.sqrt(1 + tn * tn)
                     m = _to_global(int(kg["frames"][g]), 0.0 if di == 0 else rn, rn if di == 0 else 0.0, -tn * rn)
                     assert np.allclose(m, want, atol=1e-14), (b, ax, r, k)
+
+
+def test_step_fusable_integrators():
+    """Integrators a one-kernel step can hold on chip (stages combine the
+    step-start state with the previous stage output)."""
+    from stsphere.models.integrators import get_integrator, step_kernel_compatible
+    assert step_kernel_compatible(get_integrator("ssprk3"))
+    assert step_kernel_compatible(get_integrator("ssprk2"))
+    assert not step_kernel_compatible(get_integrator("rk4"))
+    assert not step_kernel_compatible(get_integrator("euler"))

@@ -124,55 +124,3 @@ def test_rccl_loopback_full_multigpu_path(nccl_comm, use_graph, phys):
     torch.cuda.synchronize()
     assert torch.equal(ref.tiles_view(), e.tiles_view())
     ns.close()
-
-
-@pytest.mark.parametrize("N,t,block", [(32, 2, (16, 8)), (48, 2, (16, 16)), (40, 2, (16, 16))])
-def test_persistent_step_kernel_matches_launch_per_stage(N, t, block):
-    """The persistent step kernel (state in registers, granule hand-offs)
-    reproduces launch-per-stage stepping bit for bit, across several launches
-    (diffusion: the reconstructing physics need the panel-edge treatment the
-    persistent kernel does not have)."""
-    from stsphere.models.diffusion import Diffusion
-    from stsphere.ops.persistent import PersistentStepper
-    g = CubedSphereGrid(N)
-    L = TileLayout(N, t, 1, ng=2)
-    a = Engine(Diffusion(), L, grid=g, device="cuda", backend="hip", integrator="ssprk3", block=block)
-    b = Engine(Diffusion(), L, grid=g, device="cuda", backend="hip", dt=a.dt, integrator="ssprk3", block=block)
-    ps = PersistentStepper(b, timeout_s=2.0, max_steps_per_launch=7)
-    a.step(20)
-    ps.run(20)
-    torch.cuda.synchronize()
-    ps.check()
-    assert ps.stats["launches"] == 3 and b.step_count == 20
-    assert torch.equal(a.tiles_view(), b.tiles_view())
-    assert torch.equal(a.pool[0], b.pool[0])     # the ghost slots of the final state are pushed too
-
-
-def test_persistent_refuses_reconstructing_physics():
-    from stsphere.ops.persistent import PersistentStepper
-    e = Engine(ShallowWater("tc5"), TileLayout(48, 2, 1, ng=2), grid=CubedSphereGrid(48), device="cuda",
-               backend="hip")
-    with pytest.raises(NotImplementedError, match="panel-edge"):
-        PersistentStepper(e)
-
-
-def test_persistent_refuses_ppm():
-    """PPM is not supported by the persistent step kernel (PLR only)."""
-    from stsphere.ops.persistent import PersistentStepper
-    g = CubedSphereGrid(48)
-    e = Engine(ShallowWater("tc5", limiter=4), TileLayout(48, 1, 1, ng=3), grid=g, device="cuda", backend="hip")
-    with pytest.raises(NotImplementedError, match="PPM"):
-        PersistentStepper(e)
-
-
-def test_persistent_refuses_grids_that_cannot_be_co_resident():
-    """A persistent grid whose blocks cannot all be resident would deadlock:
-    the launcher refuses it up front (5-wave 16x8 blocks,
-    one guaranteed per CU; the lighter diffusion blocks fit several per CU, so
-    the grid is C384: 6912 blocks)."""
-    from stsphere.ops.persistent import PersistentStepper
-    g = CubedSphereGrid(384)
-    from stsphere.models.diffusion import Diffusion
-    e = Engine(Diffusion(), TileLayout(384, 2, 1, ng=2), grid=g, device="cuda", backend="hip", block=(16, 8))
-    with pytest.raises(RuntimeError, match="co-resident"):
-        PersistentStepper(e)

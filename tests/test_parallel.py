@@ -81,22 +81,3 @@ def test_loopback_layout_equals_single():
     single.step(3)
     lb.step(3)
     assert torch.equal(single.tiles_view(), lb.tiles_view())
-
-
-def test_step_kernel_integrators_and_read_symmetry():
-    """Host-side contract of the persistent step kernel: which integrators it
-    can run, and the symmetric block read relation its two exchange slots rely
-    on (ops/csrc/step_kernel.hip), for every block shape and several layouts."""
-    from stsphere.models.integrators import get_integrator, step_kernel_compatible
-    from stsphere.ops.persistent import STEP_SHAPES, producer_blocks, symmetric
-    from stsphere.parallel.layout import TileLayout
-    assert step_kernel_compatible(get_integrator("ssprk3"))
-    assert step_kernel_compatible(get_integrator("ssprk2"))
-    assert not step_kernel_compatible(get_integrator("rk4"))
-    assert not step_kernel_compatible(get_integrator("euler"))
-    for N, t, ng in ((48, 2, 2), (48, 1, 3), (40, 2, 2), (96, 2, 2)):
-        plan = TileLayout(N, t, 1, ng=ng).plan(0)
-        for bx, by in STEP_SHAPES:
-            nb = producer_blocks(plan, bx, by, ng)
-            assert symmetric(nb), (N, t, ng, bx, by)
-            assert (nb.max(axis=1) >= 0).all()
