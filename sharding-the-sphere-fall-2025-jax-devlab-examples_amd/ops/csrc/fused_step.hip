@@ -119,14 +119,14 @@ struct FArgs {
   T* out;
   const int* src;
   const int* org;
-  const int* rmap;        // [nb][5][8] per region: panel, I0, J0, m00, m01, m10, m11, 0 (window -> panel index)
-  const T* tanc;          // [N] tan of the cell-centre angles
+  const T* len;           // [nb][2 H1 (H1+1)] face lengths of the stage-1 face set (blocks with a side region)
+  const T* nrm;           // [nb][2][5][3][W+1] line normals per region (blocks with a side region)
   const T* tane;          // [N+1] tan of the grid-line angles
-  const T* ainv;          // [N*N] 1/A by panel-local index (the same on every panel)
-  const T* sloc;          // [N*N][4] curvature sum S = sum(L m) in panel-local components (e_i, e_j, n), 0
+  const T* crec;          // [N*N][8] by panel-local index (the same on every panel): 1/A, curvature sum
+                          // S = sum(L m) and cell centre in panel-local components (e_i, e_j, n), 0
   const T* lxt;           // [N][N+1] x-edge lengths by panel-local index (y-edges: transposed)
   const T* gbt;           // [S (+ ring)][4] grad b per cell in the padded layout, or null (no topography)
-  int frames[6];          // per panel: e_i, e_j, n as axis (2 bits each) and sign bits 6, 7, 8
+  unsigned long long frames;   // 9 bits per panel: e_i, e_j as axis (2 bits each), sign bits 6, 7, 8
   const unsigned long long* code;
   const int* gtab;
   const T* gw;
@@ -162,36 +162,30 @@ struct FArgs {
     }                                                                                            \
   } while (0)
 
-// Padded-storage offset of the cell at extended-panel coordinates (X, Y) of face
-// f, for one rank holding all 6 t^2 tiles in id order (tile = face t^2 + tj t + ti);
-// -1 beyond a cube corner.  The cube-edge crossing is models/topology.py's
+// Panel cell (g, I, J) at extended-panel coordinates (X, Y) of face f; false
+// beyond a cube corner.  The cube-edge crossing is models/topology.py's
 // neighbor_cell: across side k of face f lies face g's edge e2, positions
 // reversed or not (the reference's T / R / TR table, PY:114-139).
-__device__ __forceinline__ int window_src(int f, int X, int Y, int N, int n, int pw, int mg, unsigned md,
-                                          const int (&links)[6]) {
+__device__ __forceinline__ bool window_cell(int f, int X, int Y, int N, const int (&links)[6], int& g, int& I,
+                                            int& J) {
   const bool inx = (unsigned)X < (unsigned)N, iny = (unsigned)Y < (unsigned)N;
-  if (!inx && !iny) return -1;
-  int g = f, I = X, J = Y;
-  if (!(inx && iny)) {
-    int side, depth, pos;
-    if (X < 0) { side = 0; depth = -X; pos = Y; }
-    else if (X >= N) { side = 1; depth = X - N + 1; pos = Y; }
-    else if (Y < 0) { side = 2; depth = -Y; pos = X; }
-    else { side = 3; depth = Y - N + 1; pos = X; }
-    const int lk = (links[f] >> (6 * side)) & 63;
-    g = lk & 7;
-    const int e2 = (lk >> 3) & 3;
-    const int p2 = (lk >> 5) ? N - 1 - pos : pos;
-    if (e2 == 0) { I = depth - 1; J = p2; }
-    else if (e2 == 1) { I = N - depth; J = p2; }
-    else if (e2 == 2) { I = p2; J = depth - 1; }
-    else { I = p2; J = N - depth; }
-  }
-  const int t = N / n;
-  const int ti = md ? (int)__umulhi((unsigned)I, md) : I / n;
-  const int tj = md ? (int)__umulhi((unsigned)J, md) : J / n;
-  const int tid = (g * t + tj) * t + ti;
-  return (tid * pw + (J - tj * n) + mg) * pw + (I - ti * n) + mg;
+  g = f; I = X; J = Y;
+  if (inx && iny) return true;
+  if (!inx && !iny) return false;
+  int side, depth, pos;
+  if (X < 0) { side = 0; depth = -X; pos = Y; }
+  else if (X >= N) { side = 1; depth = X - N + 1; pos = Y; }
+  else if (Y < 0) { side = 2; depth = -Y; pos = X; }
+  else { side = 3; depth = Y - N + 1; pos = X; }
+  const int lk = (links[f] >> (6 * side)) & 63;
+  g = lk & 7;
+  const int e2 = (lk >> 3) & 3;
+  const int p2 = (lk >> 5) ? N - 1 - pos : pos;
+  if (e2 == 0) { I = depth - 1; J = p2; }
+  else if (e2 == 1) { I = N - depth; J = p2; }
+  else if (e2 == 2) { I = p2; J = depth - 1; }
+  else { I = p2; J = N - depth; }
+  return true;
 }
 
 // panel-local components (along e_i, e_j, n) -> Cartesian, for a panel whose
@@ -254,18 +248,6 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   // panel-independent tables (1/A, curvature sum, edge lengths, line tangents,
   // L2-resident) through each region's window -> panel index map, and the cell
   // centre is computed (gnomonic point of the cell-centre angles).
-  // region maps: block-uniform scalars (named, not an array: a per-lane pick
-  // from an array would be a dynamic index into scratch)
-  const int* rmb = a.rmap + bid * 40;
-#define RM_LOAD(k)                                                                             \
-  const int rm0_##k = __builtin_amdgcn_readfirstlane(rmb[k]),                                  \
-            rm1_##k = __builtin_amdgcn_readfirstlane(rmb[8 + k]),                              \
-            rm2_##k = __builtin_amdgcn_readfirstlane(rmb[16 + k]),                             \
-            rm3_##k = __builtin_amdgcn_readfirstlane(rmb[24 + k]),                             \
-            rm4_##k = __builtin_amdgcn_readfirstlane(rmb[32 + k]);
-  RM_LOAD(0) RM_LOAD(1) RM_LOAD(2) RM_LOAD(3) RM_LOAD(4) RM_LOAD(5) RM_LOAD(6)
-#undef RM_LOAD
-#define pick(r_, k) sel5((r_), rm0_##k, rm1_##k, rm2_##k, rm3_##k, rm4_##k)
   int u = -1, v = -1;
   const bool owner = tid < W * W;
   if (owner) owner_cell<NS, B>(tid, u, v);
@@ -273,16 +255,11 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   int xe = 0;                                            // steps this block has completed (XG)
   if constexpr (XG) xe = a.epoch[bid];
   const int n = a.n;
-  // own cell: region, panel and panel-local index
-  int rc = owner ? fregion(X0 + u, Y0 + v, N) : -1;
+  // own cell: panel and panel-local index (cube topology)
   int cg_ = 0, cI = 0, cJ = 0;
-  if (rc >= 0) {
-    cg_ = pick(rc, 0);
-    cI = pick(rc, 1) + pick(rc, 3) * u + pick(rc, 4) * v;
-    cJ = pick(rc, 2) + pick(rc, 5) * u + pick(rc, 6) * v;
-  }
+  const bool cvalid = owner && window_cell((int)((unsigned)ow >> 29), X0 + u, Y0 + v, N, a.links, cg_, cI, cJ);
   int src = -1;
-  if (rc >= 0) {
+  if (cvalid) {
     if (a.local_src) {  // computed: no dependent table load in front of the window load
       const int t = N / n;
       const int ti = a.mdiv_n ? (int)__umulhi((unsigned)cI, a.mdiv_n) : cI / n;
@@ -318,43 +295,30 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   // upper), its panel-local edge through the region map, the shared length table
   constexpr int LPT = (NFL + NT - 1) / NT;
   T lnv[LPT];
+  if (flags == 1) {   // one panel, identity map: x-face (row v, line k) = lx[Y0+v][X0+k], y-face transposed
 #pragma unroll
-  for (int k = 0; k < LPT; ++k) {
-    const int j = tid + k * NT;
-    lnv[k] = T(0);
-    if (j < NFL) {
+    for (int k = 0; k < LPT; ++k) {
+      const int j = tid + k * NT;
       const bool yf = j >= NFX;
       const int jj = yf ? j - NFX : j;
       const int r = yf ? jj / H1 : jj / (H1 + 1), c = yf ? jj - r * H1 : jj - r * (H1 + 1);
-      const int au = yf ? L1 + c : L1 + c - 1, av = yf ? L1 + r - 1 : L1 + r;   // lower cell
-      int rf = fregion(X0 + au, Y0 + av, N);
-      if (rf < 0) rf = fregion(X0 + au + (yf ? 0 : 1), Y0 + av + (yf ? 1 : 0), N);
-      if (rf >= 0) {
-        const int Ia = pick(rf, 1) + pick(rf, 3) * au + pick(rf, 4) * av;
-        const int Ja = pick(rf, 2) + pick(rf, 5) * au + pick(rf, 6) * av;
-        const int di = yf ? pick(rf, 4) : pick(rf, 3), dj = yf ? pick(rf, 6) : pick(rf, 5);
-        const int li = di != 0 ? Ja * (N + 1) + Ia + (di > 0) : Ia * (N + 1) + Ja + (dj > 0);
-        lnv[k] = a.lxt[li];
-      }
+      const int li = yf ? (X0 + L1 + c) * (N + 1) + Y0 + L1 + r : (Y0 + L1 + r) * (N + 1) + X0 + L1 + c;
+      lnv[k] = j < NFL ? a.lxt[li] : T(0);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < LPT; ++k) {
+      const int j = tid + k * NT;
+      lnv[k] = j < NFL ? a.len[(long)bid * NFL + j] : T(0);
     }
   }
-  // line normals of the regions present: thread (axis, region, line) < 2 * 5 * (W + 1)
-  T nrm3[3] = {T(0), T(0), T(0)};
-  const int n_ax = tid / (5 * (W + 1)), n_r = (tid / (W + 1)) % 5, n_k = tid % (W + 1);
-  const bool n_do = tid < 2 * 5 * (W + 1) && (n_r == 0 || ((flags >> n_r) & 1));
-  T n_t = T(0);
-  int n_sign = 0, n_isj = 0;
-  if (n_do) {
-    // the line between window cells k-1 and k along the axis, as a panel line
-    const int au = n_ax ? 0 : n_k - 1, av = n_ax ? n_k - 1 : 0;
-    const int Ia = pick(n_r, 1) + pick(n_r, 3) * au + pick(n_r, 4) * av;
-    const int Ja = pick(n_r, 2) + pick(n_r, 5) * au + pick(n_r, 6) * av;
-    const int di = n_ax ? pick(n_r, 4) : pick(n_r, 3), dj = n_ax ? pick(n_r, 6) : pick(n_r, 5);
-    n_isj = di == 0;
-    n_sign = di != 0 ? di : dj;
-    int line = di != 0 ? Ia + (di > 0) : Ja + (dj > 0);
-    line = line < 0 ? 0 : (line > N ? N : line);       // lines outside the region are never read
-    n_t = a.tane[line];
+  // line normals: one panel -> the panel's own lines from the tangents (thread
+  // (axis, line) < 2 (W + 1)), else the block's table (thread per value)
+  T nrv = T(0);
+  const bool nr_ld = flags == 1 ? tid < 2 * (W + 1) : tid < NN;
+  if (nr_ld) {
+    if (flags == 1) nrv = a.tane[(tid < W + 1 ? X0 + tid : Y0 + tid - (W + 1))];
+    else nrv = a.nrm[(long)bid * NN + tid];
   }
   // own window cell: state (+ geometry for the cells stage 1 updates)
   T Q[4];
@@ -401,21 +365,31 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
     for (int f = 0; f < 4; ++f) Q[f] = T(0);
   }
   if (loaded && in1) {
-    const int pi = cJ * N + cI;
-    iA = a.ainv[pi];
-    const T* sp = a.sloc + (long)pi * 4;
-    const T sx = sp[0], sy = sp[1], sz = sp[2];
-    const T ti = a.tanc[cI], tj = a.tanc[cJ];
+    using V2 = typename V16<T>::type;
+    const T* cp = a.crec + (long)(cJ * N + cI) * 8;
+    T cr[8];
+    if constexpr (sizeof(T) == 8) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const V2 x = *reinterpret_cast<const V2*>(cp + 2 * k);
+        cr[2 * k] = x.x; cr[2 * k + 1] = x.y;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const V2 x = *reinterpret_cast<const V2*>(cp + 4 * k);
+        cr[4 * k] = x.x; cr[4 * k + 1] = x.y; cr[4 * k + 2] = x.z; cr[4 * k + 3] = x.w;
+      }
+    }
     if (a.gbt) {
       const unsigned ci = src >= 0 ? (unsigned)src : (unsigned)(a.S + (-2 - src));
       const T* gp = a.gbt + (long)ci * 4;
       gb0 = gp[0]; gb1 = gp[1]; gb2 = gp[2];
     }
-    const int fr = a.frames[cg_];
-    to_global(fr, sx, sy, sz, S0, S1, S2);
-    // cell centre: the gnomonic point n + tan(alpha) e_i + tan(beta) e_j, normalised
-    const T rn = trcp(tsqrt(T(1) + ti * ti + tj * tj));
-    to_global(fr, ti * rn, tj * rn, rn, r0, r1, r2);
+    const int fr = (int)(a.frames >> (9 * cg_)) & 511;
+    iA = cr[0];
+    to_global(fr, cr[1], cr[2], cr[3], S0, S1, S2);
+    to_global(fr, cr[4], cr[5], cr[6], r0, r1, r2);
   }
   if (tid < NX2) {
 #pragma unroll
@@ -427,13 +401,18 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
     const int j = tid + k * NT;
     if (j < NFL) s_len[j] = lnv[k];
   }
-  if (n_do) {
-    // unit normal of the panel line: (e - t n) / sqrt(1 + t^2), e = e_i (x-line) or
-    // e_j (y-line), oriented along the window axis
-    const T rn = T(n_sign) * trcp(tsqrt(T(1) + n_t * n_t));
-    to_global(a.frames[pick(n_r, 0)], n_isj ? T(0) : rn, n_isj ? rn : T(0), -n_t * rn, nrm3[0], nrm3[1], nrm3[2]);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) s_nrm[n_ax][n_r][c][n_k] = nrm3[c];
+  if (nr_ld) {
+    if (flags == 1) {
+      // panel line: (e - t n) / sqrt(1 + t^2), e = e_i (x-line) or e_j (y-line)
+      const int ax = tid < W + 1 ? 0 : 1, k = tid - ax * (W + 1);
+      const T rn = trcp(tsqrt(T(1) + nrv * nrv));
+      T m0, m1, m2;
+      to_global((int)(a.frames >> (9 * ((unsigned)ow >> 29))) & 511, ax ? T(0) : rn, ax ? rn : T(0), -nrv * rn,
+                m0, m1, m2);
+      s_nrm[ax][0][0][k] = m0; s_nrm[ax][0][1][k] = m1; s_nrm[ax][0][2][k] = m2;
+    } else {
+      (&s_nrm[0][0][0][0])[tid] = nrv;
+    }
   }
   if (edge) {
     if (owner) s_code[v * W + u] = cdv;
@@ -457,11 +436,15 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   __syncthreads();
   FSTAMP(2);
 
+  // panel-edge lines in the window (block-uniform): x-lines X = 0 (W) / X = N
+  // (E), y-lines Y = 0 (S) / Y = N (N); far away when absent
+  const int kx0 = (flags & 2) ? -X0 : -1000, kx1 = (flags & 4) ? N - X0 : -1000;
+  const int ky0 = (flags & 8) ? -Y0 : -1000, ky1 = (flags & 16) ? N - Y0 : -1000;
+
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int lo = R - 2 * (NS - 1 - s), hi = W - lo;
     const int nr = hi - lo, nl = nr + 1, nx = nr * nl;
-    const int ntask = 2 * nx + ncor;
     // ---- ghost entries of this stage's input (edge blocks) ----------------------
     // the Putman-Lin interpolation of the neighbour panel's edge cells onto each
     // reader's grid line, one entry per thread; faces then read it like a cell
@@ -476,39 +459,35 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
         }
       }
       __syncthreads();
+      FSTAMP(10 + s);
     }
     // ---- faces ---------------------------------------------------------------
-    // EDGE: stencil neighbours come from the codes (window cell or ghost entry)
-    auto face_task = [&](int task, auto edge_c) {
+    // EDGE (blocks with a side region): the face's normal is that of the lower
+    // cell's region; only faces within one line of a panel edge line (a few
+    // lanes) take their stencil neighbours from the codes (window cell or ghost
+    // entry) -- a short divergent branch instead of a second face body.
+    auto face = [&](bool ax, int fu, int fv, int k, auto edge_c) {
       constexpr bool EDGE = decltype(edge_c)::value;
-      const bool ax = task >= nx;                            // false: x-face, true: y-face
-      const int t2 = ax ? task - nx : task;
-      int fu, fv, k, fslot, st;
-      if (!ax) {
-        const int r = t2 / nl, c = t2 - r * nl;
-        fv = lo + r; k = lo + c; fu = k;                     // b = (k, fv), a = (k - 1, fv)
-        fslot = (fv - L1) * (H1 + 1) + (k - L1);
-        st = 1;
-      } else {
-        const int r = t2 / nr, c = t2 - r * nr;
-        k = lo + r; fu = lo + c; fv = k;                     // b = (fu, k), a = (fu, k - 1)
-        fslot = NFX + (k - L1) * H1 + (fu - L1);
-        st = WS;
-      }
+      const int st = ax ? WS : 1;
+      const int fslot = ax ? NFX + (k - L1) * H1 + (fu - L1) : (fv - L1) * (H1 + 1) + (k - L1);
       const int ib = fv * WS + fu, ia = ib - st;
       int iam = ia - st, iap = ib, ibm = ia, ibp = ib + st, ra = 0;
       if constexpr (EDGE) {
-        const int sm = ax ? 2 : 0;                           // side index of -axis; +axis = sm + 1
-        const int ci = fv * W + fu, cj = ci - (ax ? W : 1);  // window indices of b and a
-        const unsigned long long ca = s_code[cj], cb = s_code[ci];
-        const int eam = ncode(ca, sm), eap = ncode(ca, sm + 1);
-        const int ebm = ncode(cb, sm), ebp = ncode(cb, sm + 1);
-        if (eam == -3 || ebm == -3) return;                  // a cell is missing: a corner face
-        if (eam >= 0) iam = GB + eam;
-        if (eap >= 0) iap = GB + eap;
-        if (ebm >= 0) ibm = GB + ebm;
-        if (ebp >= 0) ibp = GB + ebp;
+        const int e0 = ax ? ky0 : kx0, e1 = ax ? ky1 : kx1;
+        if ((unsigned)(k - e0 + 1) <= 2u || (unsigned)(k - e1 + 1) <= 2u) {
+          const int sm = ax ? 2 : 0;                         // side index of -axis; +axis = sm + 1
+          const int ci = fv * W + fu, cj = ci - (ax ? W : 1);  // window indices of b and a
+          const unsigned long long ca = s_code[cj], cb = s_code[ci];
+          const int eam = ncode(ca, sm), eap = ncode(ca, sm + 1);
+          const int ebm = ncode(cb, sm), ebp = ncode(cb, sm + 1);
+          if (eam == -3 || ebm == -3) return;                // a cell is missing: a corner face
+          if (eam >= 0) iam = GB + eam;
+          if (eap >= 0) iap = GB + eap;
+          if (ebm >= 0) ibm = GB + ebm;
+          if (ebp >= 0) ibp = GB + ebp;
+        }
         ra = fregion(X0 + fu - (ax ? 0 : 1), Y0 + fv - (ax ? 1 : 0), N);
+        ra = ra < 0 ? 0 : ra;                                // a missing: junk face, never read
       }
       T wl[4], wr[4], cl[5], cr[5];
 #pragma unroll
@@ -530,13 +509,26 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) s_fl[f][fslot] = fl[f];
     };
+    // corner faces start on a wave boundary (a wave runs every branch its lanes take)
+    const int p3 = (2 * nx + 63) & ~63;
+    const int ntask = ncor ? p3 + ncor : 2 * nx;
     for (int task = tid; task < ntask; task += NT) {
       if (task < 2 * nx) {
-        if (edge) face_task(task, std::true_type{});
-        else face_task(task, std::false_type{});
-      } else {
+        const bool ax = task >= nx;                          // false: x-face, true: y-face
+        const int t2 = ax ? task - nx : task;
+        int fu, fv, k;
+        if (!ax) {
+          const int r = t2 / nl, c = t2 - r * nl;
+          fv = lo + r; k = lo + c; fu = k;                   // b = (k, fv), a = (k - 1, fv)
+        } else {
+          const int r = t2 / nr, c = t2 - r * nr;
+          k = lo + r; fu = lo + c; fv = k;                   // b = (fu, k), a = (fu, k - 1)
+        }
+        if (edge) face(ax, fu, fv, k, std::true_type{});
+        else face(ax, fu, fv, k, std::false_type{});
+      } else if (task >= p3) {
         // cube-corner face j: cell c's face on side_c meets cell d's face on side_d
-        const int j = task - 2 * nx;
+        const int j = task - p3;
         const int ec = s_ct[j][0], ed = s_ct[j][1];
         T fv2[2][4], cc[2][5];
 #pragma unroll
@@ -655,8 +647,6 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   FSTAMP(3 + 2 * NS);
 }
 
-#undef pick
-
 template <typename T, int NS, int B>
 int launch_fused(const FusedDesc* d, hipStream_t s) {
   using D = FD<NS, B>;
@@ -664,10 +654,11 @@ int launch_fused(const FusedDesc* d, hipStream_t s) {
   if (d->pw != d->n + 2 * d->mg || d->mg < 2 || d->n % B) return -3;
   FArgs<T> a;
   a.Q = (const T*)d->Q; a.out = (T*)d->out; a.src = d->src; a.org = d->org;
-  a.rmap = d->rmap; a.tanc = (const T*)d->tanc; a.tane = (const T*)d->tane; a.ainv = (const T*)d->ainv;
-  a.sloc = (const T*)d->sloc; a.lxt = (const T*)d->lxt; a.gbt = (const T*)d->gbt;
-  for (int k = 0; k < 6; ++k) a.frames[k] = d->frames[k];
-  if (!a.rmap || !a.tanc || !a.tane || !a.ainv || !a.sloc || !a.lxt) return -4;
+  a.len = (const T*)d->len; a.nrm = (const T*)d->nrm; a.tane = (const T*)d->tane; a.crec = (const T*)d->crec;
+  a.lxt = (const T*)d->lxt; a.gbt = (const T*)d->gbt;
+  a.frames = 0;
+  for (int k = 0; k < 6; ++k) a.frames |= (unsigned long long)(d->frames[k] & 511) << (9 * k);
+  if (!a.len || !a.nrm || !a.tane || !a.crec || !a.lxt) return -4;
   a.code = (const unsigned long long*)d->code; a.gtab = d->gtab;
   a.gw = (const T*)d->gw;
   a.ctab = d->ctab; a.cgf = (const T*)d->cgf; a.ccnt = d->ccnt; a.push = d->push;

@@ -367,15 +367,14 @@ __device__ __forceinline__ void swe_flux(const T (&wl)[4], const T (&wr)[4], con
   const T sL = tabs(cl[1] * m0 + cl[2] * m1 + cl[3] * m2) + cl[4];
   const T sR = tabs(cr[1] * m0 + cr[2] * m1 + cr[3] * m2) + cr[4];
   const T hc = T(0.5) * tmax(sL, sR);
-  const T pL = hL * vnL, pR = hR * vnR;
-  f[0] = (T(0.5) * (pL + pR) - hc * (hR - hL)) * L;
-  const T pr = T(0.25) * g * (hL * hL + hR * hR);
-  const T mm[3] = {m0, m1, m2};
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const T uL = hL * wl[1 + k], uR = hR * wr[1 + k];
-    f[1 + k] = (T(0.5) * (uL * vnL + uR * vnR) + pr * mm[k] - hc * (uR - uL)) * L;
-  }
+  // F = L [ hL (vnL/2 + hc) (1, vL) + hR (vnR/2 - hc) (1, vR) + (0, pr m) ]: the
+  // Rusanov average and jump folded into one weight per side (fewer fp64 ops)
+  const T bL = L * hL * (T(0.5) * vnL + hc), bR = L * hR * (T(0.5) * vnR - hc);
+  const T prL = T(0.25) * g * L * (hL * hL + hR * hR);
+  f[0] = bL + bR;
+  f[1] = bL * wl[1] + (bR * wr[1] + prL * m0);
+  f[2] = bL * wl[2] + (bR * wr[2] + prL * m1);
+  f[3] = bL * wl[3] + (bR * wr[3] + prL * m2);
 }
 
 // State access: plain in launch-per-stage kernels; in the persistent kernel,

@@ -76,13 +76,13 @@ typedef struct FusedDesc {
   void* out;            // [F][S] step output: interior + same-rank ghost pushes
   const int* src;       // [nb][W*W] padded offset of each window cell's source, -1 = not loaded
   const int* org;       // [nb][4] X0, Y0, tile_local, xo | yo << 12 | region flags << 24 | face << 29
-  // geometry (ops/fused.py::kernel_geometry): per-block region maps and
-  // panel-independent tables, no per-cell records
-  const int* rmap;      // [nb][5][8] panel, I0, J0, m00, m01, m10, m11, 0
-  const void* tanc;     // [N]
+  // geometry (ops/fused.py::kernel_geometry): panel-independent tables, no
+  // per-cell records; blocks with a side region also read their own face
+  // lengths and line normals
+  const void* len;      // [nb][2 H1 (H1+1)] x-faces, then y-faces
+  const void* nrm;      // [nb][2][5][3][W+1] line normals per region, component-major
   const void* tane;     // [N+1]
-  const void* ainv;     // [N*N]
-  const void* sloc;     // [N*N][4]
+  const void* crec;     // [N*N][8] 1/A, S (3), centre (3), 0 in panel-local components
   const void* lxt;      // [N][N+1]
   const void* gbt;      // [S (+ ring)][4] grad b, padded layout; null without topography
   int frames[6];

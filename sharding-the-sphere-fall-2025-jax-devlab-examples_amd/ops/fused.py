@@ -90,17 +90,6 @@ def frame_map(N: int, face: int, reg: int) -> Tuple[int, np.ndarray]:
     return int(F[0]), M
 
 
-def region_affine(N: int, face: int, reg: int) -> Tuple[int, np.ndarray, np.ndarray]:
-    """(panel, c, M): the panel-local index of extended-panel coordinates
-    (X, Y) of region ``reg`` around ``face`` is c + M @ (X, Y) (the cube-edge
-    crossing of models/topology.py is an integer rotation / reflection)."""
-    F, M = frame_map(N, face, reg)
-    p = _region_point(N, reg)
-    _, I, J = neighbor_cells(N, face, np.array([p[0]]), np.array([p[1]]))
-    c = np.array([int(I[0]), int(J[0])], dtype=np.int64) - M @ np.array(p, dtype=np.int64)
-    return F, c, M
-
-
 def frame_code(face: int) -> int:
     """Panel frame for the kernel's to_global: axis of e_i (bits 0-1), of e_j
     (bits 2-3), sign bits of e_i, e_j, n (6, 7, 8); FACE_FRAMES rows are n, e_i, e_j."""
@@ -112,46 +101,33 @@ def frame_code(face: int) -> int:
     return ax(ei) | (ax(ej) << 2) | (neg(ei) << 6) | (neg(ej) << 7) | (neg(n) << 8)
 
 
-def kernel_geometry(layout: TileLayout, grid, P: "FusedPlan") -> Dict[str, np.ndarray]:
-    """Geometry the gfx950 kernel reconstructs per block instead of reading
-    per-cell records (fused_step.hip, prologue):
+def kernel_geometry(layout: TileLayout, grid) -> Dict[str, np.ndarray]:
+    """Panel-independent geometry the gfx950 kernel reads instead of per-cell
+    records (fused_step.hip, prologue; the window cell's panel index comes from
+    the cube topology, window_cell):
 
-      rmap  [nb, 5, 8] int32  per region: panel, I0, J0, m00, m01, m10, m11, 0 with
-                              panel index (I, J) = (I0, J0) + M @ (u, v) of window cell (u, v)
       frames [6] int32        frame_code per panel
-      tanc [N], tane [N+1]    tan of the cell-centre / grid-line angles
-      ainv [N*N]              1/A by panel-local index (equal on every panel)
-      sloc [N*N, 4]           curvature sum S = sum(L m) over the cell's faces, in
-                              panel-local components (e_i, e_j, n), 0
+      tane [N+1]              tan of the grid-line angles
+      crec [N*N, 8]           by panel-local index (equal on every panel): 1/A, the
+                              curvature sum S = sum(L m) over the cell's faces and the
+                              cell centre, both in panel-local components (e_i, e_j, n), 0
       lxt  [N, N+1]           x-edge lengths (j, i'); y-edge (j', i) = lxt[i, j']
     """
-    N, B = layout.N, P.B
-    nb = P.nb
-    rmap = np.zeros((nb, NREG, 8), dtype=np.int64)
-    aff = {}
-    for b in range(nb):
-        li, rem = divmod(b, P.nbx * P.nby)
-        face = layout.tile_origin(P.tiles[li])[0]
-        X0, Y0 = int(P.org[b, 0]), int(P.org[b, 1])
-        for r in range(NREG):
-            if (face, r) not in aff:
-                aff[(face, r)] = region_affine(N, face, r)
-            F, c, M = aff[(face, r)]
-            I0, J0 = c + M @ np.array([X0, Y0])
-            rmap[b, r] = (F, I0, J0, M[0, 0], M[0, 1], M[1, 0], M[1, 1], 0)
+    N = layout.N
     lx, ly = grid.x_edge_lengths(), grid.y_edge_lengths()
     mx, my = grid.x_edge_normals(), grid.y_edge_normals()
     # panel 4 has the identity frame (n, e_i, e_j) = (x, y, z): local = (y, z, x)
     f4 = 4
     Sv = (lx[f4, :, 1:, None] * mx[f4, None, 1:, :] - lx[f4, :, :-1, None] * mx[f4, None, :-1, :]
           + ly[f4, 1:, :, None] * my[f4, 1:, None, :] - ly[f4, :-1, :, None] * my[f4, :-1, None, :])   # [N,N,3]
-    sloc = np.zeros((N * N, 4))
-    sloc[:, 0], sloc[:, 1], sloc[:, 2] = Sv[..., 1].ravel(), Sv[..., 2].ravel(), Sv[..., 0].ravel()
+    c4 = grid.centers()[f4]                                   # [N, N, 3] (x, y, z) = (n, e_i, e_j)
+    crec = np.zeros((N * N, 8))
+    crec[:, 0] = (1.0 / grid.areas()[0]).ravel()
+    crec[:, 1], crec[:, 2], crec[:, 3] = Sv[..., 1].ravel(), Sv[..., 2].ravel(), Sv[..., 0].ravel()
+    crec[:, 4], crec[:, 5], crec[:, 6] = c4[..., 1].ravel(), c4[..., 2].ravel(), c4[..., 0].ravel()
     return {
-        "rmap": rmap.astype(np.int32),
         "frames": np.array([frame_code(f) for f in range(6)], dtype=np.int32),
-        "tanc": np.tan(grid.alpha_centers()), "tane": np.tan(grid.alpha_edges()),
-        "ainv": (1.0 / grid.areas()[0]).ravel(), "sloc": sloc, "lxt": lx[0].copy(),
+        "tane": np.tan(grid.alpha_edges()), "crec": crec, "lxt": lx[0].copy(),
     }
 
 
@@ -992,14 +968,13 @@ class FusedKernel:
             org[b, 3] = np.int32(np.uint32((xb * B) | ((yb * B) << 12) | (flags << 24) | (face << 29)).view(np.int32))
         # geometry: shared panel tables + per-block region maps (kernel_geometry);
         # grad b per cell [S (+ ring)][4] in the padded layout, only with topography
-        kg = kernel_geometry(e.layout, e.grid, P)
+        kg = kernel_geometry(e.layout, e.grid)
         self.frames = [int(x) for x in kg["frames"]]
-        rm = kg["rmap"]
-        assert rm.shape == (nb, NREG, 8)
         t = lambda a, ty=dt: torch.as_tensor(np.ascontiguousarray(a), dtype=ty, device=dev)
         self.tens = {
-            "rmap": t(rm, torch.int32), "tanc": t(kg["tanc"]), "tane": t(kg["tane"]), "ainv": t(kg["ainv"]),
-            "sloc": t(kg["sloc"]), "lxt": t(kg["lxt"]),
+            "len": t(np.concatenate([P.lx.reshape(nb, -1), P.ly.reshape(nb, -1)], 1)),
+            "nrm": t(np.ascontiguousarray(np.moveaxis(P.nrm, -1, -2))),      # [nb,2,5,3,W+1]
+            "tane": t(kg["tane"]), "crec": t(kg["crec"]), "lxt": t(kg["lxt"]),
             "src": t(P.src, torch.int32), "org": t(org, torch.int32),
             "code": t(code.view(np.int64), torch.int64), "gtab": t(gpair, torch.int32), "gw": t(P.gt),
             "ctab": t(ct, torch.int32), "cgf": t(P.cgeo), "ccnt": t(P.ccnt, torch.int32),
@@ -1069,7 +1044,7 @@ class FusedKernel:
         p = native.ptr
         d = native.FusedDesc()
         d.Q, d.out = p(e.pool[qi]), p(e.pool[oi])
-        for k in ("rmap", "tanc", "tane", "ainv", "sloc", "lxt", "src", "org", "code", "gtab", "gw", "ctab", "cgf",
+        for k in ("len", "nrm", "tane", "crec", "lxt", "src", "org", "code", "gtab", "gw", "ctab", "cgf",
                   "ccnt", "push"):
             setattr(d, k, p(tn[k]))
         d.gbt = p(tn["gbt"]) if tn["gbt"] is not None else 0

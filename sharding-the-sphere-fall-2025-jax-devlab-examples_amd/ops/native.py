@@ -47,8 +47,7 @@ class FusedDesc(ctypes.Structure):
     """Mirror of FusedDesc (stsp_kernels.h): one fused SSP-RK3 step."""
     _fields_ = [
         ("Q", ctypes.c_void_p), ("out", ctypes.c_void_p), ("src", ctypes.c_void_p), ("org", ctypes.c_void_p),
-        ("rmap", ctypes.c_void_p), ("tanc", ctypes.c_void_p), ("tane", ctypes.c_void_p), ("ainv", ctypes.c_void_p),
-        ("sloc", ctypes.c_void_p), ("lxt", ctypes.c_void_p), ("gbt", ctypes.c_void_p), ("frames", ctypes.c_int * 6),
+        ("len", ctypes.c_void_p), ("nrm", ctypes.c_void_p), ("tane", ctypes.c_void_p), ("crec", ctypes.c_void_p), ("lxt", ctypes.c_void_p), ("gbt", ctypes.c_void_p), ("frames", ctypes.c_int * 6),
         ("code", ctypes.c_void_p),
         ("gtab", ctypes.c_void_p), ("gw", ctypes.c_void_p), ("ctab", ctypes.c_void_p), ("cgf", ctypes.c_void_p),
         ("ccnt", ctypes.c_void_p), ("push", ctypes.c_void_p),

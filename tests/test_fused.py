@@ -245,104 +245,54 @@ def test_kernel_tables_cpu():
     assert np.allclose(sbal, want, rtol=1e-12, atol=1e-12 * np.abs(want).max())
 
 
-def _fregion(X, Y, N):
-    inx, iny = 0 <= X < N, 0 <= Y < N
-    if inx:
-        return 0 if iny else (3 if Y < 0 else 4)
-    return (1 if X < 0 else 2) if iny else -1
-
-
 def _to_global(fr, xi, xj, xn):
     ai, aj = fr & 3, (fr >> 2) & 3
     xi, xj, xn = (-xi if fr & 64 else xi), (-xj if fr & 128 else xj), (-xn if fr & 256 else xn)
     return np.array([xi if ai == c else (xj if aj == c else xn) for c in range(3)])
 
 
-@pytest.mark.parametrize("N,t,B", [(32, 2, 16), (36, 2, 18)])
+@pytest.mark.parametrize("N,t,B", [(64, 2, 16), (72, 2, 18)])
 def test_kernel_geometry_reconstruction_cpu(N, t, B):
-    """The fused kernel's prologue rebuilds every block's geometry from region
-    maps + panel-independent tables (ops/fused.py::kernel_geometry); this
-    emulates that arithmetic on the host and checks it against the plan's
-    per-block normals / face lengths and the per-cell records (1/A, centre,
-    curvature sum) it replaced, for every window cell of every block."""
-    from stsphere.ops.fused import NREG, global_cell_records, kernel_geometry
+    """The fused kernel's prologue reads panel-independent tables instead of
+    per-cell records (ops/fused.py::kernel_geometry): emulated on the host,
+    the panel-local record of every window cell, rotated by its panel's
+    frame code, reproduces the global record (1/A, centre, curvature sum);
+    and in blocks inside one panel the identity-map face lengths and the
+    tangent-built line normals equal the plan's per-block tables."""
+    from stsphere.ops.fused import global_cell_records, kernel_geometry
     L = TileLayout(N, t, 1, ng=2)
     grid = CubedSphereGrid(N)
     e = Engine(ShallowWater("tc5"), L, grid=grid)
     P = FusedPlan(L, 0, grid, B=B)
-    kg = kernel_geometry(L, grid, P)
+    kg = kernel_geometry(L, grid)
     d = P.d
     W, L1, H1 = d.W, d.L1, d.H1
     rec = global_cell_records(e)
-    lxt, tanc, tane = kg["lxt"], kg["tanc"], kg["tane"]
+    lxt, tane, crec = kg["lxt"], kg["tane"], kg["crec"]
+    inner = 0
     for b in range(P.nb):
         X0, Y0 = int(P.org[b, 0]), int(P.org[b, 1])
-        rm = kg["rmap"][b]
-        reg = P.reg[b].reshape(W, W)
-
-        def pan(r, u, v):
-            m = rm[r]
-            return m[0], m[1] + m[3] * u + m[4] * v, m[2] + m[5] * u + m[6] * v
-
-        # per-cell records
-        for v in range(W):
-            for u in range(W):
-                r = _fregion(X0 + u, Y0 + v, N)
-                assert r == reg[v, u]
-                if r < 0:
-                    continue
-                g, I, J = pan(r, u, v)
-                gid = P.gid[b, v * W + u]
-                assert gid == (g * N + J) * N + I
-                fr = int(kg["frames"][g])
-                pi = J * N + I
-                assert np.isclose(kg["ainv"][pi], rec[gid, 0], rtol=1e-13)
-                S = _to_global(fr, *kg["sloc"][pi, :3])
-                assert np.allclose(S, rec[gid, 7:10], rtol=1e-9, atol=1e-9 * np.abs(rec[gid, 7:10]).max())
-                rn = 1.0 / np.sqrt(1 + tanc[I] ** 2 + tanc[J] ** 2)
-                assert np.allclose(_to_global(fr, tanc[I] * rn, tanc[J] * rn, rn), rec[gid, 1:4], atol=1e-14)
-        # stage-1 face lengths
-        lens = np.concatenate([P.lx[b].ravel(), P.ly[b].ravel()])
-        nfx = H1 * (H1 + 1)
-        for j in range(2 * nfx):
-            yf = j >= nfx
-            jj = j - nfx if yf else j
-            r_, c = (divmod(jj, H1) if yf else divmod(jj, H1 + 1))
-            au, av = (L1 + c, L1 + r_ - 1) if yf else (L1 + c - 1, L1 + r_)
-            rf = _fregion(X0 + au, Y0 + av, N)
-            if rf < 0:
-                rf = _fregion(X0 + au + (0 if yf else 1), Y0 + av + (1 if yf else 0), N)
-            if rf < 0:
-                assert lens[j] == 0.0
-                continue
-            _, Ia, Ja = pan(rf, au, av)
-            di, dj = (rm[rf][4], rm[rf][6]) if yf else (rm[rf][3], rm[rf][5])
-            got = lxt[Ja, Ia + (di > 0)] if di != 0 else lxt[Ia, Ja + (dj > 0)]
-            assert np.isclose(got, lens[j], rtol=1e-12), (b, j)
-        # line normals of the regions present
+        for gid in P.gid[b][P.gid[b] >= 0]:
+            g, rem = divmod(int(gid), N * N)
+            J, I = divmod(rem, N)
+            fr = int(kg["frames"][g])
+            pi = J * N + I
+            assert np.isclose(crec[pi, 0], rec[gid, 0], rtol=1e-13)
+            S = _to_global(fr, *crec[pi, 1:4])
+            assert np.allclose(S, rec[gid, 7:10], rtol=1e-9, atol=1e-9 * np.abs(rec[gid, 7:10]).max())
+            assert np.allclose(_to_global(fr, *crec[pi, 4:7]), rec[gid, 1:4], atol=1e-15)
+        if (P.reg[b] != 0).any():
+            continue
+        inner += 1
+        face = L.tile_origin(P.tiles[b // (P.nbx * P.nby)])[0]
+        r = np.arange(H1)[:, None]
+        c = np.arange(H1 + 1)[None, :]
+        assert np.allclose(lxt[Y0 + L1 + r, X0 + L1 + c], P.lx[b], rtol=1e-12)
+        assert np.allclose(lxt[X0 + L1 + r, Y0 + L1 + c], P.ly[b].T, rtol=1e-12)
         for ax in (0, 1):
-            for r in range(NREG):
-                if not (reg == r).any():
-                    continue
-                for k in range(W + 1):
-                    want = P.nrm[b, ax, r, k]
-                    if not want.any():
-                        continue
-                    au, av = (0, k - 1) if ax else (k - 1, 0)
-                    g, Ia, Ja = pan(r, au, av)
-                    di, dj = (rm[r][4], rm[r][6]) if ax else (rm[r][3], rm[r][5])
-                    line = Ia + (di > 0) if di != 0 else Ja + (dj > 0)
-                    tn = tane[min(max(line, 0), N)]
-                    rn = (di if di != 0 else dj) / np.sqrt(1 + tn * tn)
-                    m = _to_global(int(kg["frames"][g]), 0.0 if di == 0 else rn, rn if di == 0 else 0.0, -tn * rn)
-                    assert np.allclose(m, want, atol=1e-14), (b, ax, r, k)
-
-
-def test_step_fusable_integrators():
-    """Integrators a one-kernel step can hold on chip (stages combine the
-    step-start state with the previous stage output)."""
-    from stsphere.models.integrators import get_integrator, step_kernel_compatible
-    assert step_kernel_compatible(get_integrator("ssprk3"))
-    assert step_kernel_compatible(get_integrator("ssprk2"))
-    assert not step_kernel_compatible(get_integrator("rk4"))
-    assert not step_kernel_compatible(get_integrator("euler"))
+            for k in range(W + 1):
+                tn = tane[(Y0 if ax else X0) + k]
+                rn = 1.0 / np.sqrt(1 + tn * tn)
+                m = _to_global(int(kg["frames"][face]), 0.0 if ax else rn, rn if ax else 0.0, -tn * rn)
+                assert np.allclose(m, P.nrm[b, ax, 0, k], atol=1e-14), (b, ax, k)
+    assert inner > 0

@@ -96,10 +96,14 @@ def main():
         ph = {}
         side = edge & ~corner
         mean = lambda m, k: round(float(blk[m, k].mean()), 0) if m.any() else None
+        names = names + [f"s{s}_fix" for s in range(1, 4)]
         for k, nm in enumerate(names):
             ph[nm] = {"int_mean": mean(~edge, k), "edge_mean": mean(side, k), "corner_mean": mean(corner, k),
                       "max": float(blk[:, k].max())}
         out["phases_cycles"] = ph
+        P = fk.plan
+        out["ghost_entries_max"] = int(P.gcnt.max())
+        out["corner_faces_max"] = int(P.ccnt.max())
         out["start_spread"] = float(t0.max() - t0.min())
         out["end_max"] = float((v[:, :, 9].max(1) - t0.min()).max())
         out["edge_blocks"] = int(edge.sum())
