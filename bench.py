@@ -59,6 +59,9 @@ def parse(argv=None):
     ap.add_argument("--runtime", default="auto", choices=["auto", "fused", "native", "graph", "eager"],
                     help="fused: one launch per SSP-RK3 step (temporal blocking, one rank); native: one launch "
                          "per RK stage (C++ op list, any rank count); auto: fused where it applies")
+    ap.add_argument("--steps-per-launch", type=int, default=0,
+                    help="fused runtime: steps inside one kernel launch (0 = auto: the largest even divisor of "
+                         "--steps up to 64 when every block fits on the GPU at once; 1 = one launch per step)")
     ap.add_argument("--steps-per-graph", type=int, default=0,
                     help="steps recorded per graph (0 = the whole timed run in one graph)")
     ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "rccl"],
@@ -244,6 +247,7 @@ def main():
     elif comm == "auto":
         comm = "xgmi" if world > 1 else "none"
     spg = a.steps_per_graph if a.steps_per_graph > 0 else a.steps
+    info = {"steps_per_launch": None}
 
     # collectives on CUDA tensors with RCCL, on CPU tensors with gloo
     cdev = device if (world > 1 and dist.get_backend() == "nccl") else torch.device("cpu")
@@ -281,7 +285,13 @@ def main():
             from stsphere.ops.native_runtime import NativeStepper
             fk = FusedKernel(eng, timeout_s=2.0)      # collective with several ranks
             xg = fk if world > 1 else None
-            runner = NativeStepper(eng, use_graph=True, steps_per_graph=spg, fused=fk)
+            spl = a.steps_per_launch
+            if spl == 0:
+                # several steps per launch (in-kernel producer waits) need every block resident
+                cus = torch.cuda.get_device_properties(device).multi_processor_count
+                spl = max([k for k in range(2, 65, 2) if a.steps % k == 0], default=1) if fk.plan.nb <= cus else 1
+            info["steps_per_launch"] = spl
+            runner = NativeStepper(eng, use_graph=True, steps_per_graph=spg, fused=fk, steps_per_launch=spl)
         elif runtime == "native":
             # C++ runtime, hipGraph replay; between GPUs either direct xGMI
             # stores from the stage kernels (graph-captured) or RCCL grouped
@@ -448,6 +458,7 @@ def main():
                 "runtime": runtime,
                 "comm": comm,
                 "block": list((eng.compute.bx, eng.compute.by)) if hasattr(eng.compute, "bx") else None,
+                "steps_per_launch": info["steps_per_launch"],
                 "graph_replayed_steps": timed.get("graph_steps"),
                 "eager_steps": timed.get("eager_steps"),
             },

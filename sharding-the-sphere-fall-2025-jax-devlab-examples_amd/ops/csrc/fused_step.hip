@@ -149,6 +149,14 @@ struct FArgs {
   int* err;
   long long timeout_ticks;
   unsigned long long* stamps;
+  // several steps per launch (nsteps > 1): buffers alternate (Q -> out -> Q ...);
+  // before step k > 0 a block waits until every producer (block whose cells
+  // its window loads, relation made symmetric on the host) has completed k
+  // steps of this launch; state hand-off by write-through (sc1) stores, a
+  // drained per-block epoch (sc1 store) and sc1 loads
+  int nsteps;
+  const int* prod;        // [nb][PM] producer blocks, -1 padded
+  int PM;
 };
 
 // phase stamp (profiling): lane 0 of every wave, when a.stamps is set
@@ -160,6 +168,13 @@ struct FArgs {
         a.stamps[((long)bid * 16 + (threadIdx.x >> 6)) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
       __builtin_amdgcn_sched_barrier(0);                                                         \
     }                                                                                            \
+  } while (0)
+// constant-rate clock (100 MHz) next to the shader-clock stamps: the probe
+// derives the shader clock from the pair
+#define FSTAMP_RT(k)                                                                             \
+  do {                                                                                           \
+    if (a.stamps && (threadIdx.x & 63) == 0)                                                     \
+      a.stamps[((long)bid * 16 + (threadIdx.x >> 6)) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 // Panel cell (g, I, J) at extended-panel coordinates (X, Y) of face f; false
@@ -211,7 +226,7 @@ __device__ __forceinline__ int ncode(unsigned long long c, int side) {
   return (int)(short)(unsigned short)(c >> (16 * side));
 }
 
-template <typename T, int LIM, int NS, int B, bool XG>
+template <typename T, int LIM, int NS, int B, bool XG, bool MULTI>
 __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   using D = FD<NS, B>;
   constexpr int W = D::W, WS = D::WS, WW = D::WW, GB = D::GB, R = D::R, L1 = D::L1, H1 = D::H1;
@@ -242,6 +257,7 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   const bool edge = (flags & 0x1E) != 0;                 // a side region is present (block-uniform)
   const T* wf = &s_w[0];
   FSTAMP(0);
+  FSTAMP_RT(14);
 
   // ---- 0. prologue: every global load first, then the LDS writes --------------
   // Per block only the state is unique data: the geometry comes from
@@ -252,8 +268,10 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   const bool owner = tid < W * W;
   if (owner) owner_cell<NS, B>(tid, u, v);
   const int wi = v * WS + u;                             // this owner's LDS window index
-  int xe = 0;                                            // steps this block has completed (XG)
-  if constexpr (XG) xe = a.epoch[bid];
+  int xe = 0;                                            // steps this block has completed
+  const int nsteps = MULTI ? a.nsteps : 1;
+  const bool epoch_on = XG || MULTI;
+  if (epoch_on) xe = a.epoch[bid];
   const int n = a.n;
   // own cell: panel and panel-local index (cube topology)
   int cg_ = 0, cI = 0, cJ = 0;
@@ -326,44 +344,53 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
     S2 = T(0);
   const bool loaded = src >= 0 || (XG && src <= -2);
   const bool in1 = tid < (B + 4 * (NS - 1)) * (B + 4 * (NS - 1));   // updated by stage 1
-  if (XG && src <= -2) {
-    // another rank's cell: spin on its granules in ring slot xe % SLOTS until
-    // every tag carries this step (xe + 1); a timeout sets err and falls through
-    constexpr int G = sizeof(T) / 4;
-    const gu64* rp = (const gu64*)(a.recv) + (long)(xe % STSP_XG_SLOTS) * a.ring + (long)(-2 - src) * (4 * G);
-    const unsigned want = (unsigned)xe + 1u;
-    unsigned long long gr[4 * G];
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-      bool ok = true;
+  // state of the own window cell at the start of a step: another rank's cell
+  // from the xGMI ring, else the state buffer (sc1 loads: with several steps
+  // per launch the producer may sit on another XCD)
+  auto load_state = [&](const T* Qin, int xe_) {
+    if (XG && src <= -2) {
+      // another rank's cell: spin on its granules in ring slot xe % SLOTS until
+      // every tag carries this step (xe + 1); a timeout sets err and falls through
+      constexpr int G = sizeof(T) / 4;
+      const gu64* rp = (const gu64*)(a.recv) + (long)(xe_ % STSP_XG_SLOTS) * a.ring + (long)(-2 - src) * (4 * G);
+      const unsigned want = (unsigned)xe_ + 1u;
+      unsigned long long gr[4 * G];
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        bool ok = true;
 #pragma unroll
-      for (int k = 0; k < 4 * G; ++k) {
-        gr[k] = __hip_atomic_load(rp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        ok &= (unsigned)(gr[k] >> 32) == want;
+        for (int k = 0; k < 4 * G; ++k) {
+          gr[k] = __hip_atomic_load(rp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          ok &= (unsigned)(gr[k] >> 32) == want;
+        }
+        if (ok) break;
+        if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
+          __hip_atomic_store((gu32*)a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      if (ok) break;
-      if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
-      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
-        __hip_atomic_store((gu32*)a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        if constexpr (G == 2)
+          Q[f] = __builtin_bit_cast(T, (gr[2 * f + 1] << 32) | (gr[2 * f] & 0xFFFFFFFFull));
+        else
+          Q[f] = __builtin_bit_cast(T, (unsigned)gr[f]);
       }
-      __builtin_amdgcn_s_sleep(1);
+    } else if (loaded) {
+      const unsigned S = (unsigned)a.S;
+      unsigned so = (unsigned)src;
+      asm volatile("" : "+v"(so));   // per step: keep the addresses out of registers across steps
+#pragma unroll
+      for (int f = 0; f < 4; ++f) Q[f] = ld_state<true>(o32(Qin, so + f * S));
+    } else {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) Q[f] = T(0);
     }
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      if constexpr (G == 2)
-        Q[f] = __builtin_bit_cast(T, (gr[2 * f + 1] << 32) | (gr[2 * f] & 0xFFFFFFFFull));
-      else
-        Q[f] = __builtin_bit_cast(T, (unsigned)gr[f]);
-    }
-  } else if (loaded) {
-    const unsigned S = (unsigned)a.S;
-#pragma unroll
-    for (int f = 0; f < 4; ++f) Q[f] = *o32(a.Q, (unsigned)src + f * S);
-  } else {
-#pragma unroll
-    for (int f = 0; f < 4; ++f) Q[f] = T(0);
-  }
+  };
+  T* const buf[2] = {const_cast<T*>(a.Q), a.out};
+  load_state(buf[0], xe);
   if (loaded && in1) {
     using V2 = typename V16<T>::type;
     const T* cp = a.crec + (long)(cJ * N + cI) * 8;
@@ -390,10 +417,6 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
     iA = cr[0];
     to_global(fr, cr[1], cr[2], cr[3], S0, S1, S2);
     to_global(fr, cr[4], cr[5], cr[6], r0, r1, r2);
-  }
-  if (tid < NX2) {
-#pragma unroll
-    for (int f = 0; f < 4; ++f) s_x[f][tid] = Q[f];
   }
   // tables -> LDS
 #pragma unroll
@@ -431,15 +454,40 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
     p[3 * WW] = q[3] * inv;
     p[4 * WW] = tsqrt(a.g * tmax(q[0], T(0)));
   };
-  if (owner) put(Q);
-  FSTAMP(1);
-  __syncthreads();
-  FSTAMP(2);
-
   // panel-edge lines in the window (block-uniform): x-lines X = 0 (W) / X = N
   // (E), y-lines Y = 0 (S) / Y = N (N); far away when absent
   const int kx0 = (flags & 2) ? -X0 : -1000, kx1 = (flags & 4) ? N - X0 : -1000;
   const int ky0 = (flags & 8) ? -Y0 : -1000, ky1 = (flags & 16) ? N - Y0 : -1000;
+
+  for (int it = 0; it < nsteps; ++it) {
+  if (it > 0) {
+    // wait for the producers' previous step (wave 0 polls, the barrier releases
+    // the others), then load this step's window
+    if (tid < 64) {
+      const int p = tid < a.PM ? a.prod[(long)bid * a.PM + tid] : -1;
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        const bool ok = p < 0 || __hip_atomic_load(a.epoch + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= xe;
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
+          if (tid == 0) __hip_atomic_store((gu32*)a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    load_state(buf[it & 1], xe);
+  }
+  if (tid < NX2) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) s_x[f][tid] = Q[f];
+  }
+  if (owner) put(Q);
+  FSTAMP(1);
+  __syncthreads();
+  FSTAMP(2);
 
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -472,9 +520,12 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
       const int fslot = ax ? NFX + (k - L1) * H1 + (fu - L1) : (fv - L1) * (H1 + 1) + (k - L1);
       const int ib = fv * WS + fu, ia = ib - st;
       int iam = ia - st, iap = ib, ibm = ia, ibp = ib + st, ra = 0;
+      bool wnear = false;                                    // some lane of this wave is near an edge line
       if constexpr (EDGE) {
         const int e0 = ax ? ky0 : kx0, e1 = ax ? ky1 : kx1;
-        if ((unsigned)(k - e0 + 1) <= 2u || (unsigned)(k - e1 + 1) <= 2u) {
+        const bool near = (unsigned)(k - e0 + 1) <= 2u || (unsigned)(k - e1 + 1) <= 2u;
+        wnear = __builtin_amdgcn_ballot_w64(near) != 0;
+        if (near) {
           const int sm = ax ? 2 : 0;                         // side index of -axis; +axis = sm + 1
           const int ci = fv * W + fu, cj = ci - (ax ? W : 1);  // window indices of b and a
           const unsigned long long ca = s_code[cj], cb = s_code[ci];
@@ -497,8 +548,10 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
         const T am = wf[f * WW + iam], bp = wf[f * WW + ibp];
         T ap = cr[f], bm = cl[f];
         if constexpr (EDGE) {
-          ap = wf[f * WW + iap];
-          bm = wf[f * WW + ibm];
+          if (wnear) {                                       // wave-uniform: most waves skip these loads
+            ap = wf[f * WW + iap];
+            bm = wf[f * WW + ibm];
+          }
         }
         wl[f] = cl[f] + half_slope<LIM>(cl[f] - am, ap - cl[f]);
         wr[f] = cr[f] - half_slope<LIM>(cr[f] - bm, bp - cr[f]);
@@ -517,8 +570,8 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
         const bool ax = task >= nx;                          // false: x-face, true: y-face
         const int t2 = ax ? task - nx : task;
         int fu, fv, k;
-        if (!ax) {
-          const int r = t2 / nl, c = t2 - r * nl;
+        if (!ax) {                                           // line-major, like the y-faces: the faces
+          const int c = t2 / nr, r = t2 - c * nr;            // near an edge line fill few waves
           fv = lo + r; k = lo + c; fu = k;                   // b = (k, fv), a = (k - 1, fv)
         } else {
           const int r = t2 / nr, c = t2 - r * nr;
@@ -599,23 +652,42 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   }
 
   // ---- 4. the block's cells (owners [0, B^2)) -> output, same-rank pushes ------
+  T* const Out = buf[(it + 1) & 1];
+  const bool last = it + 1 == nsteps;
   if (tid < B * B) {
     const unsigned S = (unsigned)a.S;
+    unsigned so = (unsigned)src;
+    asm volatile("" : "+v"(so));
+    if (MULTI) {             // write-through: the next step's readers may sit on another XCD
 #pragma unroll
-    for (int f = 0; f < 4; ++f) *o32(a.out, (unsigned)src + f * S) = Q[f];
-    const int n = a.n, mg = a.mg;
-    const int x = xo + u - R, y = yo + v - R;              // tile-local
-    const int* pm = a.push + (long)tile * 4 * mg * n;
-    int pt[4] = {-1, -1, -1, -1};
-    if (x < mg) pt[0] = pm[(0 * mg + x) * n + y];
-    if (x >= n - mg) pt[1] = pm[(1 * mg + (n - 1 - x)) * n + y];
-    if (y < mg) pt[2] = pm[(2 * mg + y) * n + x];
-    if (y >= n - mg) pt[3] = pm[(3 * mg + (n - 1 - y)) * n + x];
+      for (int f = 0; f < 4; ++f) {
+        T* p = o32(Out, so + f * S);
+        if constexpr (sizeof(T) == 8)
+          __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, Q[f]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        else
+          __hip_atomic_store((gu32*)p, __builtin_bit_cast(unsigned, Q[f]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (pt[k] >= 0) {
+      for (int f = 0; f < 4; ++f) *o32(Out, so + f * S) = Q[f];
+    }
+    if (last) {              // ghost slots of neighbouring tiles: for readers after the launch
+      const int n = a.n, mg = a.mg;
+      const int x = xo + u - R, y = yo + v - R;              // tile-local
+      const int* pm = a.push + (long)tile * 4 * mg * n;
+      int pt[4] = {-1, -1, -1, -1};
+      if (x < mg) pt[0] = pm[(0 * mg + x) * n + y];
+      if (x >= n - mg) pt[1] = pm[(1 * mg + (n - 1 - x)) * n + y];
+      if (y < mg) pt[2] = pm[(2 * mg + y) * n + x];
+      if (y >= n - mg) pt[3] = pm[(3 * mg + (n - 1 - y)) * n + x];
 #pragma unroll
-        for (int f = 0; f < 4; ++f) *o32(a.out, (unsigned)pt[k] + f * S) = Q[f];
+      for (int k = 0; k < 4; ++k) {
+        if (pt[k] >= 0) {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) *o32(Out, (unsigned)pt[k] + f * S) = Q[f];
+        }
       }
     }
     if constexpr (XG) {   // cells other ranks read: straight into their rings, tag xe + 2
@@ -641,10 +713,20 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
       }
     }
   }
-  if constexpr (XG) {
-    if (tid == 0) a.epoch[bid] = xe + 1;
+  if (epoch_on) {
+    // every storing wave drains its stores, then one lane publishes the step
+    if (MULTI) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(a.epoch + bid, xe + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (tid == 0) {
+      a.epoch[bid] = xe + 1;
+    }
   }
+  ++xe;
+  }   // steps
   FSTAMP(3 + 2 * NS);
+  FSTAMP_RT(15);
 }
 
 template <typename T, int NS, int B>
@@ -672,14 +754,34 @@ int launch_fused(const FusedDesc* d, hipStream_t s) {
   a.stamps = d->stamps;
   for (int k = 0; k < 6; ++k) a.links[k] = d->links[k];
   a.local_src = d->local_src;
+  a.nsteps = d->nsteps < 1 ? 1 : d->nsteps;
+  a.prod = d->prod;
+  a.PM = d->PM;
+  if (a.nsteps > 1 && (!a.prod || a.PM <= 0 || a.PM > 64 || !d->epoch || !d->err)) return -7;
   a.mdiv_n = magic_div((unsigned)d->n, (unsigned long long)d->N + 1);
   if (d->xg && (!STSP_XG_TAG || !d->recv || !d->peer_ring || !d->xpush || !d->epoch || !d->err || d->ring <= 0 ||
                 d->K <= 0))
     return -6;
   const dim3 grid(d->nblocks), block(D::NT);
-#define FUSED_LAUNCH(L_)                                                                          \
-  if (d->xg) hipLaunchKernelGGL((fused_step_kernel<T, L_, NS, B, true>), grid, block, 0, s, a);   \
-  else hipLaunchKernelGGL((fused_step_kernel<T, L_, NS, B, false>), grid, block, 0, s, a);
+  if (a.nsteps > 1) {
+    // every block must be resident at once (a waiting block holds its CU)
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return -8;
+    const void* kf = d->xg ? (const void*)fused_step_kernel<T, 0, NS, B, true, true>
+                           : (const void*)fused_step_kernel<T, 0, NS, B, false, true>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kf, D::NT, 0) != hipSuccess) return -8;
+    if ((long)per * cus < d->nblocks) return -9;
+  }
+#define FUSED_LAUNCH(L_)                                                                                  \
+  if (a.nsteps > 1) {                                                                                     \
+    if (d->xg) hipLaunchKernelGGL((fused_step_kernel<T, L_, NS, B, true, true>), grid, block, 0, s, a);   \
+    else hipLaunchKernelGGL((fused_step_kernel<T, L_, NS, B, false, true>), grid, block, 0, s, a);        \
+  } else {                                                                                                \
+    if (d->xg) hipLaunchKernelGGL((fused_step_kernel<T, L_, NS, B, true, false>), grid, block, 0, s, a);  \
+    else hipLaunchKernelGGL((fused_step_kernel<T, L_, NS, B, false, false>), grid, block, 0, s, a);       \
+  }
   switch (d->limiter) {
     case 0: FUSED_LAUNCH(0) break;
     case 1: FUSED_LAUNCH(1) break;

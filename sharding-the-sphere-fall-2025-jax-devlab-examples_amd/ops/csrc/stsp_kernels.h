@@ -120,6 +120,12 @@ typedef struct FusedDesc {
   // loading `src` (one dependent memory round trip less in the prologue)
   int local_src;
   int links[6];
+  // several steps per launch (0 / 1 = one): needs every block co-resident
+  // (checked by the launcher), epoch / err, and prod [nb][PM] (producer blocks of
+  // each block's window, -1 padded, symmetric)
+  int nsteps;
+  const int* prod;
+  int PM;
 } FusedDesc;
 int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stream);
 int stsp_fused_limits(int* gmax, int* cmax);

@@ -1000,9 +1000,15 @@ class FusedKernel:
         assert int(e.plan.push_map.max(initial=-1)) < S
         self.dcode = native.dtype_code(dt)
         self.mem = None
+        # per-block step counters (xGMI tags; waits inside a multi-step launch)
+        self.tens["epoch"] = torch.zeros(nb, dtype=torch.int32, device=dev)
+        self.tens["err"] = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.tens["prod"] = torch.as_tensor(producer_table(P), dtype=torch.int32, device=dev).contiguous()
+        self.timeout_ticks = int(timeout_s * 1e8)
         if X is not None:
             self._setup_exchange(X, timeout_s)
         self.descs = [self._desc(0, 1), self._desc(1, 0)]
+        self._multi = {}          # nsteps -> descriptor (pool[0] -> ... -> pool[nsteps % 2])
         if X is not None:
             self.prime()
 
@@ -1030,15 +1036,12 @@ class FusedKernel:
         self.tens.update({
             "peer_ring": torch.as_tensor(pr, device=dev),
             "xpush": torch.as_tensor(xpush, dtype=torch.int32, device=dev).contiguous(),
-            "epoch": torch.zeros(self.plan.nb, dtype=torch.int32, device=dev),
-            "err": torch.zeros(4, dtype=torch.int32, device=dev),
             "prime_src": torch.as_tensor(psrc, dtype=torch.int32, device=dev),
             "prime_code": torch.as_tensor(pcode, dtype=torch.int32, device=dev),
         })
         self.K = int(xpush.shape[2])
-        self.timeout_ticks = int(timeout_s * 1e8)
 
-    def _desc(self, qi: int, oi: int):
+    def _desc(self, qi: int, oi: int, nsteps: int = 1):
         from . import native
         e, P, tn = self.e, self.plan, self.tens
         p = native.ptr
@@ -1063,6 +1066,12 @@ class FusedKernel:
         d.local_src = 1 if (self.world == 1 and list(e.plan.tiles) == list(range(e.layout.num_tiles))) else 0
         for f in range(6):
             d.links[f] = face_links(f)
+        d.epoch = p(tn["epoch"])
+        d.err = p(tn["err"])
+        d.timeout_ticks = self.timeout_ticks
+        d.nsteps = nsteps
+        d.prod = p(tn["prod"])
+        d.PM = int(tn["prod"].shape[1])
         if self.mem is not None:
             d.xg = 1
             d.ring = self.ring
@@ -1070,9 +1079,16 @@ class FusedKernel:
             d.peer_ring = p(tn["peer_ring"])
             d.xpush = p(tn["xpush"])
             d.K = self.K
-            d.epoch = p(tn["epoch"])
-            d.err = p(tn["err"])
-            d.timeout_ticks = self.timeout_ticks
+        return d
+
+    def multi_desc(self, nsteps: int):
+        """Descriptor of one launch running ``nsteps`` (even) steps from pool[0]
+        (ping-pong inside the kernel; the state ends in pool[0])."""
+        if nsteps < 2 or nsteps % 2:
+            raise ValueError("a multi-step launch runs an even number of steps")
+        d = self._multi.get(nsteps)
+        if d is None:
+            d = self._multi[nsteps] = self._desc(0, 1, nsteps)
         return d
 
     # ---- several ranks: delivery of the current state, error check ----------
@@ -1105,8 +1121,11 @@ class FusedKernel:
             dist.barrier(group=self.group)
 
     def check(self) -> None:
-        if self.mem is not None and int(self.tens["err"][0].item()) != 0:
+        err = int(self.tens["err"][0].item())
+        if err == 1:
             raise RuntimeError("fused step: a peer's window cells did not arrive in time (poll timeout)")
+        if err:
+            raise RuntimeError("fused step: a producer block did not finish its step in time (multi-step launch)")
 
     def close(self) -> None:
         if self.mem is not None:
@@ -1114,15 +1133,16 @@ class FusedKernel:
             self.mem = None
 
     def set_dt(self, dt: float) -> None:
-        for d in self.descs:
+        for d in list(self.descs) + list(self._multi.values()):
             d.dt = dt
 
-    def launch(self, parity: int = 0, stream: Optional[int] = None) -> None:
+    def launch(self, parity: int = 0, stream: Optional[int] = None, nsteps: int = 1) -> None:
         """One fused step from pool[parity] into pool[1 - parity] (the
-        engine's pool list is not touched)."""
+        engine's pool list is not touched); nsteps > 1 (even, parity 0): that
+        many steps in one launch, the state back in pool[0]."""
         from . import native
-        rc = self.lib.stsp_fused_launch(self.dcode, self.descs[parity],
-                                        native.current_stream_handle() if stream is None else stream)
+        d = self.descs[parity] if nsteps == 1 else self.multi_desc(nsteps)
+        rc = self.lib.stsp_fused_launch(self.dcode, d, native.current_stream_handle() if stream is None else stream)
         native.check(rc, "fused step")
 
     def step(self, nsteps: int = 1) -> None:
@@ -1206,6 +1226,33 @@ def neighbour_codes(P: "FusedPlan") -> np.ndarray:
     c16 = (codes & 0xFFFF).astype(np.uint64)
     out = c16[:, 0] | (c16[:, 1] << np.uint64(16)) | (c16[:, 2] << np.uint64(32)) | (c16[:, 3] << np.uint64(48))
     return out.reshape(nb, W * W)
+
+
+def producer_table(P: "FusedPlan") -> np.ndarray:
+    """[nb, PM] int32: the blocks of this rank whose cells each block's window
+    loads (its producers for a step inside a multi-step launch), made
+    symmetric so the same wait also guarantees that every reader of a block's
+    previous state is done before the block overwrites it; -1 padded."""
+    L = P.layout
+    pos = {int(t): k for k, t in enumerate(P.tiles)}
+    sets = [set() for _ in range(P.nb)]
+    for b in range(P.nb):
+        m = P.src[b] >= 0
+        g = P.gid[b][m]
+        if g.size == 0:
+            continue
+        tid, i, j = L.locate(g)
+        li = np.array([pos[int(t)] for t in tid])
+        blk = (li * P.nby + j // P.B) * P.nbx + i // P.B
+        sets[b].update(int(x) for x in np.unique(blk) if int(x) != b)
+    for b in range(P.nb):
+        for c in list(sets[b]):
+            sets[c].add(b)
+    PM = max(1, max(len(x) for x in sets))
+    out = np.full((P.nb, PM), -1, dtype=np.int32)
+    for b, x in enumerate(sets):
+        out[b, :len(x)] = sorted(x)
+    return out
 
 
 def ctypes_limits(L) -> Tuple[int, int]:

@@ -61,6 +61,7 @@ class FusedDesc(ctypes.Structure):
         ("xpush", ctypes.c_void_p), ("K", ctypes.c_int), ("epoch", ctypes.c_void_p), ("err", ctypes.c_void_p),
         ("timeout_ticks", ctypes.c_longlong), ("stamps", ctypes.c_void_p),
         ("local_src", ctypes.c_int), ("links", ctypes.c_int * 6),
+        ("nsteps", ctypes.c_int), ("prod", ctypes.c_void_p), ("PM", ctypes.c_int),
     ]
 
 

@@ -119,7 +119,7 @@ class NativeStepper:
 
     def __init__(self, engine, nccl_comm: Optional[int] = None, use_graph: bool = True,
                  steps_per_graph: int = 30, roctx: bool = False, stream: Optional[torch.cuda.Stream] = None,
-                 xgmi=None, fused=None):
+                 xgmi=None, fused=None, steps_per_launch: int = 1):
         from .hip_compute import HipCompute
         e = engine
         if not isinstance(e.compute, HipCompute):
@@ -146,20 +146,26 @@ class NativeStepper:
         self.send_idx = torch.as_tensor(plan.send_idx, dtype=torch.int32, device=e.device)
         assert (plan.send_idx.size == 0) or int(plan.send_idx.max()) < plan.S
         self.stream = stream or torch.cuda.Stream(device=e.device)
-        # fused: ops/fused.py::FusedKernel, one launch per step (temporal
-        # blocking), ping-pong between pool[0] and pool[1]: the op list covers
-        # two steps
-
-        period = 2 if fused is not None else e.integ.period
+        # fused: ops/fused.py::FusedKernel (temporal blocking), ping-pong between
+        # pool[0] and pool[1]: one launch per step, the op list covers two steps;
+        # or steps_per_launch (even) steps inside one launch, the op list is that
+        # one launch
+        self.spl = 1
+        if fused is not None and steps_per_launch > 1:
+            if steps_per_launch % 2:
+                raise ValueError("steps_per_launch must be even")
+            self.spl = steps_per_launch
+        period = (self.spl if self.spl > 1 else 2) if fused is not None else e.integ.period
         self.period = period
         ops: List[StspOp] = []
         pool = list(e.pool)
         saved_pool = e.pool
-        for k in range(period if fused is not None else 0):
+        fdescs = [] if fused is None else ([fused.multi_desc(self.spl)] if self.spl > 1 else list(fused.descs))
+        for fd in fdescs:
             op = StspOp()
             op.type = OP_FUSED
             op.dtype = fused.dcode
-            op.fused = ctypes.addressof(fused.descs[k])
+            op.fused = ctypes.addressof(fd)
             ops.append(op)
         for _ in range(period if fused is None else 0):
             e.pool = pool
@@ -385,12 +391,20 @@ class NativeStepper:
             e.step_count += full
         if nsteps - full:
             if self.fused is not None:
-                # odd step count: one eager fused step, result copied back to pool[0]
+                # remainder: an even part in one launch, an odd last step copied back to pool[0]
                 cur = torch.cuda.current_stream(e.device)
-                self.fused.launch(0, int(cur.cuda_stream))
-                e.pool[0].copy_(e.pool[1])
-                e.time += e.dt
-                e.step_count += 1
+                rem = nsteps - full
+                if rem >= 2 and self.spl > 1:
+                    self.fused.launch(0, int(cur.cuda_stream), nsteps=rem - rem % 2)
+                elif rem >= 2:
+                    for _ in range(rem // 2):
+                        self.fused.launch(0, int(cur.cuda_stream))
+                        self.fused.launch(1, int(cur.cuda_stream))
+                if rem % 2:
+                    self.fused.launch(0, int(cur.cuda_stream))
+                    e.pool[0].copy_(e.pool[1])
+                e.time += rem * e.dt
+                e.step_count += rem
             else:
                 e.step(nsteps - full)
             self.stats["eager_steps"] += nsteps - full

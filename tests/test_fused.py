@@ -176,6 +176,31 @@ def test_fused_native_graph_equals_eager(nsteps):
     r.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,t,spl,nsteps", [(32, 2, 4, 9), (96, 2, 10, 20), (48, 1, 6, 13)])
+def test_fused_multi_step_launch_equals_single_steps(N, t, spl, nsteps):
+    """Several steps inside one launch (in-kernel producer waits, write-through
+    hand-off, ping-pong buffers): bitwise equal to one launch per step,
+    through NativeStepper graphs (remainders: an even multi-step launch plus
+    one single step), including the ghost slots pushed after the last step."""
+    from stsphere.ops.fused import FusedKernel
+    from stsphere.ops.native_runtime import NativeStepper
+    _, a = _gpu_pair(N, t)
+    _, b = _gpu_pair(N, t)
+    b.dt = a.dt
+    FusedKernel(a).step(nsteps)
+    fk = FusedKernel(b)
+    r = NativeStepper(b, use_graph=True, steps_per_graph=2 * spl, fused=fk, steps_per_launch=spl)
+    r.run(nsteps)
+    torch.cuda.synchronize()
+    fk.check()
+    assert torch.equal(a.tiles_view(), b.tiles_view())
+    assert torch.equal(a.pool[0], b.pool[0])
+    assert b.step_count == nsteps
+    assert r.stats["graph_steps"] == (nsteps // spl) * spl
+    r.close()
+
+
 @pytest.mark.parametrize("N,t,R", [(32, 2, 2), (32, 2, 8), (48, 1, 6), (32, 2, 3)])
 def test_fused_exchange_ranks_equal_one_rank(N, t, R):
     """Several ranks (FusedExchangePlan): each rank's window reads its remote

@@ -55,6 +55,18 @@ def main():
     s1.record()
     torch.cuda.synchronize()
     out["graph_us_per_step"] = s0.elapsed_time(s1) * 1e3 / (2 * a.reps)
+    for spl in (20, 2 * a.reps):
+        r3 = NativeStepper(e, use_graph=True, steps_per_graph=2 * a.reps, fused=fk, steps_per_launch=spl)
+        r3.prepare(2 * a.reps)
+        r3.run(2 * a.reps)
+        torch.cuda.synchronize()
+        s0.record()
+        r3.run(2 * a.reps)
+        s1.record()
+        torch.cuda.synchronize()
+        fk.check()
+        out[f"multi{spl}_us_per_step"] = s0.elapsed_time(s1) * 1e3 / (2 * a.reps)
+        r3.close()
     if a.stage:
         e2 = Engine(ShallowWater("tc5"), L, grid=CubedSphereGrid(a.N), dtype=dt, device="cuda", backend="hip")
         r2 = NativeStepper(e2, use_graph=True, steps_per_graph=2 * a.reps)
@@ -102,6 +114,13 @@ def main():
                       "max": float(blk[:, k].max())}
         out["phases_cycles"] = ph
         P = fk.plan
+        # shader clock from the (memtime, memrealtime) pairs at block start / end
+        dt_rt = (v[:, :, 15] - v[:, :, 14]).astype(np.float64) / 100e6     # seconds (100 MHz)
+        dt_sc = (v[:, :, 9] - v[:, :, 0]).astype(np.float64)
+        ok = dt_rt > 0
+        out["shader_clock_ghz"] = float(np.median(dt_sc[ok] / dt_rt[ok]) / 1e9) if ok.any() else None
+        rt0 = v[:, :, 14][v[:, :, 14] > 0].min()
+        out["kernel_span_us_rt"] = float((v[:, :, 15].max() - rt0) / 100.0)
         out["ghost_entries_max"] = int(P.gcnt.max())
         out["corner_faces_max"] = int(P.ccnt.max())
         out["start_spread"] = float(t0.max() - t0.min())
