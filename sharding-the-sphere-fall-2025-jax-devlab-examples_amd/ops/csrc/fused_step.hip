@@ -460,6 +460,7 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   const int ky0 = (flags & 8) ? -Y0 : -1000, ky1 = (flags & 16) ? N - Y0 : -1000;
 
   for (int it = 0; it < nsteps; ++it) {
+  FSTAMP(13);
   if (it > 0) {
     // wait for the producers' previous step (wave 0 polls, the barrier releases
     // the others), then load this step's window
@@ -478,7 +479,7 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
       }
     }
     __syncthreads();
-    load_state(buf[it & 1], xe);
+    if (tid >= B * B) load_state(buf[it & 1], xe);   // the own cells' new state is still in Q
   }
   if (tid < NX2) {
 #pragma unroll
@@ -507,7 +508,6 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
         }
       }
       __syncthreads();
-      FSTAMP(10 + s);
     }
     // ---- faces ---------------------------------------------------------------
     // EDGE (blocks with a side region): the face's normal is that of the lower
@@ -616,6 +616,7 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
         }
       }
     }
+    FSTAMP(10 + s);          // this wave's faces done (before the barrier)
     __syncthreads();
     FSTAMP(3 + 2 * s);
     // ---- cell updates: owners [0, |square_s|) -----------------------------------

@@ -67,6 +67,24 @@ def main():
         fk.check()
         out[f"multi{spl}_us_per_step"] = s0.elapsed_time(s1) * 1e3 / (2 * a.reps)
         r3.close()
+    # host-timed single runs of 20 steps, like bench.py's timed region
+    import time
+    r4 = NativeStepper(e, use_graph=True, steps_per_graph=20, fused=fk, steps_per_launch=20)
+    r4.prepare(20)
+    host = {"graph": [], "direct": []}
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r4.run(20)
+        torch.cuda.synchronize()
+        host["graph"].append((time.perf_counter() - t0) * 1e6 / 20)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fk.launch(0, nsteps=20)
+        torch.cuda.synchronize()
+        host["direct"].append((time.perf_counter() - t0) * 1e6 / 20)
+    r4.close()
+    out["host_timed_20_us_per_step"] = {k: round(min(v), 3) for k, v in host.items()}
     if a.stage:
         e2 = Engine(ShallowWater("tc5"), L, grid=CubedSphereGrid(a.N), dtype=dt, device="cuda", backend="hip")
         r2 = NativeStepper(e2, use_graph=True, steps_per_graph=2 * a.reps)
@@ -108,7 +126,8 @@ def main():
         ph = {}
         side = edge & ~corner
         mean = lambda m, k: round(float(blk[m, k].mean()), 0) if m.any() else None
-        names = names + [f"s{s}_fix" for s in range(1, 4)]
+        mean2 = lambda arr, m, k: round(float(arr[m, k].mean()), 0) if m.any() else None
+        names = names + [f"s{s}_faces_prebar" for s in range(1, 4)]
         for k, nm in enumerate(names):
             ph[nm] = {"int_mean": mean(~edge, k), "edge_mean": mean(side, k), "corner_mean": mean(corner, k),
                       "max": float(blk[:, k].max())}
@@ -122,6 +141,30 @@ def main():
         rt0 = v[:, :, 14][v[:, :, 14] > 0].min()
         out["kernel_span_us_rt"] = float((v[:, :, 15].max() - rt0) / 100.0)
         out["ghost_entries_max"] = int(P.gcnt.max())
+        # the same inside a 20-step launch: phases of the last step, from its loop top
+        st.zero_()
+        md = fk.multi_desc(20)
+        md.stamps = st.data_ptr()
+        fk.launch(0, nsteps=20)
+        torch.cuda.synchronize()
+        md.stamps = 0
+        fk.check()
+        v2 = st.cpu().numpy().astype(np.int64).reshape(nb, nw, 16)
+        top = v2[:, :, 13].min(1)
+        rel2 = (v2 - top[:, None, None]).max(1)
+        idx = [13, 1, 2, 3, 4, 5, 6, 7, 8, 9]
+        nm2 = ["loop_top", "wait_load_put", "bar"] + sum([[f"s{s}_faces", f"s{s}_upd"] for s in range(1, 4)], []) + ["end"]
+        # per-wave face-phase time (from the stage's start barrier to the wave's last
+        # face task), mean over each block class: which SIMD / wave limits the phase
+        starts = {1: 2, 2: 4, 3: 6}
+        pw = {}
+        for s_ in (1, 2, 3):
+            dtw = v2[:, :, 9 + s_] - v2[:, :, starts[s_]].max(1)[:, None]
+            pw[f"s{s_}"] = {"int": [int(x) for x in dtw[~edge].mean(0)], "corner": [int(x) for x in dtw[corner].mean(0)]}
+        out["multi_wave_face_cycles"] = pw
+        out["multi_last_step_cycles"] = {n_: {"int": mean2(rel2, ~edge, k), "edge": mean2(rel2, side, k),
+                                              "corner": mean2(rel2, corner, k), "max": float(rel2[:, k].max())}
+                                         for n_, k in zip(nm2, idx)}
         out["corner_faces_max"] = int(P.ccnt.max())
         out["start_spread"] = float(t0.max() - t0.min())
         out["end_max"] = float((v[:, :, 9].max(1) - t0.min()).max())
