@@ -237,7 +237,15 @@ def main():
             from stsphere.ops.fused import fused_supported
             probe = Engine(phys_factory(), layout, rank, grid=grid, dtype=dtype, device="cpu", integrator=a.integrator)
             if fused_supported(probe) is None:
-                runtime = "fused"
+                # the fused step recomputes a ring of 2 x 3 cells per block: it wins
+                # where launches and hand-offs dominate (every block resident, so
+                # several steps run per launch); larger grids keep the stage path
+                from stsphere.ops.fused import fused_block
+                B = fused_block(layout.n)
+                nb = len(layout.plan(rank).tiles) * (layout.n // B) ** 2
+                cus = torch.cuda.get_device_properties(device).multi_processor_count if device.type == "cuda" else 256
+                if nb <= cus:
+                    runtime = "fused"
             del probe
     comm = a.comm if world > 1 else "none"
     if world > 1 and runtime == "fused":
