@@ -807,6 +807,9 @@ extern "C" int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stre
   } else if (d->B == 18) {
     if (dtype == 1) return launch_fused<double, 3, 18>(d, stream);
     if (dtype == 0) return launch_fused<float, 3, 18>(d, stream);
+  } else if (d->B == 20) {   // W = 32: the 1024 window cells of one workgroup
+    if (dtype == 1) return launch_fused<double, 3, 20>(d, stream);
+    if (dtype == 0) return launch_fused<float, 3, 20>(d, stream);
   } else {
     return -1;
   }

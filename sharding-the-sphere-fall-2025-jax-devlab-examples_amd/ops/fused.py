@@ -862,7 +862,7 @@ class FusedTorch:
 # Device tables + descriptors of the gfx950 kernel (fused_step.hip)
 # ---------------------------------------------------------------------------
 
-FUSED_BLOCKS = (16, 18)      # block sizes the kernel is instantiated for
+FUSED_BLOCKS = (16, 18, 20)  # block sizes the kernel is instantiated for (preference order)
 
 
 def fused_block(n: int) -> Optional[int]:

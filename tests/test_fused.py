@@ -76,9 +76,10 @@ def test_fused_supported_reasons():
     assert "PLR" in fused_supported(e)
     e = Engine(ShallowWater("tc5"), L, integrator="rk4")
     assert "SSP-RK3" in fused_supported(e)
-    e = Engine(ShallowWater("tc5"), TileLayout(20, 1, 1, ng=2))
-    assert "multiple of 16 or 18" in fused_supported(e)
+    e = Engine(ShallowWater("tc5"), TileLayout(24, 2, 1, ng=2))
+    assert "multiple of 16 or 18 or 20" in fused_supported(e)
     assert fused_supported(Engine(ShallowWater("tc5"), TileLayout(36, 2, 1, ng=2))) is None   # B = 18
+    assert fused_supported(Engine(ShallowWater("tc5"), TileLayout(40, 2, 1, ng=2))) is None   # B = 20
     e = Engine(ShallowWater("tc5"), TileLayout(32, 2, 1, ng=2))
     assert fused_supported(e) is None
 
@@ -98,7 +99,7 @@ def _gpu_pair(N, t, dtype=torch.float64, case="tc5", lim=2):
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,t,case,lim", [(32, 2, "tc5", 2), (48, 1, "tc5", 1), (96, 2, "tc5", 2),
                                           (48, 3, "tc6", 3), (32, 1, "tc2", 0), (36, 2, "tc5", 2),
-                                          (54, 1, "tc2", 1)])
+                                          (54, 1, "tc2", 1), (40, 2, "tc5", 2), (60, 3, "tc6", 2)])
 def test_fused_kernel_fp64_matches_oracle(N, t, case, lim):
     from stsphere.ops.fused import FusedKernel
     ref, hip = _gpu_pair(N, t, case=case, lim=lim)
