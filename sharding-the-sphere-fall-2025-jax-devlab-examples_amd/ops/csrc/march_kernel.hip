@@ -1,0 +1,438 @@
+// Streaming ("march") RK stage of the shallow-water solver for large grids,
+// gfx950 (CDNA4).
+//
+// The block stage kernel (stage_kernel.hip) is built for C96-class grids where
+// every launch is latency-bound: one thread per edge, the window and the fluxes
+// in LDS, two barriers.  On C360 / C720 that shape pays its index arithmetic,
+// its LDS traffic and its barriers for every cell: the fp32 C720 stage was 85 %
+// VALU-busy with only 31 % of the VALU instructions doing floating-point math
+// (docs/ARCHITECTURE.md, profiles/r2_roofline).  Here one wave marches a strip
+// of 60 columns up the tile, one row per iteration:
+//
+//   * lane l owns column x = 60 cs + l - 2 (lanes 0, 1, 62, 63 are the x-halo);
+//     x-neighbours come from the adjacent lanes through DPP wave shifts
+//     (v_mov_b32_dpp wave_shr / wave_shl: no LDS, no barrier);
+//   * y-neighbours stay in registers: the march keeps rows j and j+1 as
+//     primitives (h, v, sqrt(g h)), the half slope of row j and the flux through
+//     the face below row j, and loads one new row per step (prefetched a row
+//     ahead), so every face flux is evaluated exactly once;
+//   * the waves of a workgroup are independent jobs (no LDS, no barrier), so a
+//     CU holds as many marches as its VGPRs allow and hides their loads behind
+//     each other's arithmetic;
+//   * panel edges (models/base.py::reconstruct) are the same treatment as the
+//     block kernel: the ghost strip used for slopes is interpolated along the
+//     neighbour's grid lines, the neighbour's edge state is reconstructed in its
+//     own frame, the wave speeds use the raw cells.  W/E strips are per-row
+//     gathers in the edge waves, S/N strips per-lane gathers at the first and
+//     last rows of the tile.
+//
+// Same inputs and outputs as one stage_kernel launch (StageDesc), same push map
+// for the same-rank ghost strips; PLR limiters only (PPM keeps the block kernel),
+// one rank without remote ghosts.  Compared with the fp64 PyTorch oracle in
+// tests/test_march.py.
+#include "stage_common.h"
+
+namespace {
+
+constexpr int MW = 64;          // lanes per wave
+constexpr int MO = MW - 4;      // output columns per wave
+constexpr int MWPB = 4;         // independent waves (jobs) per workgroup
+
+// Wave-wide lane shifts.  wave_shr:1: lane i <- lane i-1; wave_shl:1: lane i
+// <- lane i+1 (lanes without a source read 0).  DPP moves are 32-bit, so a
+// double is two moves.
+constexpr int DPP_SHR = 0x138, DPP_SHL = 0x130;
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+  int2 p = __builtin_bit_cast(int2, v);
+  p.x = __builtin_amdgcn_update_dpp(0, p.x, CTRL, 0xf, 0xf, false);
+  p.y = __builtin_amdgcn_update_dpp(0, p.y, CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, p);
+}
+template <typename T> __device__ __forceinline__ T shr(T v) { return dpp<DPP_SHR>(v); }
+template <typename T> __device__ __forceinline__ T shl(T v) { return dpp<DPP_SHL>(v); }
+
+// Waves per SIMD the register allocation must allow: fp32 fits 4 (<= 128
+// VGPRs); fp64 needs ~225 VGPRs, 2 waves (asking for 3 spills to scratch).
+#ifndef STSP_MARCH_WPE64
+#define STSP_MARCH_WPE64 2
+#endif
+#ifndef STSP_MARCH_WPE32
+#define STSP_MARCH_WPE32 4
+#endif
+template <typename T, int LIM, int R>
+__global__ __launch_bounds__(MW * MWPB) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 8 ? STSP_MARCH_WPE64 : STSP_MARCH_WPE32)))
+void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
+  pin_args(a);
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // job = (tile, column strip cs, row segment rs), rs fastest: the four waves of
+  // a workgroup march stacked segments of one strip (their halo rows are each
+  // other's rows), and consecutive workgroups share an XCD (xcd_remap)
+  const int gw = xcd_remap(blockIdx.x, gridDim.x) * MWPB + wv;
+  if (gw >= njobs) return;
+  const int rs = gw % nrs, rest = gw / nrs;
+  const int cs = rest % ncs, tile = rest / ncs;
+  const int n = a.n, S = a.S, mg = a.mg, pw = a.pw;
+  const int x = cs * MO + lane - 2;
+  const int xc = x < n + 1 ? x : n + 1;            // lanes past the padded tile load column n + 1
+  const bool outl = (lane >= 2) & (lane < MW - 2) & (x < n);
+  const bool inx = (x >= 0) & (x < n);
+  const int y0 = rs * R;
+  const int y1 = y0 + R < n ? y0 + R : n;
+  constexpr unsigned ES = sizeof(T);
+  const unsigned tb = (unsigned)(tile * pw * pw);
+  const __amdgpu_buffer_rsrc_t rQ = brsrc(a.Q), rX = brsrc(a.X), rO = brsrc(a.out), rG = brsrc(a.cgeo);
+  const unsigned fs = (unsigned)S * ES;              // field stride in bytes (soffset)
+  const T g = a.g;
+
+  auto cell = [&](int cx, int y) -> unsigned { return tb + (unsigned)((y + mg) * pw + (cx + mg)); };
+  auto ldq = [&](unsigned pa, T (&q)[4]) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) q[f] = bld<T>(rQ, pa * ES, f * fs);
+  };
+  // primitive (h, v) + sound speed, as the block kernel's put()
+  auto prim = [&](const T (&q)[4], T (&w)[5]) {
+    const T inv = q[0] != T(0) ? trcp(q[0]) : T(0);
+    w[0] = q[0];
+    w[1] = q[1] * inv;
+    w[2] = q[2] * inv;
+    w[3] = q[3] * inv;
+    w[4] = tsqrt(g * tmax(q[0], T(0)));
+  };
+  // linear interpolation between the primitives of two cells
+  auto interp2 = [&](unsigned p0, unsigned p1, T t, T (&o)[4]) {
+    T q0[4], q1[4], w0[5], w1[5];
+    ldq(p0, q0);
+    ldq(p1, q1);
+    prim(q0, w0);
+    prim(q1, w1);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) o[f] = w0[f] + t * (w1[f] - w0[f]);
+  };
+
+  // ---- panel edges of this wave's part of the tile (wave-uniform) -------------
+  const int pe = a.pedge[tile];
+  const int lnE = n - cs * MO + 2;                   // lane of column n
+  const bool peW = (pe & 1) && cs == 0;
+  const bool peE = (pe & 2) && lnE >= 0 && lnE < MW;
+  const bool peS = (pe & 4) && y0 == 0;
+  const bool peN = (pe & 8) && y1 == n;
+  auto tab = [&](int side, int pos) -> unsigned { return (unsigned)(((tile * 4 + side) * 3 + 0) * n + pos); };
+  // S / N strips (along x, per lane): interpolation of row y at this lane's table pair
+  auto interp_row = [&](int side, int y, T (&o)[4]) {
+    const unsigned ti = tab(side, inx ? x : 0);
+    const int b = a.pe_base[ti];
+    const T t = a.pe_t[ti];
+    interp2(cell(b, y), cell(b + 1, y), t, o);
+  };
+  // W / E strips (along y, one table entry per row): every lane interpolates its
+  // own column between rows b and b + 1
+  auto interp_col = [&](int side, int j, T (&o)[4]) {
+    const unsigned ti = tab(side, j);
+    const int b = a.pe_base[ti];
+    const T t = a.pe_t[ti];
+    interp2(cell(xc, b), cell(xc, b + 1), t, o);
+  };
+
+  // the primitives a row offers to its y-neighbours' slopes: the raw cells,
+  // except a panel-edge ghost row (interpolated)
+  auto wsrow = [&](int y, const T (&c)[5], T (&ws)[4]) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) ws[f] = c[f];
+    if ((peS && y == -1) || (peN && y == n)) {
+      if (inx) {
+        T o[4];
+        interp_row(y < 0 ? 2 : 3, y, o);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) ws[f] = o[f];
+      }
+    }
+  };
+  // the neighbour's state at a S / N panel-edge face, reconstructed in its own
+  // frame from [our edge row interpolated at its grid line | its raw rows]
+  auto nf_row = [&](int side, const T (&c)[5], const T (&r)[5], T (&nf)[4]) {
+    T l[4];
+    interp_row(side, side == 2 ? 0 : n - 1, l);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) nf[f] = c[f] - half_slope<LIM>(c[f] - l[f], r[f] - c[f]);
+  };
+
+  // ---- per-lane constants ------------------------------------------------------
+  const bool xe_ok = (x >= 0) & (x <= n);            // the lane's west face is a tile face
+  T mxc[3], mxe[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    mxc[k] = xe_ok ? *o32(a.mx, (unsigned)((tile * 3 + k) * (n + 1) + x)) : T(0);
+    mxe[k] = shl(mxc[k]);
+  }
+  const T* myt = a.my + (long)tile * 3 * (n + 1);
+  const T* ext = a.ex + (long)tile * n * (n + 1);
+  const T* eyt = a.ey + (long)tile * (n + 1) * n;
+  const int* pm = a.push + (long)tile * 4 * mg * n;
+  const bool need_x = (a.a0 != T(0)) || (a.acc_out && a.c1 != T(0));
+  const bool need_acc = a.acc_out && a.acc_in && (a.c0 != T(0));
+
+  // ---- prologue: rows y0-2 .. y0+1, the flux through the face below row y0 -----
+  T cA[5], cB[5], hsA[4], Gs[4];
+  T Ls;                                              // length of the face below row j
+  {
+    T q[4], cm2[5], cm1[5];
+    ldq(cell(xc, y0 - 2), q); prim(q, cm2);
+    ldq(cell(xc, y0 - 1), q); prim(q, cm1);
+    ldq(cell(xc, y0), q);     prim(q, cA);
+    ldq(cell(xc, y0 + 1), q); prim(q, cB);
+    T wsm2[4], wsm1[4], ws0[4], ws1[4];
+    wsrow(y0 - 2, cm2, wsm2);
+    wsrow(y0 - 1, cm1, wsm1);
+    wsrow(y0, cA, ws0);
+    wsrow(y0 + 1, cB, ws1);
+    T wl[4], wr[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      hsA[f] = half_slope<LIM>(cA[f] - wsm1[f], ws1[f] - cA[f]);
+      wl[f] = cm1[f] + half_slope<LIM>(cm1[f] - wsm2[f], ws0[f] - cm1[f]);
+      wr[f] = cA[f] - hsA[f];
+    }
+    if (peS && y0 == 0) nf_row(2, cm1, cm2, wl);     // the face below row 0 is a panel edge
+    if (peN && y0 + 1 == n) { /* row y0 + 1 == n: its state enters only the loop's face */ }
+    Ls = inx ? eyt[(long)y0 * n + x] : T(0);
+    swe_flux<T>(wl, wr, cm1, cA, myt[0 * (n + 1) + y0], myt[1 * (n + 1) + y0], myt[2 * (n + 1) + y0], Ls, g, Gs);
+  }
+  T qn[4];                                           // raw row j + 2, loaded one step ahead
+  ldq(cell(xc, y0 + 2), qn);
+
+  for (int j = y0; j < y1; ++j) {
+    T cC[5];
+    prim(qn, cC);
+    if (j + 1 < y1) ldq(cell(xc, j + 3), qn);        // prefetch (row j + 3 <= n + 1)
+    // own-row operands of row j (needed after the fluxes)
+    const unsigned pc = cell(xc, j);
+    T qo[4], xs[4], acs[4], rec[8];
+    ldq(pc, qo);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) { xs[f] = T(0); acs[f] = T(0); }
+    if (need_x) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) xs[f] = bld<T>(rX, pc * ES, f * fs);
+    }
+    if (need_acc) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acs[f] = *o32(a.acc_in + f * S, pc);
+    }
+    const unsigned gc = (unsigned)((tile * n + j) * n + (inx ? x : 0));
+    bld_rec8<T>(rG, gc * 8u * ES, rec);
+    const T Lw = xe_ok ? ext[(long)j * (n + 1) + x] : T(0);
+    const T Ln = inx ? eyt[(long)(j + 1) * n + x] : T(0);
+    const T my0 = myt[0 * (n + 1) + j + 1], my1 = myt[1 * (n + 1) + j + 1], my2 = myt[2 * (n + 1) + j + 1];
+    const T ms0 = myt[0 * (n + 1) + j], ms1 = myt[1 * (n + 1) + j], ms2 = myt[2 * (n + 1) + j];
+
+    // ---- y: slope of row j + 1, flux through the face above row j --------------
+    T hsB[4], Gn[4];
+    {
+      T wsC[4];
+      wsrow(j + 2, cC, wsC);
+      T wl[4], wr[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        hsB[f] = half_slope<LIM>(cB[f] - cA[f], wsC[f] - cB[f]);
+        wl[f] = cA[f] + hsA[f];
+        wr[f] = cB[f] - hsB[f];
+      }
+      if (peN && j + 1 == n) nf_row(3, cB, cC, wr);
+      swe_flux<T>(wl, wr, cA, cB, my0, my1, my2, Ln, g, Gn);
+    }
+
+    // ---- x: faces of row j across the lanes ------------------------------------
+    T Fw[4], Fe[4];
+    {
+      T ws[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) ws[f] = cA[f];
+      T giW[4] = {T(0), T(0), T(0), T(0)}, giE[4] = {T(0), T(0), T(0), T(0)};
+      if (peW) {
+        if (x == -1 || x == 0) interp_col(0, j, giW);   // lane x = -1: the ghost; x = 0: own column 0
+        if (x == -1) {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) ws[f] = giW[f];
+        }
+      }
+      if (peE) {
+        if (x == n || x == n - 1) interp_col(1, j, giE);
+        if (x == n) {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) ws[f] = giE[f];
+        }
+      }
+      T fP[4], fM[4], wm[4], wp[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        wm[f] = shr(ws[f]);
+        wp[f] = shl(ws[f]);
+        const T hs = half_slope<LIM>(cA[f] - wm[f], wp[f] - cA[f]);
+        fP[f] = cA[f] + hs;
+        fM[f] = cA[f] - hs;
+      }
+      if (peW) {
+        T gp[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) gp[f] = shl(giW[f]);   // column 0 at the ghost's grid line
+        if (x == -1) {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) fP[f] = cA[f] - half_slope<LIM>(cA[f] - gp[f], wm[f] - cA[f]);
+        }
+      }
+      if (peE) {
+        T gp[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) gp[f] = shr(giE[f]);   // column n - 1
+        if (x == n) {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) fM[f] = cA[f] - half_slope<LIM>(cA[f] - gp[f], wp[f] - cA[f]);
+        }
+      }
+      T wl[4], cl[5];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) wl[f] = shr(fP[f]);
+#pragma unroll
+      for (int f = 0; f < 5; ++f) cl[f] = shr(cA[f]);
+      swe_flux<T>(wl, fM, cl, cA, mxc[0], mxc[1], mxc[2], Lw, g, Fw);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) Fe[f] = shl(Fw[f]);
+    }
+    const T Le = shl(Lw);
+
+    // ---- divergence, sources, RK combination, tangent projection, stores --------
+    if (outl) {
+      const T iA = rec[0], r0 = rec[1], r1 = rec[2], r2 = rec[3];
+      T dq[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) dq[f] = -((Fe[f] - Fw[f]) + (Gn[f] - Gs[f])) * iA;
+      const T fc = a.omega2 * r2;
+      const T h = qo[0];
+      const T cor[3] = {r1 * qo[3] - r2 * qo[2], r2 * qo[1] - r0 * qo[3], r0 * qo[2] - r1 * qo[1]};
+      const T pb = T(0.5) * g * h * h * iA, gh = g * h;
+      const T mn[3] = {my0, my1, my2}, ms[3] = {ms0, ms1, ms2};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const T Sk = Le * mxe[k] - Lw * mxc[k] + Ln * mn[k] - Ls * ms[k];
+        const T src = -fc * cor[k] + pb * Sk - gh * rec[4 + k];
+        dq[1 + k] += src;
+      }
+      T o[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        T base = T(0);
+        if (a.a1 != T(0)) base = a.a1 * qo[f];
+        if (a.a0 != T(0)) base += a.a0 * xs[f];
+        o[f] = a.a2 * a.dt * dq[f] + base;
+      }
+      {
+        const T d = o[1] * r0 + o[2] * r1 + o[3] * r2;
+        o[1] -= d * r0; o[2] -= d * r1; o[3] -= d * r2;
+      }
+      if (a.acc_out) {
+        T p[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) p[f] = a.c2 * a.dt * dq[f];
+        if (a.c1 != T(0)) {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) p[f] += a.c1 * xs[f];
+        }
+        if (need_acc) {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) p[f] += a.c0 * acs[f];
+        }
+        const T d = p[1] * r0 + p[2] * r1 + p[3] * r2;
+        p[1] -= d * r0; p[2] -= d * r1; p[3] -= d * r2;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) *o32(a.acc_out + f * S, pc) = p[f];
+      }
+#pragma unroll
+      for (int f = 0; f < 4; ++f) bst<0>(o[f], rO, pc * ES, f * fs);
+      // same-rank ghost pushes (push map, as the block kernel)
+      int pt[4] = {-1, -1, -1, -1};
+      if (x < mg) pt[0] = pm[(0 * mg + x) * n + j];
+      if (x >= n - mg) pt[1] = pm[(1 * mg + (n - 1 - x)) * n + j];
+      if (j < mg) pt[2] = pm[(2 * mg + j) * n + x];
+      if (j >= n - mg) pt[3] = pm[(3 * mg + (n - 1 - j)) * n + x];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (pt[k] >= 0) {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) bst<0>(o[f], rO, (unsigned)pt[k] * ES, f * fs);
+        }
+      }
+    }
+    // ---- advance the march -----------------------------------------------------
+#pragma unroll
+    for (int f = 0; f < 5; ++f) { cA[f] = cB[f]; cB[f] = cC[f]; }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) { hsA[f] = hsB[f]; Gs[f] = Gn[f]; }
+    Ls = Ln;
+  }
+}
+
+template <typename T, int LIM, int R>
+int march_l(const StageDesc* d, hipStream_t s) {
+  Args<T> a = make_args<T>(d);
+  const int ncs = (d->n + MO - 1) / MO, nrs = (d->n + R - 1) / R;
+  const int njobs = d->ntile * ncs * nrs;
+  const int nb = (njobs + MWPB - 1) / MWPB;
+  hipLaunchKernelGGL((march_kernel<T, LIM, R>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+  return (int)hipGetLastError();
+}
+
+template <typename T, int R>
+int march_r(const StageDesc* d, hipStream_t s) {
+  switch (d->limiter) {
+    case 0: return march_l<T, 0, R>(d, s);
+    case 1: return march_l<T, 1, R>(d, s);
+    case 2: return march_l<T, 2, R>(d, s);
+    case 3: return march_l<T, 3, R>(d, s);
+  }
+  return -11;      // PPM: the block kernel
+}
+
+template <typename T>
+int march_t(int rows, const StageDesc* d, hipStream_t s) {
+  switch (rows) {
+    case 8: return march_r<T, 8>(d, s);
+    case 16: return march_r<T, 16>(d, s);
+    case 32: return march_r<T, 32>(d, s);
+  }
+  return -2;
+}
+
+// DPP lane-shift probe (tests/test_march.py): out[0][i] = lane i-1's value,
+// out[1][i] = lane i+1's, for one wave of doubles and one of floats
+__global__ void dpp_probe_kernel(const double* in, double* out, float* outf) {
+  const int i = threadIdx.x;
+  out[i] = shr(in[i]);
+  out[64 + i] = shl(in[i]);
+  outf[i] = shr((float)in[i]);
+  outf[64 + i] = shl((float)in[i]);
+}
+
+}  // namespace
+
+// Rows per wave `rows` (8, 16, 32).  Shallow water, PLR, one rank with every
+// ghost local (no remote ghosts, no xGMI, no block list).
+extern "C" int stsp_march_launch(int dtype, int rows, const StageDesc* d, hipStream_t stream) {
+  if (d->xg || d->remote || d->blocks) return -13;
+  if (d->pw != d->n + 2 * d->mg || d->mg < 2 || d->n < 2) return -5;
+  if (!d->pedge || !d->pe_base || !d->pe_t || !d->push || !d->cgeo || !d->mx || !d->my || !d->ex || !d->ey)
+    return -12;
+  if (dtype == 1) return march_t<double>(rows, d, stream);
+  if (dtype == 0) return march_t<float>(rows, d, stream);
+  return -4;
+}
+
+extern "C" int stsp_dpp_probe(const double* in, double* out, float* outf, hipStream_t stream) {
+  hipLaunchKernelGGL(dpp_probe_kernel, dim3(1), dim3(64), 0, stream, in, out, outf);
+  return (int)hipGetLastError();
+}

@@ -1004,7 +1004,11 @@ __global__ __launch_bounds__(256) void copy_index_kernel(const T* __restrict__ s
 
 }  // namespace
 
+extern "C" int stsp_march_launch(int dtype, int rows, const StageDesc* d, hipStream_t stream);
+
+// bx == 64: the streaming shallow-water stage (march_kernel.hip), by = rows per wave
 extern "C" int stsp_stage_launch(int phys, int dtype, int bx, int by, const StageDesc* d, hipStream_t stream) {
+  if (bx == 64) return phys == 2 ? stsp_march_launch(dtype, by, d, stream) : -2;
   if (dtype == 1) return launch_d<double>(phys, bx, by, d, stream);
   if (dtype == 0) return launch_d<float>(phys, bx, by, d, stream);
   return -4;

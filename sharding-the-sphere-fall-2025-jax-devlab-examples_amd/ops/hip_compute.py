@@ -19,6 +19,14 @@ from . import native
 from ..models.integrators import Stage
 
 BLOCK_SHAPES = ((16, 16), (32, 8), (16, 8), (8, 16), (8, 8))
+# The streaming stage (ops/csrc/march_kernel.hip): (64, R) = one wave marches 60
+# columns up R rows of a tile.  Shallow water with a PLR limiter, one rank
+# without remote ghosts.
+MARCH_SHAPES = ((64, 8), (64, 16), (64, 32))
+
+
+def march_supported(phys_id: int, limiter: int, remote: bool) -> bool:
+    return phys_id == 2 and limiter != 4 and not remote
 
 
 def block_threads_formula(bx: int, by: int, w10: bool = True) -> int:
@@ -125,10 +133,18 @@ class HipCompute:
             bx, by = choose_block(n, T, cus, getattr(phys, "limiter", 0), torch.tensor([], dtype=e.dtype).element_size())
         else:
             bx, by = e.block
-        if (bx, by) not in BLOCK_SHAPES:
+        self.march = (bx, by) in MARCH_SHAPES
+        if self.march:
+            if not march_supported(self.phys_id, int(phys.kernel_params().get("limiter", 0)), plan.num_recv > 0):
+                raise ValueError("the streaming stage (block (64, R)) runs shallow water with a PLR limiter "
+                                 "on a rank without remote ghosts")
+        elif (bx, by) not in BLOCK_SHAPES:
             raise ValueError(f"unsupported block shape {(bx, by)}")
         self.bx, self.by = bx, by
-        self.nbx, self.nby = -(-n // bx), -(-n // by)
+        if self.march:   # jobs: (tile, 60-column strip, R-row segment), four per workgroup
+            self.nbx, self.nby = -(-n // 60), -(-n // by)
+        else:
+            self.nbx, self.nby = -(-n // bx), -(-n // by)
         self.nblocks = T * self.nbx * self.nby
         t = e.tens
         F, S = phys.F, plan.S

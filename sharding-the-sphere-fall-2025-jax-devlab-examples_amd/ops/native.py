@@ -91,6 +91,8 @@ def load(build_if_missing: bool = True):
         L.stsp_pack_launch.restype = ci
         L.stsp_copy_index_launch.argtypes = [ci, vp, vp, vp, vp, ci, ci, cl, cl, vp]
         L.stsp_copy_index_launch.restype = ci
+        L.stsp_dpp_probe.argtypes = [vp, vp, vp, vp]
+        L.stsp_dpp_probe.restype = ci
         L.stsp_fused_launch.argtypes = [ci, ctypes.POINTER(FusedDesc), vp]
         L.stsp_fused_launch.restype = ci
         L.stsp_fused_limits.argtypes = [ctypes.POINTER(ci), ctypes.POINTER(ci)]

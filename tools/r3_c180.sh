@@ -9,3 +9,5 @@ for v in "--N 180 --tiles-per-edge 3 --runtime fused" "--N 180 --tiles-per-edge 
   timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 $v > $OUT/b.log 2>&1 || { tail -5 $OUT/b.log; exit 4; }
   echo "$v :: $(tail -n 1 $OUT/b.log | cut -c1-330)" | tee -a $OUT/c180.log
 done
+timeout -k 10 200 python -u tools/launch_probe.py --N 96 --t 2 --steps 20 --reps 30 > $OUT/launch_probe.json 2> $OUT/launch_probe.err || { tail -5 $OUT/launch_probe.err; exit 5; }
+cat $OUT/launch_probe.json
