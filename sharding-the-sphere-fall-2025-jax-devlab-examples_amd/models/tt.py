@@ -19,8 +19,9 @@ MI355X runs on the matrix cores through hipBLASLt / rocSOLVER):
                     factors grow to rank 3r, then QR + SVD truncation back to
                     <= r (rank-adaptive with a tolerance).  ``backend="hip"``
                     runs the step on the gfx950 kernels of ops/tt_ops.py
-                    (rank-2r expansion, MFMA Gram matrices, host k x k
-                    eigen/SVD, MFMA tall-skinny products)
+                    (rank-2r expansion, CholeskyQR3 with MFMA Gram matrices,
+                    the shifted-Cholesky kernel and MFMA tall-skinny
+                    products; the k x k core SVD on the host)
 * ``CubedSphereLowRankDiffusion``: the same factored diffusion on all six
                     panels of the cube, coupled through the cube's halo in
                     factored form (each panel side's ghost strip is gathered as
@@ -203,6 +204,85 @@ def recompress(A: torch.Tensor, B: torch.Tensor, eps: float, max_rank: Optional[
     return LowRankField(qa @ (u[:, :r] * s[:r]), qb @ vh[:r].T)
 
 
+def cholqr3_shift(N: int, k: int, dtype) -> float:
+    """Shift coefficient of shifted CholeskyQR (Fukaya, Kannan, Nakatsukasa,
+    Yamamoto, Yanagisawa 2020): s = 11 (N k + k (k + 1)) u trace(G)."""
+    return 11.0 * (N * k + k * (k + 1)) * (torch.finfo(dtype).eps / 2)
+
+
+def cholqr3(X: torch.Tensor, backend: str = "torch"):
+    """X [N, k] = Q R by three shifted CholeskyQR passes: Q orthonormal to
+    working precision (the Gram/eigen route stops at sqrt(eps)), every pass a
+    Gram matrix, a k x k Cholesky and a tall-skinny product.  Pass 1 is
+    shifted; passes 2 and 3 shift only where a pivot fails, which keeps the
+    factorisation defined for rank-deficient X (the expanded factors repeat
+    columns): X = Q R still holds and Q's near-null directions carry no
+    weight in a product.  backend "hip": MFMA Gram and
+    products (ops/tt_ops.gram / tsmm) and the one-workgroup Cholesky + inverse
+    kernel (tt_ops.chol_inv), no host round trip.  Returns (Q, R, info) with
+    info a device tensor, nonzero where a pivot failed."""
+    N, k = X.shape
+    c = cholqr3_shift(N, k, X.dtype)
+    Q, R, infos = X, None, []
+    for p in range(3):
+        # pass 1 always shifted; passes 2 and 3 plain unless a pivot fails
+        if backend == "hip":
+            from ..ops import tt_ops
+            G = tt_ops.gram(Q, Q)
+            Rk, Rik, info = tt_ops.chol_inv(G, c if p == 0 else -c)
+            Rk = Rk[0]
+            Q = tt_ops.tsmm(Q, Rik[0])
+        else:
+            G = Q.T @ Q
+            eye = torch.eye(k, dtype=X.dtype, device=X.device)
+            Lc, info = torch.linalg.cholesky_ex(G + (c * torch.trace(G)) * eye if p == 0 else G)
+            if p > 0 and int(info) != 0:
+                Lc, info = torch.linalg.cholesky_ex(G + (c * torch.trace(G)) * eye)
+            Rk = Lc.T
+            Q = torch.linalg.solve_triangular(Rk, Q, upper=True, left=False)
+            info = info.reshape(1).to(torch.int32)
+        R = Rk if R is None else Rk @ R
+        infos.append(info)
+    return Q, R, torch.cat(infos)
+
+
+def recompress_many(pairs, eps: float, max_rank: Optional[int], backend: str = "torch") -> List[LowRankField]:
+    """Recompress several products A_i B_i^T at once: CholeskyQR3 of every
+    factor on the device, the k x k cores R_a R_b^T copied to the host in ONE
+    transfer (with the pivot flags), an SVD and truncation per core there, and
+    the truncated factors Q_a (U S)_r, Q_b V_r back on the device."""
+    qs, cores, infos = [], [], []
+    for A, B in pairs:
+        qa, ra, ia = cholqr3(A, backend)
+        qb, rb, ib = cholqr3(B, backend)
+        qs.append((qa, qb))
+        cores.append((ra @ rb.T).reshape(-1))
+        infos += [ia, ib]
+    flat = torch.cat(cores + [torch.cat(infos).to(cores[0].dtype)]).double().cpu()
+    nflag = sum(int(i.numel()) for i in infos)
+    if bool((flat[flat.numel() - nflag:] != 0).any()):
+        raise RuntimeError("CholeskyQR: a shifted Cholesky pivot failed (non-finite factors?)")
+    out, o = [], 0
+    for (qa, qb), (A, B) in zip(qs, pairs):
+        ka, kb = A.shape[1], B.shape[1]
+        C = flat[o:o + ka * kb].view(ka, kb).numpy()
+        o += ka * kb
+        u, sv, vt = np.linalg.svd(C)
+        tail = np.cumsum((sv * sv)[::-1])[::-1]
+        ok = np.nonzero(tail <= (eps * eps) * max(tail[0], 1e-300))[0]
+        r = max(1, int(ok[0]) if ok.size else len(sv))
+        if max_rank is not None:
+            r = min(r, max_rank)
+        Xa = torch.as_tensor(np.ascontiguousarray(u[:, :r] * sv[:r]), dtype=A.dtype, device=A.device)
+        Xb = torch.as_tensor(np.ascontiguousarray(vt[:r].T), dtype=B.dtype, device=B.device)
+        if backend == "hip":
+            from ..ops import tt_ops
+            out.append(LowRankField(tt_ops.tsmm(qa, Xa), tt_ops.tsmm(qb, Xb)))
+        else:
+            out.append(LowRankField(qa @ Xa, qb @ Xb))
+    return out
+
+
 def second_difference(n: int, h: float, bc: str = "dirichlet", dtype=torch.float64, device="cpu") -> torch.Tensor:
     D = torch.zeros((n, n), dtype=dtype, device=device)
     i = torch.arange(n, device=device)
@@ -223,8 +303,14 @@ class LowRankDiffusion:
 
     def __init__(self, N: int, L: float = 1.0, kappa: float = 1.0, bc: str = "dirichlet",
                  eps: float = 1e-10, max_rank: Optional[int] = None, dtype=torch.float64, device="cpu",
-                 backend: str = "torch", substeps: int = 1):
+                 backend: str = "torch", substeps: int = 1, qr: str = "cholqr3"):
         self.h = L / (N + 1) if bc == "dirichlet" else L / N
+        # hip recompression: "cholqr3" (device CholeskyQR3, machine-precision
+        # factors, one host transfer of the k x k core) or "gram" (the native
+        # Gram/eigen step, ~sqrt(eps) accuracy; kept for comparison)
+        if qr not in ("cholqr3", "gram"):
+            raise ValueError(f"unknown qr {qr!r}")
+        self.qr = qr
         self.bc = bc
         self.kappa = kappa
         self.eps = eps
@@ -245,8 +331,10 @@ class LowRankDiffusion:
 
     def step(self, U: LowRankField, dt: float) -> LowRankField:
         """``substeps`` explicit steps of size dt, one recompression."""
-        if self.backend == "hip":
+        if self.backend == "hip" and self.qr == "gram":
             return self._step_hip(U, dt)
+        if self.backend == "hip":
+            return self._step_hip_cqr(U, dt)
         c = dt * self.kappa
         if self.substeps == 1:
             A = torch.cat([U.A, c * (self.D @ U.A), c * U.A], dim=1)
@@ -256,6 +344,22 @@ class LowRankDiffusion:
         for _ in range(self.substeps):     # exact rank-doubling form [A, c D A] [B + c D B, B]^T
             A, B = torch.cat([A, c * (self.D @ A)], dim=1), torch.cat([B + c * (self.D @ B), B], dim=1)
         return recompress(A, B, self.eps, self.max_rank)
+
+    def _step_hip_cqr(self, U: LowRankField, dt: float) -> LowRankField:
+        """The rank-doubling form [A, c D A] [B + c D B, B]^T per substep on the
+        device (ops/tt_ops.expand), then one CholeskyQR3 recompression
+        (``recompress_many``: MFMA Gram / product kernels, the k x k shifted
+        Cholesky kernel, one host transfer of the core)."""
+        from ..ops import tt_ops
+        c = dt * self.kappa
+        ih2 = 1.0 / (self.h * self.h)
+        per = self.bc == "periodic"
+        A, B = U.A.contiguous(), U.B.contiguous()
+        if (A.shape[1] << self.substeps) > 64:
+            raise ValueError(f"hip low-rank step: rank {A.shape[1]} x 2^{self.substeps} substeps exceeds 64 columns")
+        for _ in range(self.substeps):
+            A, B = tt_ops.expand(A, 1.0, 0.0, 0.0, c, ih2, per), tt_ops.expand(B, 1.0, c, 1.0, 0.0, ih2, per)
+        return recompress_many([(A, B)], self.eps, self.max_rank, "hip")[0]
 
     def _step_hip(self, U: LowRankField, dt: float) -> LowRankField:
         """Same update as ``step`` with the rank-2r form
@@ -348,16 +452,21 @@ class CubedSphereLowRankDiffusion:
     symmetric, so the total sum (mass) is conserved up to the truncation.
 
     backend "torch": thin QRs + a k x k SVD (rocBLAS / rocSOLVER on the GPU);
-    backend "hip": the MFMA Gram kernels (ops/tt_ops.gram), the native k x k
-    core (stsp_tt_core, one host round trip for all six panels) and the MFMA
-    tall-skinny products (ops/tt_ops.tsmm).  ``dense_step`` is the N x N
+    backend "hip": CholeskyQR3 of every factor on the device (MFMA Gram and
+    tall-skinny products, the shifted-Cholesky kernel), one host transfer of
+    the six k x k cores per step (``recompress_many``); qr="gram" keeps the
+    earlier Gram/eigen route (native k x k core, ~sqrt(eps) accuracy).  ``dense_step`` is the N x N
     six-panel reference of the same operator."""
 
     def __init__(self, N: int, kappa: float = 1.0, L: float = 1.0, eps: float = 1e-10,
-                 max_rank: Optional[int] = None, dtype=torch.float64, device="cpu", backend: str = "torch"):
+                 max_rank: Optional[int] = None, dtype=torch.float64, device="cpu", backend: str = "torch",
+                 qr: str = "cholqr3"):
         from ..parallel.layout import TileLayout
         if backend not in ("torch", "hip"):
             raise ValueError(f"unknown backend {backend!r}")
+        if qr not in ("cholqr3", "gram"):
+            raise ValueError(f"unknown qr {qr!r}")
+        self.qr = qr
         self.N, self.kappa, self.h = N, kappa, L / N
         self.eps, self.max_rank, self.backend = eps, max_rank, backend
         self.dtype, self.device = dtype, torch.device(device)
@@ -440,6 +549,9 @@ class CubedSphereLowRankDiffusion:
         ex = self.expanded(F, dt)
         if self.backend == "torch":
             return [recompress(Ah, Bh, self.eps, self.max_rank) for Ah, Bh in ex]
+        if self.qr == "cholqr3":
+            self.stats["host_syncs"] += 1
+            return recompress_many(ex, self.eps, self.max_rank, "hip")
         return self._recompress_hip(ex)
 
     def _recompress_hip(self, ex) -> List[LowRankField]:

@@ -455,6 +455,89 @@ int lr_core(int k, const double* Ga, const double* Gb, double eps, int max_rank,
   return rn;
 }
 
+
+// ---------------------------------------------------------------------------
+// Shifted CholeskyQR (Fukaya et al. 2020) for the factored step's tall-skinny
+// factors: X = Q R with Q orthonormal to working precision.  One pass is
+//   G = X^T X (gram, MFMA),  G + s I = R^T R,  Q = X R^-1 (tsmm, MFMA)
+// with s = shift_c * trace(G); three passes (CholeskyQR3) give Q to machine
+// precision where the Gram/eigen route stopped at sqrt(eps), and the shift in
+// every pass keeps the Cholesky defined when X is (numerically) rank deficient
+// (the duplicated columns of the expanded factors): X = Q R still holds, and
+// Q's near-null directions carry no weight in the product, so the truncation
+// bound of the core SVD is unchanged.
+//
+// This kernel is the k x k part of one pass: one 64-thread workgroup per
+// matrix (batch = blockIdx.x), G in LDS, right-looking Cholesky (thread c owns
+// column c), then R^-1 by back substitution (thread c owns column c of the
+// inverse).  info[b] = j + 1 if pivot j was not positive (left for the host to
+// report; the factor is then unusable).
+template <typename T>
+__global__ __launch_bounds__(64) void chol_inv_kernel(const T* __restrict__ G, int ldg, long sg, T* __restrict__ R,
+                                                      T* __restrict__ Ri, int ldr, long sr, int k, double shift_c,
+                                                      int* __restrict__ info) {
+  __shared__ T a[64][65];
+  __shared__ T xi[64][65];
+  __shared__ T tr;
+  __shared__ int piv;
+  const int b = blockIdx.x, t = threadIdx.x;
+  G += b * sg;
+  R += b * sr;
+  Ri += b * sr;
+  // shift_c < 0: try the plain Cholesky first and shift (by |shift_c|) only
+  // if a pivot fails (CholeskyQR passes 2 and 3: orthonormal to eps when the
+  // factor is well conditioned, defined when it is rank deficient)
+  const bool adaptive = shift_c < 0;
+  const T sc = T(adaptive ? -shift_c : shift_c);
+  int bad = 0;
+  for (int attempt = adaptive ? 0 : 1; attempt < 2; ++attempt) {
+    if (t < k)
+      for (int i = 0; i < k; ++i) a[i][t] = G[(long)i * ldg + t];
+    __syncthreads();
+    if (t == 0) {
+      T s = T(0);
+      for (int i = 0; i < k; ++i) s += a[i][i];
+      tr = s;
+      piv = 0;
+    }
+    __syncthreads();
+    if (attempt == 1 && t < k) a[t][t] += sc * tr;
+    __syncthreads();
+    for (int j = 0; j < k; ++j) {
+      if (t == 0) {
+        T d = a[j][j];
+        if (!(d > T(0))) { if (!piv) piv = j + 1; d = T(1); }
+        a[j][j] = sqrt(d);
+      }
+      __syncthreads();
+      if (t > j && t < k) a[j][t] /= a[j][j];
+      __syncthreads();
+      if (t > j && t < k) {
+        const T rt = a[j][t];
+        for (int i = j + 1; i <= t; ++i) a[i][t] -= a[j][i] * rt;
+      }
+      __syncthreads();
+    }
+    bad = piv;
+    __syncthreads();
+    if (!bad) break;
+  }
+  // column c of R^-1: x[c][c] = 1 / R[c][c], x[i][c] = -(sum_{i<l<=c} R[i][l] x[l][c]) / R[i][i]
+  if (t < k) {
+    xi[t][t] = T(1) / a[t][t];
+    for (int i = t - 1; i >= 0; --i) {
+      T s = T(0);
+      for (int l = i + 1; l <= t; ++l) s += a[i][l] * xi[l][t];
+      xi[i][t] = -s / a[i][i];
+    }
+    for (int i = 0; i < k; ++i) {
+      R[(long)i * ldr + t] = i <= t ? a[i][t] : T(0);
+      Ri[(long)i * ldr + t] = i <= t ? xi[i][t] : T(0);
+    }
+  }
+  if (t == 0) info[b] = bad;
+}
+
 }  // namespace
 
 extern "C" {
@@ -474,6 +557,24 @@ int stsp_tt_gram(int dtype, const void* A, int lda, const void* B, int ldb, int 
   if (dtype == 1) return gram_t<double>(A, lda, B, ldb, N, k, m, work, P, C, ldc, alpha, stream);
   if (dtype == 0) return gram_t<float>(A, lda, B, ldb, N, k, m, work, P, C, ldc, alpha, stream);
   return -4;
+}
+
+// Batched shifted Cholesky + factor inverse (chol_inv_kernel): for b < batch,
+// G_b + shift_c trace(G_b) I = R_b^T R_b, Ri_b = R_b^-1 (k <= 64, row-major;
+// shift_c < 0: unshifted unless a pivot fails, then shifted by |shift_c|,
+// batch strides sg / sr in elements), info[b] = 0 or the failing pivot + 1.
+int stsp_tt_chol_inv(int dtype, const void* G, int ldg, long sg, void* R, void* Ri, int ldr, long sr, int k,
+                     int batch, double shift_c, int* info, hipStream_t stream) {
+  if (k < 1 || k > 64 || batch < 1) return -1;
+  if (dtype == 1)
+    hipLaunchKernelGGL(chol_inv_kernel<double>, dim3(batch), dim3(64), 0, stream, (const double*)G, ldg, sg,
+                       (double*)R, (double*)Ri, ldr, sr, k, shift_c, info);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(chol_inv_kernel<float>, dim3(batch), dim3(64), 0, stream, (const float*)G, ldg, sg, (float*)R,
+                       (float*)Ri, ldr, sr, k, shift_c, info);
+  else
+    return -4;
+  return (int)hipGetLastError();
 }
 
 // C[N][m] (ldc) = alpha * A X + beta * C,  A [N][k] (lda), X [k][m] (ldx), k, m <= 64.

@@ -135,6 +135,8 @@ def _declare_tt(L):
     L.stsp_tt_gram.restype = ci
     L.stsp_tt_mm.argtypes = [ci, vp, ci, vp, ci, vp, ci, ci, ci, ci, cd, cd, vp]
     L.stsp_tt_mm.restype = ci
+    L.stsp_tt_chol_inv.argtypes = [ci, vp, ci, ctypes.c_long, vp, vp, ci, ctypes.c_long, ci, ci, cd, vp, vp]
+    L.stsp_tt_chol_inv.restype = ci
     L.stsp_tt_expand.argtypes = [ci, vp, ci, vp, ci, ci, ci, cd, cd, cd, cd, cd, ci, vp]
     L.stsp_tt_expand.restype = ci
     L.stsp_tt_dense_diffusion.argtypes = [ci, vp, vp, ci, ci, cd, vp]

@@ -82,6 +82,28 @@ def tsmm(A: torch.Tensor, X: torch.Tensor, out: torch.Tensor = None, alpha: floa
     return out
 
 
+def chol_inv(G: torch.Tensor, shift_c: float = 0.0):
+    """Batched shifted Cholesky of k x k Gram matrices G [b, k, k] (k <= 64):
+    G_i + shift_c trace(G_i) I = R_i^T R_i (shift_c < 0: unshifted unless a
+    pivot fails, then shifted by |shift_c|).  Returns (R, R^-1, info) with R
+    upper triangular [b, k, k] and info [b] int32 (0, or failing pivot + 1;
+    read it only where a host sync happens anyway)."""
+    L = native.require_native()
+    if G.dim() == 2:
+        G = G.unsqueeze(0)
+    b, k, k2 = G.shape
+    if k != k2 or not 1 <= k <= 64 or G.stride(2) != 1:
+        raise ValueError(f"chol_inv: shape {tuple(G.shape)}")
+    code = _check(G[0])
+    R = torch.empty((b, k, k), dtype=G.dtype, device=G.device)
+    Ri = torch.empty_like(R)
+    info = torch.empty(b, dtype=torch.int32, device=G.device)
+    rc = L.stsp_tt_chol_inv(code, native.ptr(G), G.stride(1), G.stride(0), native.ptr(R), native.ptr(Ri), k, k * k, k, b,
+                            float(shift_c), native.ptr(info), native.current_stream_handle())
+    native.check(rc, "tt_chol_inv")
+    return R, Ri, info
+
+
 def expand(X: torch.Tensor, x0: float, x1: float, y0: float, y1: float, ih2: float, periodic: bool = False,
            out: torch.Tensor = None) -> torch.Tensor:
     """[N, 2r] = [x0 X + x1 D X, y0 X + y1 D X], (D X)_i = (X_{i-1} - 2 X_i + X_{i+1}) ih2."""

@@ -159,3 +159,36 @@ def test_low_rank_diffusion_substeps_exact_between_recompressions(substeps):
         D = s.dense_step(D, dt)
     assert float((F.dense() - D).norm() / D.norm()) < 1e-13
     assert F.rank == 2
+
+
+def test_cholqr3_orthonormal_and_exact_cpu():
+    """Shifted CholeskyQR3 (models/tt.py::cholqr3): Q orthonormal and X = Q R to
+    working precision, also for exactly rank-deficient factors (repeated
+    columns, as in the expanded factors of a step)."""
+    from stsphere.models import tt
+    g = torch.Generator().manual_seed(1)
+    A = torch.randn(400, 6, dtype=torch.float64, generator=g)
+    X = torch.cat([A, 0.3 * A[:, :2], torch.randn(400, 4, dtype=torch.float64, generator=g)], 1)   # rank 10 of 12
+    Q, R, info = tt.cholqr3(X)
+    assert int(info.abs().sum()) == 0
+    assert float((Q @ R - X).norm() / X.norm()) < 1e-14
+    # full-rank factor: orthonormal to machine precision
+    Q2, R2, _ = tt.cholqr3(torch.randn(400, 12, dtype=torch.float64, generator=g))
+    assert float((Q2.T @ Q2 - torch.eye(12, dtype=torch.float64)).abs().max()) < 1e-13
+
+
+def test_recompress_many_machine_precision_cpu():
+    """The CholeskyQR3 recompression keeps a step's product to ~1e-15, where the
+    Gram/eigen route stops near sqrt(eps)."""
+    from stsphere.models import tt
+    N = 256
+    x = torch.linspace(0, 1, N, dtype=torch.float64)
+    U = torch.exp(-((x[:, None] - 0.4) ** 2 + (x[None, :] - 0.6) ** 2) / 0.02) + torch.sin(3 * x[:, None]) * torch.cos(2 * x[None, :])
+    lr = tt.LowRankField.from_dense(U, eps=1e-15)
+    s = tt.LowRankDiffusion(N, eps=1e-14)
+    c = 0.2 * s.h ** 2
+    A = torch.cat([lr.A, c * (s.D @ lr.A), c * lr.A], 1)
+    B = torch.cat([lr.B, lr.B, s.D @ lr.B], 1)
+    f, = tt.recompress_many([(A, B)], 1e-14, None)
+    dense = A @ B.T
+    assert float((f.dense() - dense).norm() / dense.norm()) < 1e-13

@@ -176,7 +176,7 @@ def test_low_rank_diffusion_hip_substeps_match_dense(substeps):
     stepping for the same simulated time (truncation error only)."""
     N = 512
     mr = 64 >> substeps
-    s = tt.LowRankDiffusion(N, kappa=1.0, eps=1e-9, max_rank=mr, backend="hip", substeps=substeps)
+    s = tt.LowRankDiffusion(N, kappa=1.0, eps=1e-9, max_rank=mr, backend="hip", substeps=substeps, qr="gram")
     ref = tt.LowRankDiffusion(N, kappa=1.0, eps=1e-9, max_rank=mr, substeps=substeps)
     U = _panel(N)
     lr = tt.LowRankField.from_dense(U.cuda(), eps=1e-12)
@@ -195,3 +195,66 @@ def test_low_rank_diffusion_hip_substeps_match_dense(substeps):
     # range than one step's: measured 4.1e-7 at 2 substeps (1 substep: < 1e-7)
     assert float((got - lt.dense()).norm() / lt.dense().norm()) < 2e-6
     assert float((got - dense).norm() / dense.norm()) < 2e-6
+
+
+@pytest.mark.gpu
+def test_chol_inv_kernel_matches_torch():
+    """The k x k shifted-Cholesky kernel of CholeskyQR3: R^T R = G + s I and
+    R R^-1 = I, for full-rank and exactly rank-deficient Gram matrices (the
+    adaptive form falls back to the shift only for the latter)."""
+    from stsphere.ops import tt_ops
+    g = torch.Generator().manual_seed(3)
+    for k in (3, 17, 40, 64):
+        X = torch.randn(500, k, dtype=torch.float64, generator=g)
+        if k > 3:
+            X[:, -1] = 2.0 * X[:, 0]
+        G = (X.T @ X).cuda()
+        c = tt.cholqr3_shift(500, k, torch.float64)
+        for sc in (c, -c):
+            R, Ri, info = tt_ops.chol_inv(G, sc)
+            torch.cuda.synchronize()
+            assert int(info[0]) == 0
+            s = c * float(torch.trace(G))
+            want = G + s * torch.eye(k, dtype=torch.float64, device="cuda")
+            if sc < 0 and k == 3:     # full rank: the plain factor
+                want = G
+            assert float((R[0].T @ R[0] - want).abs().max() / want.abs().max()) < 1e-13
+            assert float((R[0] @ Ri[0] - torch.eye(k, dtype=torch.float64, device="cuda")).abs().max()) < 1e-8
+            assert float(torch.tril(R[0], -1).abs().max()) == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bc", ["dirichlet", "periodic"])
+def test_low_rank_diffusion_hip_cholqr3_machine_precision(bc):
+    """Round-2 verdict item 7: the device recompression (CholeskyQR3 with MFMA
+    Gram / product kernels) has no sqrt(eps) floor: with a 1e-13 tolerance and
+    no rank cap the factored run stays within 1e-10 of dense stepping, where the
+    Gram/eigen route (qr="gram") stops near 1e-8."""
+    N = 512
+    s = tt.LowRankDiffusion(N, kappa=1.0, bc=bc, eps=1e-13, backend="hip")
+    ref = tt.LowRankDiffusion(N, kappa=1.0, bc=bc, eps=1e-13)
+    U = _panel(N)
+    lr = tt.LowRankField.from_dense(U.cuda(), eps=1e-15)
+    dt = 0.5 * s.dt_max
+    dense = U.clone()
+    for _ in range(30):
+        lr = s.step(lr, dt)
+        dense = ref.dense_step(dense, dt)
+    got = lr.dense().cpu()
+    assert float((got - dense).norm() / dense.norm()) < 1e-10
+
+
+@pytest.mark.gpu
+def test_cube_low_rank_diffusion_hip_cholqr3_machine_precision():
+    N = 64
+    x = (torch.arange(N, dtype=torch.float64) + 0.5) / N
+    U = torch.stack([torch.outer(torch.sin(math.pi * x * (p + 1) / 3), torch.cos(math.pi * x * (p % 3 + 1) / 2))
+                     for p in range(6)]).cuda()
+    mh = tt.CubedSphereLowRankDiffusion(N, eps=1e-13, device="cuda", backend="hip")
+    F, D = mh.to_factored(U), U.clone()
+    dt = 0.8 * mh.dt_max
+    for _ in range(10):
+        F, D = mh.step(F, dt), mh.dense_step(D, dt)
+    torch.cuda.synchronize()
+    assert max(f.rank for f in F) <= 30
+    assert float((mh.to_dense(F) - D).norm() / D.norm()) < 1e-10

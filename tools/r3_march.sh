@@ -6,7 +6,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/${TAG:-r3_march}
 mkdir -p $OUT
 cd $ROOT
-timeout -k 10 300 python -u -m pytest tests/test_march.py -x -v --timeout 120 --timeout-method thread \
+timeout -k 10 400 python -u -m pytest tests/test_march.py tests/test_tt_kernels.py -x -v --timeout 120 --timeout-method thread \
   > $OUT/pytest.log 2>&1; rc=$?; tail -3 $OUT/pytest.log; [ $rc = 0 ] || exit $rc
 run() {
   timeout -k 10 240 python -u bench.py --runtime native "$@" > $OUT/b.log 2>&1 || { tail -5 $OUT/b.log; exit 4; }
