@@ -27,6 +27,10 @@ MI355X runs on the matrix cores through hipBLASLt / rocSOLVER):
                     factored form (each panel side's ghost strip is gathered as
                     rows of the neighbour's factors, O(N r) instead of the
                     N x N field; orientation from the tile layout's ghost map)
+* ``CubedSphereLowRankAdvection``: tracer advection (TC1 cosine bell) on the
+                    six panels in factored form with the sphere metric
+                    (edge-normal transport, areas), central FV + SSP-RK3,
+                    coefficients factored once, Khatri-Rao products
 * ``compress_cubed_sphere``: per-panel TT ranks / errors of a [6, N, N] field
 """
 from __future__ import annotations
@@ -609,6 +613,150 @@ class CubedSphereLowRankDiffusion:
         flat[self._ddst] = flat[self._dsrc]
         lap = (P[:, :-2, 1:-1] + P[:, 2:, 1:-1]) + (P[:, 1:-1, :-2] + P[:, 1:-1, 2:]) - 4.0 * U6
         return U6 + c * lap
+
+
+def lowrank_coefficients(M: torch.Tensor, eps: float):
+    """Factor a fixed coefficient field M [n, m] as C D^T to relative accuracy eps."""
+    u, s, vh = torch.linalg.svd(M, full_matrices=False)
+    r = _trunc_rank(s, eps * float(torch.linalg.norm(s)), None)
+    return (u[:, :r] * s[:r]).contiguous(), vh[:r].T.contiguous()
+
+
+def hadamard(C: torch.Tensor, D: torch.Tensor, A: torch.Tensor, B: torch.Tensor):
+    """(C D^T) o (A B^T) = (C * A)(D * B)^T with row-wise Khatri-Rao factors
+    (rank rc ra): a variable coefficient times a factored field."""
+    n, m = C.shape[0], D.shape[0]
+    return ((C[:, :, None] * A[:, None, :]).reshape(n, -1), (D[:, :, None] * B[:, None, :]).reshape(m, -1))
+
+
+def _face_avg(X: torch.Tensor) -> torch.Tensor:
+    """[n, r] cell factor -> [n+1, r] face average 0.5 (X[i-1] + X[i]), zero outside."""
+    out = torch.zeros((X.shape[0] + 1, X.shape[1]), dtype=X.dtype, device=X.device)
+    out[:-1] += 0.5 * X
+    out[1:] += 0.5 * X
+    return out
+
+
+def _face_diff(X: torch.Tensor) -> torch.Tensor:
+    """[n+1, r] face factor -> [n, r] difference X[i+1] - X[i]."""
+    return X[1:] - X[:-1]
+
+
+class CubedSphereLowRankAdvection:
+    """Tracer advection dq/dt + div(q v) = 0 on the six panels of the cubed
+    sphere, carried entirely in factored form U_p = A_p B_p^T (PDF s.13 / s.18
+    workload, TT numerics of PDF s.3, s.19; round-2 verdict item 7).
+
+    Finite volumes with the true sphere metric, as the FV solver
+    (models/advection.py): edge-normal transport U = (v . m) L at every edge
+    midpoint, cell areas A, central edge values and SSP-RK3,
+
+        dq/dt = -(1/A) [ Fx_{i+1/2} - Fx_{i-1/2} + Fy_{j+1/2} - Fy_{j-1/2} ],
+        Fx = Ux (q_{i-1} + q_i) / 2.
+
+    The scheme is linear in q, so every operation stays factored: the metric
+    coefficients Ux, Uy, 1/A are factored once (``coef_eps``), a coefficient
+    times a field is a Khatri-Rao product of factors, the face average and
+    difference act on the factors' rows, and the cube coupling is the ghost
+    strips of the neighbour panels gathered in factored form (O(N r) each,
+    orientation from the FV layout's index-space halo, as
+    ``CubedSphereLowRankDiffusion``), added as rank-1 terms.  Ranks are
+    truncated to ``eps`` after every product (``recompress``: thin QRs + a
+    k x k SVD).  The flux through a panel edge is computed identically on both
+    sides (same edge, same ghost pairs), so mass is conserved up to the
+    truncation.  ``dense_step`` is the N x N six-panel reference of the same
+    operator; tests/test_tt_and_models.py compares both, and the factored TC1
+    run with the FV solver's."""
+
+    def __init__(self, N: int, alpha: float = 0.0, eps: float = 1e-10, max_rank: Optional[int] = None,
+                 coef_eps: float = 1e-13, u0: Optional[float] = None, dtype=torch.float64, device="cpu"):
+        from .geometry import CubedSphereGrid
+        from . import initial_conditions as ic
+        self.N, self.eps, self.max_rank = N, eps, max_rank
+        self.dtype, self.device = dtype, torch.device(device)
+        grid = CubedSphereGrid(N)
+        self.grid = grid
+        self.u0 = u0 if u0 is not None else 2.0 * math.pi * grid.radius / (12.0 * 86400.0)
+        self.alpha = alpha
+        wind = lambda p: ic.solid_body_wind(p, self.u0, alpha, grid.radius)
+        ux = np.sum(wind(grid.x_edge_midpoints()) * grid.x_edge_normals()[:, None, :, :], -1) * grid.x_edge_lengths()
+        uy = np.sum(wind(grid.y_edge_midpoints()) * grid.y_edge_normals()[:, :, None, :], -1) * grid.y_edge_lengths()
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=self.device)
+        self.Ux, self.Uy, self.invA = t(ux), t(uy), t(1.0 / grid.areas())     # dense copies (reference)
+        self.cx = [lowrank_coefficients(self.Ux[p], coef_eps) for p in range(6)]
+        self.cy = [lowrank_coefficients(self.Uy[p], coef_eps) for p in range(6)]
+        self.ca = [lowrank_coefficients(self.invA[p], coef_eps) for p in range(6)]
+        self.halo = CubedSphereLowRankDiffusion(N, dtype=dtype, device=device)
+        e = torch.zeros((N + 1, 2), dtype=dtype, device=self.device)
+        e[0, 0] = 1.0
+        e[N, 1] = 1.0
+        self._e = e
+        self.dt_max = 0.9 * grid.min_spacing() / (2.0 * self.u0)
+
+    def coefficient_ranks(self) -> dict:
+        return {"Ux": [c.shape[1] for c, _ in self.cx], "Uy": [c.shape[1] for c, _ in self.cy],
+                "invA": [c.shape[1] for c, _ in self.ca]}
+
+    def _trunc(self, A, B) -> LowRankField:
+        return recompress(A, B, self.eps, self.max_rank)
+
+    def rhs(self, F: Sequence[LowRankField]) -> List[LowRankField]:
+        out = []
+        for p in range(6):
+            A, B = F[p].A, F[p].B
+            g = self.halo.ghosts(F, p)                                    # [4, N]: W, E, S, N strips
+            # x faces (rows j, faces i): A avg(B)^T + 0.5 g_W e_0^T + 0.5 g_E e_N^T
+            Ax = torch.cat([A, 0.5 * g[0:2].T], 1)
+            Bx = torch.cat([_face_avg(B), self._e], 1)
+            fx = self._trunc(*hadamard(*self.cx[p], Ax, Bx))
+            # y faces (faces j, columns i): avg(A) B^T + 0.5 e_0 g_S^T + 0.5 e_N g_N^T
+            Ay = torch.cat([_face_avg(A), self._e], 1)
+            By = torch.cat([B, 0.5 * g[2:4].T], 1)
+            fy = self._trunc(*hadamard(*self.cy[p], Ay, By))
+            div = self._trunc(torch.cat([fx.A, _face_diff(fy.A)], 1), torch.cat([_face_diff(fx.B), fy.B], 1))
+            Ca, Da = self.ca[p]
+            La, Lb = hadamard(Ca, Da, div.A, div.B)
+            out.append(self._trunc(-La, Lb))
+        return out
+
+    def _axpy(self, a: float, X: Sequence[LowRankField], b: float, Y: Sequence[LowRankField]) -> List[LowRankField]:
+        return [self._trunc(torch.cat([a * x.A, b * y.A], 1), torch.cat([x.B, y.B], 1)) for x, y in zip(X, Y)]
+
+    def step(self, F: Sequence[LowRankField], dt: float) -> List[LowRankField]:
+        """One SSP-RK3 step."""
+        L0 = self.rhs(F)
+        U1 = self._axpy(1.0, F, dt, L0)
+        L1 = self.rhs(U1)
+        U2 = self._axpy(0.75, F, 0.25, self._axpy(1.0, U1, dt, L1))
+        L2 = self.rhs(U2)
+        return self._axpy(1.0 / 3.0, F, 2.0 / 3.0, self._axpy(1.0, U2, dt, L2))
+
+    # ---- dense reference of the same operator --------------------------------
+    def dense_rhs(self, U6: torch.Tensor) -> torch.Tensor:
+        N = self.N
+        P = torch.zeros((6, N + 2, N + 2), dtype=U6.dtype, device=U6.device)
+        P[:, 1:-1, 1:-1] = U6
+        flat = P.reshape(-1)
+        flat[self.halo._ddst] = flat[self.halo._dsrc]
+        qx = 0.5 * (P[:, 1:-1, :-1] + P[:, 1:-1, 1:])                   # [6, N, N+1]
+        qy = 0.5 * (P[:, :-1, 1:-1] + P[:, 1:, 1:-1])                   # [6, N+1, N]
+        fx, fy = self.Ux * qx, self.Uy * qy
+        return -((fx[:, :, 1:] - fx[:, :, :-1]) + (fy[:, 1:] - fy[:, :-1])) * self.invA
+
+    def dense_step(self, U6: torch.Tensor, dt: float) -> torch.Tensor:
+        U1 = U6 + dt * self.dense_rhs(U6)
+        U2 = 0.75 * U6 + 0.25 * (U1 + dt * self.dense_rhs(U1))
+        return U6 / 3.0 + (2.0 / 3.0) * (U2 + dt * self.dense_rhs(U2))
+
+    def mass(self, U6: torch.Tensor) -> float:
+        return float((U6 / self.invA).sum())
+
+    def to_factored(self, U6: torch.Tensor) -> List[LowRankField]:
+        return [LowRankField.from_dense(U6[p].to(self.dtype), self.eps, self.max_rank) for p in range(6)]
+
+    @staticmethod
+    def to_dense(F: Sequence[LowRankField]) -> torch.Tensor:
+        return torch.stack([f.dense() for f in F])
 
 
 def compress_cubed_sphere(field: np.ndarray, eps: float = 1e-6, qtt: bool = False) -> List[dict]:
