@@ -62,6 +62,9 @@ def parse(argv=None):
     ap.add_argument("--steps-per-launch", type=int, default=0,
                     help="fused runtime: steps inside one kernel launch (0 = auto: the largest even divisor of "
                          "--steps up to 64 when every block fits on the GPU at once; 1 = one launch per step)")
+    ap.add_argument("--launch", default="direct", choices=["direct", "graph"],
+                    help="fused runtime: issue each multi-step kernel launch directly (default) or replay it "
+                         "from a hipGraph (a one-kernel graph only adds hipGraphLaunch's host floor)")
     ap.add_argument("--steps-per-graph", type=int, default=0,
                     help="steps recorded per graph (0 = the whole timed run in one graph)")
     ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "rccl"],
@@ -299,7 +302,8 @@ def main():
                 cus = torch.cuda.get_device_properties(device).multi_processor_count
                 spl = max([k for k in range(2, 65, 2) if a.steps % k == 0], default=1) if fk.plan.nb <= cus else 1
             info["steps_per_launch"] = spl
-            runner = NativeStepper(eng, use_graph=True, steps_per_graph=spg, fused=fk, steps_per_launch=spl)
+            runner = NativeStepper(eng, use_graph=True, steps_per_graph=spg, fused=fk, steps_per_launch=spl,
+                                   direct=a.launch == "direct")
         elif runtime == "native":
             # C++ runtime, hipGraph replay; between GPUs either direct xGMI
             # stores from the stage kernels (graph-captured) or RCCL grouped
@@ -426,6 +430,8 @@ def main():
         and not getattr(runner, "_cxx_graph", False)
     if graph_path and (timed.get("eager_steps", 0) != 0 or timed.get("graph_steps", 0) != a.steps):
         raise SystemExit(f"[bench] timed region was not a pure graph replay: {timed}")
+    if getattr(runner, "direct", False) and (timed.get("eager_steps", 0) != 0 or timed.get("direct_steps", 0) != a.steps):
+        raise SystemExit(f"[bench] timed region was not whole direct fused launches: {timed}")
     diag = eng.diagnostics()
     if world > 1:
         t = torch.tensor([diag.get("mass", 0.0)], dtype=torch.float64, device=cdev)
@@ -468,6 +474,8 @@ def main():
                 "block": list((eng.compute.bx, eng.compute.by)) if hasattr(eng.compute, "bx") else None,
                 "steps_per_launch": info["steps_per_launch"],
                 "graph_replayed_steps": timed.get("graph_steps"),
+                "direct_launch_steps": timed.get("direct_steps"),
+                "kernel_launches": timed.get("launches") if timed.get("direct_steps") else None,
                 "eager_steps": timed.get("eager_steps"),
             },
             "simulated_days_per_day": sdpd,

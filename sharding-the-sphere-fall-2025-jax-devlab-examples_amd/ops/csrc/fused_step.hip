@@ -766,14 +766,22 @@ int launch_fused(const FusedDesc* d, hipStream_t s) {
   const dim3 grid(d->nblocks), block(D::NT);
   if (a.nsteps > 1) {
     // every block must be resident at once (a waiting block holds its CU)
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return -8;
-    const void* kf = d->xg ? (const void*)fused_step_kernel<T, 0, NS, B, true, true>
-                           : (const void*)fused_step_kernel<T, 0, NS, B, false, true>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kf, D::NT, 0) != hipSuccess) return -8;
-    if ((long)per * cus < d->nblocks) return -9;
+    // (the residency query is cached per device and variant: it costs host
+    // microseconds on every launch of the bench's timed region otherwise)
+    static int cdev[2] = {-1, -1}, ccap[2] = {0, 0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -8;
+    const int xi = d->xg ? 1 : 0;
+    if (cdev[xi] != dev) {
+      int cus = 0, per = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -8;
+      const void* kf = d->xg ? (const void*)fused_step_kernel<T, 0, NS, B, true, true>
+                             : (const void*)fused_step_kernel<T, 0, NS, B, false, true>;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kf, D::NT, 0) != hipSuccess) return -8;
+      ccap[xi] = per * cus;
+      cdev[xi] = dev;
+    }
+    if (ccap[xi] < d->nblocks) return -9;
   }
 #define FUSED_LAUNCH(L_)                                                                                  \
   if (a.nsteps > 1) {                                                                                     \

@@ -119,7 +119,7 @@ class NativeStepper:
 
     def __init__(self, engine, nccl_comm: Optional[int] = None, use_graph: bool = True,
                  steps_per_graph: int = 30, roctx: bool = False, stream: Optional[torch.cuda.Stream] = None,
-                 xgmi=None, fused=None, steps_per_launch: int = 1):
+                 xgmi=None, fused=None, steps_per_launch: int = 1, direct: bool = False):
         from .hip_compute import HipCompute
         e = engine
         if not isinstance(e.compute, HipCompute):
@@ -221,7 +221,18 @@ class NativeStepper:
         self._primed = set()       # (periods, copy) replayed at least once
         self._next_copy = {}       # periods -> copy the next replay of that length uses
         self._pool0 = list(e.pool)  # construction order = the op list's buffer pointers
-        self.stats = {"graph_steps": 0, "eager_steps": 0, "replays": 0}
+        self.stats = {"graph_steps": 0, "eager_steps": 0, "replays": 0, "direct_steps": 0, "launches": 0}
+        # direct (fused runtime only): every period is ONE kernel launch issued
+        # from Python through ctypes on torch's current stream, no graph.  A
+        # fused multi-step period is a single kernel, so a graph around it buys
+        # nothing; measured at C96 20/5 (tools/launch_probe.py,
+        # profiles/r3_march/launch_probe.json): 13.70 us/step direct against
+        # 14.22 replaying the one-node graph (hipGraphLaunch's host floor)
+        if direct and fused is None:
+            raise ValueError("direct launches are the fused runtime's")
+        self.direct = bool(direct)
+        if self.direct:
+            self.use_graph = False
         self._warmed = False
         d.stream = int(self.stream.cuda_stream)
         d.nccl_comm = nccl_comm or 0
@@ -330,12 +341,35 @@ class NativeStepper:
             chunks.append(periods % k)
         return chunks
 
+    def _run_direct(self, nsteps: int) -> None:
+        """nsteps (a multiple of the period) as direct fused launches."""
+        st = int(torch.cuda.current_stream(self.e.device).cuda_stream)
+        for _ in range(nsteps // self.period):
+            if self.spl > 1:
+                self.fused.launch(0, st, nsteps=self.spl)
+                self.stats["launches"] += 1
+            else:
+                self.fused.launch(0, st)
+                self.fused.launch(1, st)
+                self.stats["launches"] += 2
+        self.stats["direct_steps"] += nsteps
+
     def prepare(self, nsteps: int, prime: bool = True) -> None:
         """Record every graph ``run(nsteps)`` will replay and (prime=True)
         replay each once on a scratch copy of the state, so the first timed
         replay pays neither capture, instantiation nor upload.  The state,
         time and step count are unchanged.  With the direct xGMI exchange this
         is collective (the restore re-primes the rings)."""
+        if self.direct:
+            # one untimed pass of the same launches on a scratch copy (first-use costs)
+            if prime and nsteps // self.period:
+                saved = self._save()
+                self._run_direct((nsteps // self.period) * self.period)
+                torch.cuda.synchronize(self.e.device)
+                self._restore(saved)
+                self.stats["direct_steps"] = 0
+                self.stats["launches"] = 0
+            return
         if not self.use_graph or self._cxx_graph:
             return
         todo = []
@@ -355,6 +389,9 @@ class NativeStepper:
 
     def _run(self, nsteps: int) -> None:
         """nsteps (a multiple of the period)."""
+        if self.direct:
+            self._run_direct(nsteps)
+            return
         if not self.use_graph or self._cxx_graph:
             self._run_native(nsteps)
             return

@@ -215,10 +215,14 @@ def test_chol_inv_kernel_matches_torch():
             torch.cuda.synchronize()
             assert int(info[0]) == 0
             s = c * float(torch.trace(G))
-            want = G + s * torch.eye(k, dtype=torch.float64, device="cuda")
-            if sc < 0 and k == 3:     # full rank: the plain factor
-                want = G
-            assert float((R[0].T @ R[0] - want).abs().max() / want.abs().max()) < 1e-13
+            shifted = G + s * torch.eye(k, dtype=torch.float64, device="cuda")
+            err = lambda want: float((R[0].T @ R[0] - want).abs().max() / want.abs().max())
+            if sc > 0:
+                assert err(shifted) < 1e-13
+            else:   # adaptive: the plain factor unless a pivot failed (a duplicated column may or may not)
+                assert min(err(G), err(shifted)) < 1e-13
+                if k == 3:
+                    assert err(G) < 1e-13
             assert float((R[0] @ Ri[0] - torch.eye(k, dtype=torch.float64, device="cuda")).abs().max()) < 1e-8
             assert float(torch.tril(R[0], -1).abs().max()) == 0.0
 
