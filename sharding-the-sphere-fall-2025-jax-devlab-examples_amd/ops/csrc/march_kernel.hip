@@ -64,7 +64,9 @@ template <typename T> __device__ __forceinline__ T shl(T v) { return dpp<DPP_SHL
 #ifndef STSP_MARCH_WPE32
 #define STSP_MARCH_WPE32 4
 #endif
-template <typename T, int LIM, int R>
+// ACC: the RK4 accumulator operands (acc_in / acc_out); the SSP-RK3 and Euler
+// stages run the instantiation without them (4 fewer live values per lane)
+template <typename T, int LIM, int R, bool ACC>
 __global__ __launch_bounds__(MW * MWPB) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 8 ? STSP_MARCH_WPE64 : STSP_MARCH_WPE32)))
 void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   pin_args(a);
@@ -174,8 +176,8 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   const T* ext = a.ex + (long)tile * n * (n + 1);
   const T* eyt = a.ey + (long)tile * (n + 1) * n;
   const int* pm = a.push + (long)tile * 4 * mg * n;
-  const bool need_x = (a.a0 != T(0)) || (a.acc_out && a.c1 != T(0));
-  const bool need_acc = a.acc_out && a.acc_in && (a.c0 != T(0));
+  const bool need_x = (a.a0 != T(0)) || (ACC && a.c1 != T(0));
+  const bool need_acc = ACC && a.acc_in && (a.c0 != T(0));
 
   // ---- prologue: rows y0-2 .. y0+1, the flux through the face below row y0 -----
   T cA[5], cB[5], hsA[4], Gs[4];
@@ -212,17 +214,17 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
     if (j + 1 < y1) ldq(cell(xc, j + 3), qn);        // prefetch (row j + 3 <= n + 1)
     // own-row operands of row j (needed after the fluxes)
     const unsigned pc = cell(xc, j);
-    T qo[4], xs[4], acs[4], rec[8];
+    T qo[4], xs[4], acs[ACC ? 4 : 1], rec[8];
     ldq(pc, qo);
 #pragma unroll
-    for (int f = 0; f < 4; ++f) { xs[f] = T(0); acs[f] = T(0); }
+    for (int f = 0; f < 4; ++f) xs[f] = T(0);
     if (need_x) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) xs[f] = bld<T>(rX, pc * ES, f * fs);
     }
-    if (need_acc) {
+    if constexpr (ACC) {
 #pragma unroll
-      for (int f = 0; f < 4; ++f) acs[f] = *o32(a.acc_in + f * S, pc);
+      for (int f = 0; f < 4; ++f) acs[f] = need_acc ? *o32(a.acc_in + f * S, pc) : T(0);
     }
     const unsigned gc = (unsigned)((tile * n + j) * n + (inx ? x : 0));
     bld_rec8<T>(rG, gc * 8u * ES, rec);
@@ -335,7 +337,7 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
         const T d = o[1] * r0 + o[2] * r1 + o[3] * r2;
         o[1] -= d * r0; o[2] -= d * r1; o[3] -= d * r2;
       }
-      if (a.acc_out) {
+      if constexpr (ACC) {
         T p[4];
 #pragma unroll
         for (int f = 0; f < 4; ++f) p[f] = a.c2 * a.dt * dq[f];
@@ -383,7 +385,10 @@ int march_l(const StageDesc* d, hipStream_t s) {
   const int ncs = (d->n + MO - 1) / MO, nrs = (d->n + R - 1) / R;
   const int njobs = d->ntile * ncs * nrs;
   const int nb = (njobs + MWPB - 1) / MWPB;
-  hipLaunchKernelGGL((march_kernel<T, LIM, R>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+  if (d->acc_out)
+    hipLaunchKernelGGL((march_kernel<T, LIM, R, true>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+  else
+    hipLaunchKernelGGL((march_kernel<T, LIM, R, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
   return (int)hipGetLastError();
 }
 
@@ -401,6 +406,7 @@ int march_r(const StageDesc* d, hipStream_t s) {
 template <typename T>
 int march_t(int rows, const StageDesc* d, hipStream_t s) {
   switch (rows) {
+    case 4: return march_r<T, 4>(d, s);
     case 8: return march_r<T, 8>(d, s);
     case 16: return march_r<T, 16>(d, s);
     case 32: return march_r<T, 32>(d, s);
@@ -420,7 +426,7 @@ __global__ void dpp_probe_kernel(const double* in, double* out, float* outf) {
 
 }  // namespace
 
-// Rows per wave `rows` (8, 16, 32).  Shallow water, PLR, one rank with every
+// Rows per wave `rows` (4, 8, 16, 32).  Shallow water, PLR, one rank with every
 // ghost local (no remote ghosts, no xGMI, no block list).
 extern "C" int stsp_march_launch(int dtype, int rows, const StageDesc* d, hipStream_t stream) {
   if (d->xg || d->remote || d->blocks) return -13;

@@ -40,9 +40,11 @@ def main():
     r.prepare(K)
     cur = torch.cuda.current_stream()
 
-    def timed(fn):
+    def timed(fn, idle=0.0):
         ts = []
         for _ in range(a.reps):
+            if idle:
+                time.sleep(idle)      # GPU idle before the timed region (as after the bench's warmup)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             fn()
@@ -51,17 +53,22 @@ def main():
         return statistics.median(ts), min(ts)
 
     out = {"N": a.N, "t": a.t, "steps": K, "blocks": fk.plan.nb}
+    rd = NativeStepper(e, use_graph=True, steps_per_graph=K, fused=fk, steps_per_launch=K, direct=True)
+    rd.prepare(K)
     forms = {
         "graph_replay": lambda: r.run(K),
         "cxx_eager": lambda: r._run_native(K),
         "ctypes_direct": lambda: fk.launch(0, int(cur.cuda_stream), nsteps=K),
+        "runner_direct": lambda: rd.run(K),
     }
-    for name, fn in forms.items():
-        fn()
-        torch.cuda.synchronize()
-        med, best = timed(fn)
-        out[name + "_us_per_step"] = round(med, 3)
-        out[name + "_best"] = round(best, 3)
+    for idle in (0.0, 0.002, 0.05):
+        for name, fn in forms.items():
+            fn()
+            torch.cuda.synchronize()
+            med, best = timed(fn, idle)
+            tag = name if not idle else f"{name}_idle{int(idle * 1e3)}ms"
+            out[tag + "_us_per_step"] = round(med, 3)
+            out[tag + "_best"] = round(best, 3)
     # an empty timed region: the synchronize pair alone
     med, best = timed(lambda: None)
     out["empty_region_us_total"] = round(med * K, 2)
