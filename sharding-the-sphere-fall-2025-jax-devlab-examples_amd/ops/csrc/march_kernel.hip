@@ -122,8 +122,11 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   const int lnE = n - cs * MO + 2;                   // lane of column n
   const bool peW = (pe & 1) && cs == 0;
   const bool peE = (pe & 2) && lnE >= 0 && lnE < MW;
-  const bool peS = (pe & 4) && y0 == 0;
-  const bool peN = (pe & 8) && y1 == n;
+  // a segment reads rows y0 - 2 .. y1 + 1: the S ghost row -1 when y0 <= 1 and
+  // the N ghost row n when y1 >= n - 1 (a segment ending one row short of the
+  // tile still takes the slope of row n - 1 across the panel edge)
+  const bool peS = (pe & 4) && y0 <= 1;
+  const bool peN = (pe & 8) && y1 >= n - 1;
   auto tab = [&](int side, int pos) -> unsigned { return (unsigned)(((tile * 4 + side) * 3 + 0) * n + pos); };
   // S / N strips (along x, per lane): interpolation of row y at this lane's table pair
   auto interp_row = [&](int side, int y, T (&o)[4]) {

@@ -294,11 +294,16 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   // neighbour's edge state in the neighbour's frame (one field per thread, so
   // the F fields run on F waves / SIMDs side by side).  Its table entries are
   // issued here.
-  // sides of this block on a cube edge; evaluated where first needed (after the window)
+  // sides of this block on a cube edge; evaluated where first needed (after the window).
+  // A side counts as soon as the block's window reaches that side's ghost strip:
+  // also the last-but-one block of a tile whose last block is 1 (PLR) or 1-2
+  // (PPM) cells wide, whose outer faces reconstruct a cell next to the ghost
+  // (found by the streaming stage's odd-size tests: C25 with 8 x 8 blocks was
+  // 4.8e-2 off the oracle)
   auto block_sides = [&]() {
     if constexpr (RECON)
-      return (x0 == 0 ? (pe_word & 1) : 0) | (x0 + BX >= n ? (pe_word & 2) : 0) | (y0 == 0 ? (pe_word & 4) : 0) |
-             (y0 + BY >= n ? (pe_word & 8) : 0);
+      return (x0 == 0 ? (pe_word & 1) : 0) | (x0 + BX + NG > n ? (pe_word & 2) : 0) | (y0 == 0 ? (pe_word & 4) : 0) |
+             (y0 + BY + NG > n ? (pe_word & 8) : 0);
     else
       return 0;
   };
@@ -546,8 +551,11 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   };
   auto fix_write = [&](int f, const T (&gk)[KG], T nf, T c) {
     T* wm = &s_w[f][0][0];
+    const int wend = (pside < 2 ? x0 + BX : y0 + BY) + NG;   // first coordinate past the window
 #pragma unroll
-    for (int k = 0; k < KG; ++k) wm[widx(plow ? -1 - k : n + k, pj)] = gk[k];
+    for (int k = 0; k < KG; ++k) {
+      if (plow || n + k < wend) wm[widx(plow ? -1 - k : n + k, pj)] = gk[k];
+    }
     s_pf[f][pslt] = nf;
     if constexpr (SW) s_pr[f][pslt] = c;
   };

@@ -141,3 +141,17 @@ def test_stage_kernel_never_uses_a_corner_ghost(name, block):
     torch.cuda.synchronize()
     assert torch.isfinite(b.tiles_view()).all()
     assert torch.equal(a.tiles_view(), b.tiles_view())
+
+
+@pytest.mark.parametrize("name,N,block", [("swe_tc5", 25, (8, 8)), ("swe_tc5", 33, (16, 16)),
+                                          ("adv", 25, (8, 8)), ("swe_ppm", 34, (16, 16)), ("swe_ppm", 33, (16, 8))])
+def test_partial_block_one_or_two_cells_from_a_panel_edge(name, N, block):
+    """A tile whose last block is 1 cell wide (PLR) or 1-2 cells (PPM): the
+    block before it reconstructs a cell next to the panel-edge ghost strip and
+    must see the interpolated ghosts (stage_kernel.hip, block_sides; C25 with
+    8 x 8 blocks was 4.8e-2 off the oracle before)."""
+    ref, hip = _pair(name, N, 1, torch.float64, block=block)
+    ref.step(3)
+    hip.step(3)
+    torch.cuda.synchronize()
+    assert _relerr(ref, hip) < 1e-11

@@ -49,7 +49,8 @@ def test_dpp_wave_shifts():
     assert torch.equal(outf[:64].double(), want_r) and torch.equal(outf[64:].double(), want_l)
 
 
-@pytest.mark.parametrize("N,t,R", [(24, 1, 16), (24, 2, 8), (72, 1, 16), (130, 1, 32), (96, 3, 8), (64, 2, 32)])
+@pytest.mark.parametrize("N,t,R", [(24, 1, 16), (24, 2, 8), (72, 1, 16), (130, 1, 32), (96, 3, 8), (64, 2, 32),
+                                   (25, 1, 8), (50, 2, 4), (27, 1, 16)])
 def test_march_fp64_matches_reference(N, t, R):
     ref, hip = _pair(N, t, torch.float64, (64, R))
     ref.step(3)
@@ -76,12 +77,21 @@ def test_march_integrators(integ):
     assert _relerr(ref, hip) < 1e-11
 
 
-def test_march_fp32_close_to_fp64_reference():
-    ref, hip = _pair(72, 1, torch.float32, (64, 16))
+@pytest.mark.parametrize("N,t,R", [(72, 1, 16), (48, 2, 8), (96, 3, 8), (250, 1, 8), (25, 1, 8)])
+def test_march_fp32_close_to_fp64_reference(N, t, R):
+    """fp32 rounding grows with the grid (differences of nearby cells over
+    smaller faces), so the gate is the block stage kernel's own fp32 error on
+    the same case."""
+    ref, hip = _pair(N, t, torch.float32, (64, R))
+    blk = Engine(ShallowWater("tc5"), TileLayout(N, t, 1, ng=2), grid=CubedSphereGrid(N), dtype=torch.float32,
+                 device="cuda", backend="hip", block=(16, 16), dt=ref.dt)
     ref.step(3)
     hip.step(3)
+    blk.step(3)
     torch.cuda.synchronize()
-    assert _relerr(ref, hip) < 1e-4
+    e_blk, e_m = _relerr(ref, blk), _relerr(ref, hip)
+    assert e_m < 1.5 * e_blk + 2e-5, (e_m, e_blk)
+    assert e_blk < 1e-3, e_blk
 
 
 def test_march_agrees_with_block_kernel():
