@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--eps", type=float, default=1e-8)
     ap.add_argument("--max-rank", type=int, default=16)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--qr", default="cholqr3", choices=["cholqr3", "gram"],
+                    help="hip recompression: device CholeskyQR3 (default) or the native Gram/eigen step")
     ap.add_argument("--substeps", default="1,2,3",
                     help="explicit steps per recompression (tt us is per simulated step)")
     a = ap.parse_args()
@@ -93,7 +95,7 @@ def main():
         t_dense = time_loop(dense_step, a.steps, sync)
         for ns in subs:
             s = tt.LowRankDiffusion(N, kappa=1.0, eps=a.eps, max_rank=min(a.max_rank, 64 >> ns), backend="hip", device=dev,
-                                    substeps=ns)
+                                    substeps=ns, qr=a.qr)
             st = {"lr": tt.LowRankField(A.clone(), B.clone())}
 
             def tt_step():
@@ -109,7 +111,7 @@ def main():
                 dense_step()
             sync()
             diff = rel_diff_chunked(st["lr"], state["u"])
-            row = {"N": N, "substeps": ns, "rank": st["lr"].rank, "dense_us": 1e6 * t_dense,
+            row = {"N": N, "qr": a.qr, "substeps": ns, "rank": st["lr"].rank, "dense_us": 1e6 * t_dense,
                    "dense_GBps": 16.0 * N * N / t_dense / 1e9, "tt_us": 1e6 * t_tt, "speedup": t_dense / t_tt,
                    "rel_diff": diff, "steps": calls * ns}
             rows.append(row)
