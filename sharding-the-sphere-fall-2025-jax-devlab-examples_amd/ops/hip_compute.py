@@ -25,7 +25,7 @@ BLOCK_SHAPES = ((16, 16), (32, 8), (16, 8), (8, 16), (8, 8))
 MARCH_SHAPES = ((64, 4), (64, 8), (64, 16), (64, 32))
 
 
-MARCH_AUTO = (64, 8)
+MARCH_AUTO = (64, 4)
 MARCH_CELLS_PER_CU = 8192
 
 
@@ -136,7 +136,7 @@ class HipCompute:
             cus = torch.cuda.get_device_properties(e.device).multi_processor_count
             bx, by = choose_block(n, T, cus, getattr(phys, "limiter", 0), torch.tensor([], dtype=e.dtype).element_size())
             # streaming stage once the rank streams: measured C720 (3.1M cells, 12k per CU)
-            # fp64 423 vs 467 us/step, fp32 202 vs 252 (64 x 8); C360 (3k per CU) a tie,
+            # fp64 423 vs 467 us/step, fp32 190 vs 252 (64 x 4; 64 x 8: 431 / 203); C360 (3k per CU) a tie,
             # C180 the block kernel (43 vs 75): too few marches to hide their latency
             if march_supported(self.phys_id, int(phys.kernel_params().get("limiter", 0)), plan.num_recv > 0) \
                     and T * n * n >= MARCH_CELLS_PER_CU * cus:
