@@ -56,6 +56,19 @@ __device__ __forceinline__ double dpp(double v) {
 template <typename T> __device__ __forceinline__ T shr(T v) { return dpp<DPP_SHR>(v); }
 template <typename T> __device__ __forceinline__ T shl(T v) { return dpp<DPP_SHL>(v); }
 
+// panel-local components (e_i, e_j, n) -> Cartesian for a panel whose frame
+// vectors are signed coordinate axes (frame code of ops/fused.py::frame_code)
+template <typename T>
+__device__ __forceinline__ void frame_to_global(int fr, T xi, T xj, T xn, T& o0, T& o1, T& o2) {
+  const int ai = fr & 3, aj = (fr >> 2) & 3;
+  if (fr & 64) xi = -xi;
+  if (fr & 128) xj = -xj;
+  if (fr & 256) xn = -xn;
+  o0 = ai == 0 ? xi : (aj == 0 ? xj : xn);
+  o1 = ai == 1 ? xi : (aj == 1 ? xj : xn);
+  o2 = ai == 2 ? xi : (aj == 2 ? xj : xn);
+}
+
 // Waves per SIMD the register allocation must allow: fp32 fits 4 (<= 128
 // VGPRs); fp64 needs ~225 VGPRs, 2 waves (asking for 3 spills to scratch).
 #ifndef STSP_MARCH_WPE64
@@ -70,8 +83,13 @@ template <typename T> __device__ __forceinline__ T shl(T v) { return dpp<DPP_SHL
 #define STSP_MARCH_PROBE_NOWE 0
 #endif
 // ACC: the RK4 accumulator operands (acc_in / acc_out); the SSP-RK3 and Euler
-// stages run the instantiation without them (4 fewer live values per lane)
-template <typename T, int LIM, int R, bool ACC>
+// stages run the instantiation without them (4 fewer live values per lane).
+// CG: compact geometry: the panel-shared tables of the fused step (1/A,
+// curvature sum and centre by panel-local index, rotated by the panel frame;
+// edge lengths by panel-local index) instead of the per-tile records, and the
+// topography gradient formed from b itself (104 instead of 176 B per fp64 cell
+// through HBM; the shared tables are read by all six panels)
+template <typename T, int LIM, int R, bool ACC, bool CG>
 __global__ __launch_bounds__(MW * MWPB) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 8 ? STSP_MARCH_WPE64 : STSP_MARCH_WPE32)))
 void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   pin_args(a);
@@ -93,7 +111,8 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   const int y1 = y0 + R < n ? y0 + R : n;
   constexpr unsigned ES = sizeof(T);
   const unsigned tb = (unsigned)(tile * pw * pw);
-  const __amdgpu_buffer_rsrc_t rQ = brsrc(a.Q), rX = brsrc(a.X), rO = brsrc(a.out), rG = brsrc(a.cgeo);
+  const __amdgpu_buffer_rsrc_t rQ = brsrc(a.Q), rX = brsrc(a.X), rO = brsrc(a.out),
+                               rG = brsrc(CG ? (const T*)a.crec : a.cgeo);
   const unsigned fs = (unsigned)S * ES;              // field stride in bytes (soffset)
   const T g = a.g;
 
@@ -184,6 +203,22 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   const T* ext = a.ex + (long)tile * n * (n + 1);
   const T* eyt = a.ey + (long)tile * (n + 1) * n;
   const int* pm = a.push + (long)tile * 4 * mg * n;
+  // compact geometry: panel-local cell (I0 + x, J0 + y) of this tile's face
+  int I0 = 0, J0 = 0, fr = 0, Nf = n, Nf1 = n + 1;
+  if constexpr (CG) {
+    const int face = a.torg[3 * tile];
+    I0 = a.torg[3 * tile + 1];
+    J0 = a.torg[3 * tile + 2];
+    fr = (int)(a.frames >> (9 * face)) & 511;
+    Nf = a.Nf;
+    Nf1 = a.Nf + 1;
+  }
+  const int xg = I0 + (inx ? x : 0);                  // panel column of the lane (clamped)
+  const bool topo = CG && a.bpad != nullptr;
+  const __amdgpu_buffer_rsrc_t rB = brsrc(topo ? a.bpad : a.Q);
+  // edge lengths: x-face (j, x) and y-face (j', x) of this tile
+  auto len_x = [&](int j) -> T { return CG ? a.lxt[(J0 + j) * Nf1 + I0 + x] : ext[(long)j * (n + 1) + x]; };
+  auto len_y = [&](int jp) -> T { return CG ? a.lxt[xg * Nf1 + J0 + jp] : eyt[(long)jp * n + x]; };
   const bool need_x = (a.a0 != T(0)) || (ACC && a.c1 != T(0));
   const bool need_acc = ACC && a.acc_in && (a.c0 != T(0));
 
@@ -210,16 +245,27 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
     }
     if (peS && y0 == 0) nf_row(2, cm1, cm2, wl);     // the face below row 0 is a panel edge
     if (peN && y0 + 1 == n) { /* row y0 + 1 == n: its state enters only the loop's face */ }
-    Ls = inx ? eyt[(long)y0 * n + x] : T(0);
+    Ls = inx ? len_y(y0) : T(0);
     swe_flux<T>(wl, wr, cm1, cA, myt[0 * (n + 1) + y0], myt[1 * (n + 1) + y0], myt[2 * (n + 1) + y0], Ls, g, Gs);
   }
   T qn[4];                                           // raw row j + 2, loaded one step ahead
   ldq(cell(xc, y0 + 2), qn);
+  T bS = T(0), bA = T(0), bB = T(0), bn = T(0);       // topography of rows j - 1 .. j + 2 (CG)
+  if (topo) {
+    bS = bld<T>(rB, cell(xc, y0 - 1) * ES, 0);
+    bA = bld<T>(rB, cell(xc, y0) * ES, 0);
+    bB = bld<T>(rB, cell(xc, y0 + 1) * ES, 0);
+    bn = bld<T>(rB, cell(xc, y0 + 2) * ES, 0);
+  }
 
   for (int j = y0; j < y1; ++j) {
     T cC[5];
     prim(qn, cC);
-    if (j + 1 < y1) ldq(cell(xc, j + 3), qn);        // prefetch (row j + 3 <= n + 1)
+    const T bC = bn;
+    if (j + 1 < y1) {                                // prefetch (row j + 3 <= n + 1)
+      ldq(cell(xc, j + 3), qn);
+      if (topo) bn = bld<T>(rB, cell(xc, j + 3) * ES, 0);
+    }
     // own-row operands of row j (needed after the fluxes)
     const unsigned pc = cell(xc, j);
     T qo[4], xs[4], acs[ACC ? 4 : 1], rec[8];
@@ -234,10 +280,10 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) acs[f] = need_acc ? *o32(a.acc_in + f * S, pc) : T(0);
     }
-    const unsigned gc = (unsigned)((tile * n + j) * n + (inx ? x : 0));
+    const unsigned gc = CG ? (unsigned)((J0 + j) * Nf + xg) : (unsigned)((tile * n + j) * n + (inx ? x : 0));
     bld_rec8<T>(rG, gc * 8u * ES, rec);
-    const T Lw = xe_ok ? ext[(long)j * (n + 1) + x] : T(0);
-    const T Ln = inx ? eyt[(long)(j + 1) * n + x] : T(0);
+    const T Lw = xe_ok ? len_x(j) : T(0);
+    const T Ln = inx ? len_y(j + 1) : T(0);
     const T my0 = myt[0 * (n + 1) + j + 1], my1 = myt[1 * (n + 1) + j + 1], my2 = myt[2 * (n + 1) + j + 1];
     const T ms0 = myt[0 * (n + 1) + j], ms1 = myt[1 * (n + 1) + j], ms2 = myt[2 * (n + 1) + j];
 
@@ -315,10 +361,16 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
       for (int f = 0; f < 4; ++f) Fe[f] = shl(Fw[f]);
     }
     const T Le = shl(Lw);
+    const T bW = shr(bA), bE = shl(bA);               // (every lane: DPP reads the neighbours' registers)
 
     // ---- divergence, sources, RK combination, tangent projection, stores --------
     if (outl) {
-      const T iA = rec[0], r0 = rec[1], r1 = rec[2], r2 = rec[3];
+      const T iA = rec[0];
+      T r0 = rec[1], r1 = rec[2], r2 = rec[3], Sg[3] = {T(0), T(0), T(0)};
+      if constexpr (CG) {
+        frame_to_global(fr, rec[1], rec[2], rec[3], Sg[0], Sg[1], Sg[2]);   // curvature sum S = sum(L m)
+        frame_to_global(fr, rec[4], rec[5], rec[6], r0, r1, r2);            // cell centre
+      }
       T dq[4];
 #pragma unroll
       for (int f = 0; f < 4; ++f) dq[f] = -((Fe[f] - Fw[f]) + (Gn[f] - Gs[f])) * iA;
@@ -327,10 +379,25 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
       const T cor[3] = {r1 * qo[3] - r2 * qo[2], r2 * qo[1] - r0 * qo[3], r0 * qo[2] - r1 * qo[1]};
       const T pb = T(0.5) * g * h * h * iA, gh = g * h;
       const T mn[3] = {my0, my1, my2}, ms[3] = {ms0, ms1, ms2};
+      T gb[3] = {rec[4], rec[5], rec[6]};
+      if constexpr (CG) {
+        gb[0] = gb[1] = gb[2] = T(0);
+        if (topo) {
+          // grad b = (sum_e b_e L_e m_e - b S) / A with face averages b_e, projected
+          // onto the tangent plane (models/base.py::fv_gradient)
+          const T fE = T(0.5) * (bA + bE) * Le, fW = T(0.5) * (bW + bA) * Lw;
+          const T fN = T(0.5) * (bA + bB) * Ln, fS = T(0.5) * (bS + bA) * Ls;
+#pragma unroll
+          for (int k = 0; k < 3; ++k)
+            gb[k] = (((fE * mxe[k] - fW * mxc[k]) + (fN * mn[k] - fS * ms[k])) - bA * Sg[k]) * iA;
+          const T d = gb[0] * r0 + gb[1] * r1 + gb[2] * r2;
+          gb[0] -= d * r0; gb[1] -= d * r1; gb[2] -= d * r2;
+        }
+      }
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const T Sk = Le * mxe[k] - Lw * mxc[k] + Ln * mn[k] - Ls * ms[k];
-        const T src = -fc * cor[k] + pb * Sk - gh * rec[4 + k];
+        const T Sk = CG ? Sg[k] : Le * mxe[k] - Lw * mxc[k] + Ln * mn[k] - Ls * ms[k];
+        const T src = -fc * cor[k] + pb * Sk - gh * gb[k];
         dq[1 + k] += src;
       }
       T o[4];
@@ -384,6 +451,7 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
 #pragma unroll
     for (int f = 0; f < 4; ++f) { hsA[f] = hsB[f]; Gs[f] = Gn[f]; }
     Ls = Ln;
+    bS = bA; bA = bB; bB = bC;
   }
 }
 
@@ -393,10 +461,14 @@ int march_l(const StageDesc* d, hipStream_t s) {
   const int ncs = (d->n + MO - 1) / MO, nrs = (d->n + R - 1) / R;
   const int njobs = d->ntile * ncs * nrs;
   const int nb = (njobs + MWPB - 1) / MWPB;
-  if (d->acc_out)
-    hipLaunchKernelGGL((march_kernel<T, LIM, R, true>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
-  else
-    hipLaunchKernelGGL((march_kernel<T, LIM, R, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+  const bool cg = d->crec && d->lxt && d->torg;
+  if (d->acc_out) {
+    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, true, true>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+    else hipLaunchKernelGGL((march_kernel<T, LIM, R, true, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+  } else {
+    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, false, true>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+    else hipLaunchKernelGGL((march_kernel<T, LIM, R, false, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+  }
   return (int)hipGetLastError();
 }
 
@@ -439,8 +511,9 @@ __global__ void dpp_probe_kernel(const double* in, double* out, float* outf) {
 extern "C" int stsp_march_launch(int dtype, int rows, const StageDesc* d, hipStream_t stream) {
   if (d->xg || d->remote || d->blocks) return -13;
   if (d->pw != d->n + 2 * d->mg || d->mg < 2 || d->n < 2) return -5;
-  if (!d->pedge || !d->pe_base || !d->pe_t || !d->push || !d->cgeo || !d->mx || !d->my || !d->ex || !d->ey)
-    return -12;
+  if (!d->pedge || !d->pe_base || !d->pe_t || !d->push || !d->mx || !d->my) return -12;
+  const bool cg = d->crec && d->lxt && d->torg;
+  if (cg ? d->Nf < d->n : (!d->cgeo || !d->ex || !d->ey)) return -12;
   if (dtype == 1) return march_t<double>(rows, d, stream);
   if (dtype == 0) return march_t<float>(rows, d, stream);
   return -4;

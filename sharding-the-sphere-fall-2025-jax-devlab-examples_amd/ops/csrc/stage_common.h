@@ -339,6 +339,13 @@ struct Args {
   const int* pedge;
   const int* pe_base;
   const T* pe_t;
+  // streaming stage (march_kernel.hip)
+  const int* torg;
+  const T* crec;
+  const T* lxt;
+  const T* bpad;
+  int Nf;
+  unsigned long long frames;   // 9 bits per panel (ops/fused.py::frame_code)
 };
 
 #ifdef STSP_STAMPS
@@ -486,6 +493,13 @@ Args<T> make_args(const StageDesc* d) {
   a.pedge = d->pedge;
   a.pe_base = d->pe_base;
   a.pe_t = (const T*)d->pe_t;
+  a.torg = d->torg;
+  a.crec = (const T*)d->crec;
+  a.lxt = (const T*)d->lxt;
+  a.bpad = (const T*)d->bpad;
+  a.Nf = d->Nf;
+  a.frames = 0;
+  for (int k = 0; k < 6; ++k) a.frames |= (unsigned long long)(d->frames[k] & 511) << (9 * k);
   return a;
 }
 

@@ -59,6 +59,15 @@ typedef struct StageDesc {
   // the raw strip x of that layer, b = pe_base[t][s][k][j] (tile-local), t = pe_t[...]
   const int* pe_base;   // [T][4][3][n]
   const void* pe_t;     // [T][4][3][n] element type
+  // streaming stage only (march_kernel.hip): panel-shared geometry instead of
+  // the per-tile records (cgeo, ex, ey), and the topography itself instead of
+  // its gradient (ops/hip_compute.py::march_tables)
+  const int* torg;      // [T][3] face, I0, J0 of each tile
+  const void* crec;     // [Nf*Nf][8] 1/A, S (3), centre (3), 0 in panel-local components (ops/fused.py::kernel_geometry)
+  const void* lxt;      // [Nf][Nf+1] x-edge lengths; the y-edge (J', I) has length lxt[I][J']
+  const void* bpad;     // [S] topography in the padded layout, ghost ring filled (null: no topography)
+  int Nf;               // cells per panel edge
+  int frames[6];        // ops/fused.py::frame_code of each panel
 } StageDesc;
 
 int stsp_stage_launch(int phys, int dtype, int bx, int by, const StageDesc* d, hipStream_t stream);

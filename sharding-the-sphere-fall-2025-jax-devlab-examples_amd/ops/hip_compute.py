@@ -13,6 +13,7 @@ from __future__ import annotations
 import ctypes
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import native
@@ -31,6 +32,36 @@ MARCH_CELLS_PER_CU = 8192
 
 def march_supported(phys_id: int, limiter: int, remote: bool) -> bool:
     return phys_id == 2 and limiter != 4 and not remote
+
+
+def march_tables(engine) -> dict:
+    """Compact-geometry tables of the streaming stage (march_kernel.hip, CG):
+    tile origins, the panel-shared geometry of the fused step
+    (ops/fused.py::kernel_geometry: 1/A, curvature sum and centre per
+    panel-local cell, edge lengths, panel frames) and the topography b in the
+    padded state layout with its ghost ring filled through the same-rank halo
+    map (None without topography)."""
+    from .fused import kernel_geometry
+    e = engine
+    plan, lay = e.plan, e.layout
+    kg = kernel_geometry(lay, e.grid)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=e.dtype, device=e.device)
+    torg = np.array([lay.tile_origin(tid) for tid in plan.tiles], dtype=np.int32).reshape(-1, 3)
+    out = {"torg": torch.as_tensor(torg, device=e.device), "crec": t(kg["crec"]), "lxt": t(kg["lxt"]),
+           "frames": [int(v) for v in kg["frames"]], "bpad": None}
+    gf = getattr(e.physics, "global_fields", None)
+    if gf is not None:
+        b = np.asarray(gf(e.grid)[2], dtype=np.float64)
+        if np.any(b != 0):
+            n, P, ng = plan.n, plan.P, plan.ng
+            bp = np.zeros((plan.T, P, P))
+            for li, tid in enumerate(plan.tiles):
+                f, I0, J0 = lay.tile_origin(tid)
+                bp[li, ng:ng + n, ng:ng + n] = b[f, J0:J0 + n, I0:I0 + n]
+            flat = bp.reshape(-1)
+            flat[plan.halo_dst] = flat[plan.halo_src]
+            out["bpad"] = t(flat)
+    return out
 
 
 def block_threads_formula(bx: int, by: int, w10: bool = True) -> int:
@@ -156,6 +187,9 @@ class HipCompute:
         else:
             self.nbx, self.nby = -(-n // bx), -(-n // by)
         self.nblocks = T * self.nbx * self.nby
+        # streaming stage geometry: compact (panel-shared tables) unless STSP_MARCH_COMPACT=0
+        import os
+        self.mt = march_tables(e) if self.march and os.environ.get("STSP_MARCH_COMPACT", "1") != "0" else None
         t = e.tens
         F, S = phys.F, plan.S
         # ---- host-side shape contract checks ----------------------------
@@ -227,6 +261,13 @@ class HipCompute:
             d.pedge = p(t["pedge"])
         if "pe_base" in t:
             d.pe_base, d.pe_t = p(t["pe_base"]), p(t["pe_t"])
+        if self.mt is not None:
+            mt = self.mt
+            d.torg, d.crec, d.lxt = p(mt["torg"]), p(mt["crec"]), p(mt["lxt"])
+            d.bpad = p(mt["bpad"]) if mt["bpad"] is not None else 0
+            d.Nf = e.layout.N
+            for f in range(6):
+                d.frames[f] = mt["frames"][f]
         d.ntile = e.plan.T
         d.n = e.plan.n
         d.S = e.plan.S

@@ -40,6 +40,9 @@ class StageDesc(ctypes.Structure):
         ("nprod", ctypes.c_void_p), ("bmask", ctypes.c_void_p), ("epoch", ctypes.c_void_p), ("err", ctypes.c_void_p),
         ("timeout_ticks", ctypes.c_longlong),
         ("pedge", ctypes.c_void_p), ("pe_base", ctypes.c_void_p), ("pe_t", ctypes.c_void_p),
+        # streaming stage (march_kernel.hip)
+        ("torg", ctypes.c_void_p), ("crec", ctypes.c_void_p), ("lxt", ctypes.c_void_p), ("bpad", ctypes.c_void_p),
+        ("Nf", ctypes.c_int), ("frames", ctypes.c_int * 6),
     ]
 
 
