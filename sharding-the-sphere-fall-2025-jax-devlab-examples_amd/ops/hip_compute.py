@@ -187,9 +187,13 @@ class HipCompute:
         else:
             self.nbx, self.nby = -(-n // bx), -(-n // by)
         self.nblocks = T * self.nbx * self.nby
-        # streaming stage geometry: compact (panel-shared tables) unless STSP_MARCH_COMPACT=0
+        # streaming stage geometry: compact (panel-shared tables, grad b from b) for fp64,
+        # per-tile records for fp32 (C720 64x4: fp64 409 vs 415 us/step, fp32 225 vs 195,
+        # where the compact path spills; profiles/r3_march/sizes_compact_geometry_ab.log);
+        # STSP_MARCH_COMPACT=0/1 overrides
         import os
-        self.mt = march_tables(e) if self.march and os.environ.get("STSP_MARCH_COMPACT", "1") != "0" else None
+        cg = os.environ.get("STSP_MARCH_COMPACT", "1" if e.dtype == torch.float64 else "0") != "0"
+        self.mt = march_tables(e) if self.march and cg else None
         t = e.tens
         F, S = phys.F, plan.S
         # ---- host-side shape contract checks ----------------------------
