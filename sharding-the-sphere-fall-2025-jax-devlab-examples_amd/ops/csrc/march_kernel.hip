@@ -77,21 +77,6 @@ __device__ __forceinline__ void frame_to_global(int fr, T xi, T xj, T xn, T& o0,
 #ifndef STSP_MARCH_WPE32
 #define STSP_MARCH_WPE32 4
 #endif
-// with the own-row prefetch (PF): fp64 1 wave per SIMD, fp32 3
-#ifndef STSP_MARCH_WPE64_PF
-#define STSP_MARCH_WPE64_PF 1
-#endif
-#ifndef STSP_MARCH_WPE32_PF
-#define STSP_MARCH_WPE32_PF 3
-#endif
-// own-row operands one row ahead (march_kernel PF); STSP_MARCH_PF=0/1 (A/B)
-inline bool march_pf() {
-  static const int v = [] {
-    const char* e = std::getenv("STSP_MARCH_PF");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v != 0;
-}
 // timing-only probe (wrong numerics; build variant "mprobe"): no W / E
 // panel-edge treatment, to price its registers
 #ifndef STSP_MARCH_PROBE_NOWE
@@ -104,10 +89,8 @@ inline bool march_pf() {
 // edge lengths by panel-local index) instead of the per-tile records, and the
 // topography gradient formed from b itself (104 instead of 176 B per fp64 cell
 // through HBM; the shared tables are read by all six panels)
-template <typename T, int LIM, int R, bool ACC, bool CG, bool PF>
-__global__ __launch_bounds__(MW * MWPB)
-__attribute__((amdgpu_waves_per_eu(sizeof(T) == 8 ? (PF ? STSP_MARCH_WPE64_PF : STSP_MARCH_WPE64)
-                                                 : (PF ? STSP_MARCH_WPE32_PF : STSP_MARCH_WPE32))))
+template <typename T, int LIM, int R, bool ACC, bool CG>
+__global__ __launch_bounds__(MW * MWPB) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 8 ? STSP_MARCH_WPE64 : STSP_MARCH_WPE32)))
 void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   pin_args(a);
   const int lane = threadIdx.x & 63;
@@ -267,22 +250,6 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   }
   T qn[4];                                           // raw row j + 2, loaded one step ahead
   ldq(cell(xc, y0 + 2), qn);
-  auto load_own = [&](int j, T (&qo)[4], T (&xs)[4], T (&rec)[8], T& Lw, T& Ln) {
-    const unsigned pc = cell(xc, j);
-    ldq(pc, qo);
-#pragma unroll
-    for (int f = 0; f < 4; ++f) xs[f] = T(0);
-    if (need_x) {
-#pragma unroll
-      for (int f = 0; f < 4; ++f) xs[f] = bld<T>(rX, pc * ES, f * fs);
-    }
-    const unsigned gc = CG ? (unsigned)((J0 + j) * Nf + xg) : (unsigned)((tile * n + j) * n + (inx ? x : 0));
-    bld_rec8<T>(rG, gc * 8u * ES, rec);
-    Lw = xe_ok ? len_x(j) : T(0);
-    Ln = inx ? len_y(j + 1) : T(0);
-  };
-  T nqo[PF ? 4 : 1], nxs[PF ? 4 : 1], nrec[PF ? 8 : 1], nLw = T(0), nLn = T(0);
-  if constexpr (PF) load_own(y0, nqo, nxs, nrec, nLw, nLn);
   T bS = T(0), bA = T(0), bB = T(0), bn = T(0);       // topography of rows j - 1 .. j + 2 (CG)
   if (topo) {
     bS = bld<T>(rB, cell(xc, y0 - 1) * ES, 0);
@@ -299,25 +266,24 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
       ldq(cell(xc, j + 3), qn);
       if (topo) bn = bld<T>(rB, cell(xc, j + 3) * ES, 0);
     }
-    // own-row operands of row j (needed after the fluxes); PF: loaded one row
-    // ahead, so a row's memory round trip overlaps the previous row's fluxes
+    // own-row operands of row j (needed after the fluxes)
     const unsigned pc = cell(xc, j);
-    T qo[4], xs[4], acs[ACC ? 4 : 1], rec[8], Lw, Ln;
-    if constexpr (PF) {
+    T qo[4], xs[4], acs[ACC ? 4 : 1], rec[8];
+    ldq(pc, qo);
 #pragma unroll
-      for (int f = 0; f < 4; ++f) { qo[f] = nqo[f]; xs[f] = nxs[f]; }
+    for (int f = 0; f < 4; ++f) xs[f] = T(0);
+    if (need_x) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) rec[k] = nrec[k];
-      Lw = nLw;
-      Ln = nLn;
-      if (j + 1 < y1) load_own(j + 1, nqo, nxs, nrec, nLw, nLn);
-    } else {
-      load_own(j, qo, xs, rec, Lw, Ln);
+      for (int f = 0; f < 4; ++f) xs[f] = bld<T>(rX, pc * ES, f * fs);
     }
     if constexpr (ACC) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) acs[f] = need_acc ? *o32(a.acc_in + f * S, pc) : T(0);
     }
+    const unsigned gc = CG ? (unsigned)((J0 + j) * Nf + xg) : (unsigned)((tile * n + j) * n + (inx ? x : 0));
+    bld_rec8<T>(rG, gc * 8u * ES, rec);
+    const T Lw = xe_ok ? len_x(j) : T(0);
+    const T Ln = inx ? len_y(j + 1) : T(0);
     const T my0 = myt[0 * (n + 1) + j + 1], my1 = myt[1 * (n + 1) + j + 1], my2 = myt[2 * (n + 1) + j + 1];
     const T ms0 = myt[0 * (n + 1) + j], ms1 = myt[1 * (n + 1) + j], ms2 = myt[2 * (n + 1) + j];
 
@@ -496,16 +462,12 @@ int march_l(const StageDesc* d, hipStream_t s) {
   const int njobs = d->ntile * ncs * nrs;
   const int nb = (njobs + MWPB - 1) / MWPB;
   const bool cg = d->crec && d->lxt && d->torg;
-  const dim3 g(nb), b(MW * MWPB);
-  if (d->acc_out) {        // RK4: no prefetch variant (rarely used on large grids)
-    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, true, true, false>), g, b, 0, s, a, ncs, nrs, njobs);
-    else hipLaunchKernelGGL((march_kernel<T, LIM, R, true, false, false>), g, b, 0, s, a, ncs, nrs, njobs);
-  } else if (march_pf()) {
-    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, false, true, true>), g, b, 0, s, a, ncs, nrs, njobs);
-    else hipLaunchKernelGGL((march_kernel<T, LIM, R, false, false, true>), g, b, 0, s, a, ncs, nrs, njobs);
+  if (d->acc_out) {
+    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, true, true>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+    else hipLaunchKernelGGL((march_kernel<T, LIM, R, true, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
   } else {
-    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, false, true, false>), g, b, 0, s, a, ncs, nrs, njobs);
-    else hipLaunchKernelGGL((march_kernel<T, LIM, R, false, false, false>), g, b, 0, s, a, ncs, nrs, njobs);
+    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, false, true>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+    else hipLaunchKernelGGL((march_kernel<T, LIM, R, false, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
   }
   return (int)hipGetLastError();
 }
