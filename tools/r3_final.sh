@@ -40,12 +40,12 @@ for set in "FETCH_SIZE GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_
            "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32"; do
   for dt in fp64 fp32; do
     timeout -s KILL 90 rocprofv3 --pmc $set -d $OUT/pmc_$dt/pmc$i -o k --output-format csv -- \
-      python3 $ROOT/tools/kprobe.py --reps 10 --N 720 --t 1 --dtype $dt --blocks 64x8 > $OUT/pmc_${dt}_$i.log 2>&1 || { echo "pmc $dt $i failed"; tail -3 $OUT/pmc_${dt}_$i.log; exit 5; }
+      python3 $ROOT/tools/kprobe.py --reps 10 --N 720 --t 1 --dtype $dt --blocks 64x4 > $OUT/pmc_${dt}_$i.log 2>&1 || { echo "pmc $dt $i failed"; tail -3 $OUT/pmc_${dt}_$i.log; exit 5; }
   done
   i=$((i+1))
 done
 for dt in fp64 fp32; do
-  timeout -k 10 100 python3 $ROOT/tools/kprobe.py --reps 50 --N 720 --t 1 --dtype $dt --blocks 64x8,8x8,16x8 > $OUT/kprobe_$dt.json 2>&1
+  timeout -k 10 100 python3 $ROOT/tools/kprobe.py --reps 50 --N 720 --t 1 --dtype $dt --blocks 64x4,64x8,8x8,16x8 > $OUT/kprobe_$dt.json 2>&1
   python3 $ROOT/tools/pmc_summary.py march_kernel $OUT/pmc_$dt > $OUT/pmc_${dt}_summary.txt
   echo "== $dt"; cat $OUT/pmc_${dt}_summary.txt
 done
