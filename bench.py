@@ -247,7 +247,10 @@ def main():
                 B = fused_block(layout.n)
                 nb = len(layout.plan(rank).tiles) * (layout.n // B) ** 2
                 cus = torch.cuda.get_device_properties(device).multi_processor_count if device.type == "cuda" else 256
-                if nb <= cus:
+                # one GPU up to two passes over the CUs: one fused launch per step still
+                # beats three stage launches (C180, 3 tiles per edge, 486 blocks: 38.6 vs
+                # 44.5 us/step, profiles/r3_march/c180_fused_b20.log)
+                if nb <= cus or (world == 1 and nb <= 2 * cus):
                     runtime = "fused"
             del probe
     comm = a.comm if world > 1 else "none"
