@@ -62,9 +62,10 @@ def parse(argv=None):
     ap.add_argument("--steps-per-launch", type=int, default=0,
                     help="fused runtime: steps inside one kernel launch (0 = auto: the largest even divisor of "
                          "--steps up to 64 when every block fits on the GPU at once; 1 = one launch per step)")
-    ap.add_argument("--launch", default="direct", choices=["direct", "graph"],
-                    help="fused runtime: issue each multi-step kernel launch directly (default) or replay it "
-                         "from a hipGraph (a one-kernel graph only adds hipGraphLaunch's host floor)")
+    ap.add_argument("--launch", default="auto", choices=["auto", "direct", "graph"],
+                    help="fused runtime: issue each multi-step kernel launch directly or replay it from a "
+                         "hipGraph (a one-kernel graph only adds hipGraphLaunch's host floor); auto: direct on "
+                         "one GPU, graph across GPUs (the path the multi-rank rehearsals validated)")
     ap.add_argument("--steps-per-graph", type=int, default=0,
                     help="steps recorded per graph (0 = the whole timed run in one graph)")
     ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "rccl"],
@@ -306,7 +307,7 @@ def main():
                 spl = max([k for k in range(2, 65, 2) if a.steps % k == 0], default=1) if fk.plan.nb <= cus else 1
             info["steps_per_launch"] = spl
             runner = NativeStepper(eng, use_graph=True, steps_per_graph=spg, fused=fk, steps_per_launch=spl,
-                                   direct=a.launch == "direct")
+                                   direct=a.launch == "direct" or (a.launch == "auto" and world == 1))
         elif runtime == "native":
             # C++ runtime, hipGraph replay; between GPUs either direct xGMI
             # stores from the stage kernels (graph-captured) or RCCL grouped
