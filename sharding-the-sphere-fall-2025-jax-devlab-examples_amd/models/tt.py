@@ -310,9 +310,10 @@ class LowRankDiffusion:
                  backend: str = "torch", substeps: int = 1, qr: str = "cholqr3"):
         self.h = L / (N + 1) if bc == "dirichlet" else L / N
         # hip recompression: "cholqr3" (device CholeskyQR3, machine-precision
-        # factors, one host transfer of the k x k core) or "gram" (the native
-        # Gram/eigen step, ~sqrt(eps) accuracy; kept for comparison)
-        if qr not in ("cholqr3", "gram"):
+        # factors, one host transfer of the k x k core; composed in Python),
+        # "cholqr3n" (the same in one native call, stsp_tt_lr_step3) or "gram"
+        # (the native Gram/eigen step, ~sqrt(eps) accuracy; kept for comparison)
+        if qr not in ("cholqr3", "cholqr3n", "gram"):
             raise ValueError(f"unknown qr {qr!r}")
         self.qr = qr
         self.bc = bc
@@ -350,10 +351,44 @@ class LowRankDiffusion:
         return recompress(A, B, self.eps, self.max_rank)
 
     def _step_hip_cqr(self, U: LowRankField, dt: float) -> LowRankField:
-        """The rank-doubling form [A, c D A] [B + c D B, B]^T per substep on the
-        device (ops/tt_ops.expand), then one CholeskyQR3 recompression
-        (``recompress_many``: MFMA Gram / product kernels, the k x k shifted
-        Cholesky kernel, one host transfer of the core)."""
+        if self.qr == "cholqr3n":
+            return self._step_hip_cqr_native(U, dt)
+        return self._step_hip_cqr_py(U, dt)
+
+    def _step_hip_cqr_native(self, U: LowRankField, dt: float) -> LowRankField:
+        """The rank-doubling form [A, c D A] [B + c D B, B]^T per substep, then
+        one CholeskyQR3 recompression, as ONE native call
+        (ops/csrc/tt_kernels.hip, stsp_tt_lr_step3: expansion, three passes per
+        factor of MFMA Gram / shifted-Cholesky kernel / MFMA product, one host
+        round trip for the six k x k R factors, the core SVD on the host, two
+        MFMA products).  ``_step_hip_cqr_py`` is the same step composed in
+        Python (``recompress_many``)."""
+        from ..ops import native
+        L = native.require_native()
+        N, r = U.A.shape
+        ns = self.substeps
+        if (r << ns) > 64:
+            raise ValueError(f"hip low-rank step: rank {r} x 2^{ns} substeps exceeds the 64-column kernels")
+        A = U.A if U.A.stride(1) == 1 else U.A.contiguous()
+        B = U.B if U.B.stride(1) == 1 else U.B.contiguous()
+        dev, dt_ = A.device, A.dtype
+        k = r << ns
+        key = ("cqr", N, r, ns, dt_, dev)
+        if getattr(self, "_wkey3", None) != key:
+            self._ws3 = torch.empty(L.stsp_tt_step_workspace3(N, r, ns), dtype=dt_, device=dev)
+            self._hbuf3 = torch.empty(8 * k * k + 8, dtype=torch.float64).pin_memory()
+            self._wkey3 = key
+        rmax = k if self.max_rank is None else min(k, self.max_rank)
+        out = torch.empty((2, N, rmax), dtype=dt_, device=dev)
+        rn = L.stsp_tt_lr_step3(native.dtype_code(dt_), native.ptr(A), A.stride(0), native.ptr(B), B.stride(0), N, r,
+                                ns, dt * self.kappa, 1.0 / (self.h * self.h), int(self.bc == "periodic"), self.eps,
+                                self.max_rank or 0, native.ptr(self._ws3), native.ptr(self._hbuf3),
+                                native.ptr(out[0]), native.ptr(out[1]), rmax, native.current_stream_handle())
+        if rn <= 0:
+            raise RuntimeError(f"stsp_tt_lr_step3 failed ({rn})")
+        return LowRankField(out[0, :, :rn], out[1, :, :rn])
+
+    def _step_hip_cqr_py(self, U: LowRankField, dt: float) -> LowRankField:
         from ..ops import tt_ops
         c = dt * self.kappa
         ih2 = 1.0 / (self.h * self.h)

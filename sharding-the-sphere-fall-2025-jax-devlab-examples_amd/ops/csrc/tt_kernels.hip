@@ -693,6 +693,139 @@ int stsp_tt_lr_step2(int dtype, const void* A, int lda, const void* B, int ldb, 
   return rn;
 }
 
+// The same step with the CholeskyQR3 recompression (models/tt.py::cholqr3) in
+// one native call: expansion, three passes per factor of {MFMA Gram, shifted
+// Cholesky + inverse (chol_inv_kernel), MFMA product}, one device-to-host copy
+// of the six k x k R factors and pivot flags, the core C = Ra Rb^T and its
+// one-sided Jacobi SVD on the host, one host-to-device copy, two MFMA products.
+// Workspace: stsp_tt_step_workspace3 elements; hbuf: 8 k^2 + 8 doubles.
+size_t stsp_tt_step_workspace3(int N, int r, int nsub) {
+  const int k = r << nsub, kp = (k + 15) / 16 * 16;
+  return (size_t)2 * 2 * N * k + 2 * (size_t)k * k + (size_t)stsp_tt_gram_blocks(N) * kp * kp + (size_t)k * 2 * k +
+         (size_t)12 * k * k + 16;
+}
+
+int stsp_tt_lr_step3(int dtype, const void* A, int lda, const void* B, int ldb, int N, int r, int nsub, double c,
+                     double ih2, int periodic, double eps, int max_rank, void* ws, double* hbuf, void* Aout,
+                     void* Bout, int ldo, hipStream_t st) {
+  if (N < 1 || r < 1 || nsub < 1 || nsub > 6) return -1;
+  const int k = r << nsub;
+  if (k > 64) return -1;
+  const size_t es = dtype == 1 ? 8 : 4;
+  char* w = (char*)ws;
+  void* buf[2][2] = {{w, w + es * (size_t)N * k}, {w + es * 2 * (size_t)N * k, w + es * 3 * (size_t)N * k}};
+  void* G = w + es * 4 * (size_t)N * k;
+  void* part = (char*)G + es * 2 * (size_t)k * k;
+  const int P = stsp_tt_gram_blocks(N);
+  const int kp = (k + 15) / 16 * 16;
+  void* dX = (char*)part + es * (size_t)P * kp * kp;
+  char* Rs = (char*)dX + es * (size_t)2 * k * k;          // [side][pass][R, Ri] k x k
+  int* dinfo = (int*)(Rs + es * (size_t)12 * k * k);       // [side][pass]
+  auto Rp = [&](int side, int pass, int inv) { return (void*)(Rs + es * (size_t)((side * 3 + pass) * 2 + inv) * k * k); };
+  int rc;
+  const void* srcA = A;
+  const void* srcB = B;
+  int sa = lda, sb = ldb, rr = r, cur = 0;
+  for (int s = 0; s < nsub; ++s, rr *= 2) {
+    void* dA = buf[cur][0];
+    void* dB = buf[cur][1];
+    if ((rc = stsp_tt_expand(dtype, srcA, sa, dA, 2 * rr, N, rr, 1.0, 0.0, 0.0, c, ih2, periodic, st))) return rc;
+    if ((rc = stsp_tt_expand(dtype, srcB, sb, dB, 2 * rr, N, rr, 1.0, c, 1.0, 0.0, ih2, periodic, st))) return rc;
+    srcA = dA;
+    srcB = dB;
+    sa = sb = 2 * rr;
+    cur ^= 1;
+  }
+  // shift coefficient 11 (N k + k (k + 1)) u (models/tt.py::cholqr3_shift)
+  const double u = dtype == 1 ? 1.1102230246251565e-16 : 5.960464477539063e-08;
+  const double shc = 11.0 * ((double)N * k + (double)k * (k + 1)) * u;
+  void* Q[2] = {(void*)srcA, (void*)srcB};
+  int qb = cur;     // the free buffer set
+  for (int side = 0; side < 2; ++side) {
+    int qcur = qb;
+    for (int pass = 0; pass < 3; ++pass) {
+      if ((rc = stsp_tt_gram(dtype, Q[side], k, Q[side], k, N, k, k, part, P, G, k, 1.0, st))) return rc;
+      if ((rc = stsp_tt_chol_inv(dtype, G, k, 0, Rp(side, pass, 0), Rp(side, pass, 1), k, 0, k, 1,
+                                 pass == 0 ? shc : -shc, dinfo + side * 3 + pass, st)))
+        return rc;
+      void* dst = buf[qcur][side];
+      if ((rc = stsp_tt_mm(dtype, Q[side], k, Rp(side, pass, 1), k, dst, k, N, k, k, 1.0, 0.0, st))) return rc;
+      // the next pass reads dst; its own output goes to the buffer Q held
+      void* old = Q[side];
+      Q[side] = dst;
+      buf[qcur][side] = old;
+    }
+  }
+  // R factors (not the inverses) and flags to the host in one copy each
+  double* hR = hbuf;                 // [side][pass] k x k
+  int* hinfo = (int*)(hbuf + 6 * k * k);
+  double* hX = hbuf + 6 * k * k + 8;
+  for (int side = 0; side < 2; ++side)
+    for (int pass = 0; pass < 3; ++pass)
+      if (hipMemcpyAsync((char*)hR + es * (size_t)(side * 3 + pass) * k * k, Rp(side, pass, 0), es * (size_t)k * k,
+                         hipMemcpyDeviceToHost, st) != hipSuccess)
+        return -20;
+  if (hipMemcpyAsync(hinfo, dinfo, sizeof(int) * 6, hipMemcpyDeviceToHost, st) != hipSuccess) return -20;
+  if (hipStreamSynchronize(st) != hipSuccess) return -21;
+  for (int i = 0; i < 6; ++i)
+    if (hinfo[i] != 0) return -24;
+  if (dtype == 0) {
+    const float* f = (const float*)hR;
+    for (int i = 6 * k * k - 1; i >= 0; --i) hR[i] = (double)f[i];
+  }
+  // R = R3 R2 R1 per side, core C = Ra Rb^T
+  std::vector<double> Rt[2], tmp(k * k), C(k * k), sig(k), W(k * k);
+  for (int side = 0; side < 2; ++side) {
+    Rt[side].assign(hR + (size_t)(side * 3) * k * k, hR + (size_t)(side * 3 + 1) * k * k);
+    for (int pass = 1; pass < 3; ++pass) {
+      const double* Rk = hR + (size_t)(side * 3 + pass) * k * k;
+      for (int i = 0; i < k; ++i)
+        for (int j = 0; j < k; ++j) {
+          double acc = 0;
+          for (int l = i; l < k; ++l) acc += Rk[i * k + l] * Rt[side][l * k + j];   // Rk upper triangular
+          tmp[i * k + j] = acc;
+        }
+      Rt[side] = tmp;
+    }
+  }
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) {
+      double acc = 0;
+      for (int l = 0; l < k; ++l) acc += Rt[0][i * k + l] * Rt[1][j * k + l];
+      C[i * k + j] = acc;
+    }
+  jacobi_svd(k, k, C.data(), sig.data(), W.data());       // C = (U S) W^T, U S in C's columns
+  std::vector<int> ord(k);
+  for (int j = 0; j < k; ++j) ord[j] = j;
+  std::sort(ord.begin(), ord.end(), [&](int a, int b) { return sig[a] > sig[b]; });
+  double tot = 0;
+  for (int j = 0; j < k; ++j) tot += sig[j] * sig[j];
+  int rn = k;
+  double tail = 0;
+  for (int jj = k - 1; jj >= 1; --jj) {
+    tail += sig[ord[jj]] * sig[ord[jj]];
+    if (tail <= eps * eps * tot) rn = jj;
+    else break;
+  }
+  if (max_rank > 0) rn = std::min(rn, max_rank);
+  rn = std::max(rn, 1);
+  if (!(tot > 0)) return -22;
+  for (int i = 0; i < k; ++i)
+    for (int jj = 0; jj < rn; ++jj) {
+      const int j = ord[jj];
+      hX[i * 2 * k + jj] = C[i * k + j];
+      hX[i * 2 * k + rn + jj] = W[i * k + j];
+    }
+  if (dtype == 0) {
+    float* f = (float*)hX;
+    for (int i = 0; i < 2 * k * k; ++i) f[i] = (float)hX[i];
+  }
+  if (hipMemcpyAsync(dX, hX, es * 2 * k * k, hipMemcpyHostToDevice, st) != hipSuccess) return -23;
+  if ((rc = stsp_tt_mm(dtype, Q[0], k, dX, 2 * k, Aout, ldo, N, k, rn, 1.0, 0.0, st))) return rc;
+  if ((rc = stsp_tt_mm(dtype, Q[1], k, (char*)dX + es * rn, 2 * k, Bout, ldo, N, k, rn, 1.0, 0.0, st))) return rc;
+  return rn;
+}
+
 int stsp_tt_lr_step(int dtype, const void* A, int lda, const void* B, int ldb, int N, int r, double c, double ih2,
                     int periodic, double eps, int max_rank, void* ws, double* hbuf, void* Aout, void* Bout, int ldo,
                     hipStream_t st) {

@@ -262,3 +262,21 @@ def test_cube_low_rank_diffusion_hip_cholqr3_machine_precision():
     torch.cuda.synchronize()
     assert max(f.rank for f in F) <= 30
     assert float((mh.to_dense(F) - D).norm() / D.norm()) < 1e-10
+
+
+@pytest.mark.gpu
+def test_native_cholqr3_step_matches_python_composition():
+    """stsp_tt_lr_step3 (one native call) and the Python-composed CholeskyQR3
+    step give the same factored field (to rounding), fp64 and 2 substeps."""
+    N = 384
+    U = _panel(N)
+    for ns in (1, 2):
+        s = tt.LowRankDiffusion(N, kappa=1.0, eps=1e-12, max_rank=16 if ns == 2 else None, backend="hip", substeps=ns,
+                                qr="cholqr3n")
+        lr = tt.LowRankField.from_dense(U.cuda(), eps=1e-14)
+        dt = 0.5 * s.dt_max
+        a = s.step(lr, dt)
+        b = s._step_hip_cqr_py(lr, dt)
+        torch.cuda.synchronize()
+        da, db = a.dense(), b.dense()
+        assert float((da - db).norm() / db.norm()) < 1e-12

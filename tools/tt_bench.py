@@ -56,7 +56,7 @@ def main():
     ap.add_argument("--eps", type=float, default=1e-8)
     ap.add_argument("--max-rank", type=int, default=16)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--qr", default="cholqr3", choices=["cholqr3", "gram"],
+    ap.add_argument("--qr", default="cholqr3", choices=["cholqr3", "cholqr3n", "gram"],
                     help="hip recompression: device CholeskyQR3 (default) or the native Gram/eigen step")
     ap.add_argument("--substeps", default="1,2,3",
                     help="explicit steps per recompression (tt us is per simulated step)")
