@@ -67,6 +67,7 @@ class Solver:
         self.engines: List[Engine] = []
         self.cluster: Optional[VirtualCluster] = None
         self.runner = None            # NativeStepper (GPU) once stepping starts
+        self.fused = None             # ops/fused.py::FusedKernel when the runner steps with it
         self.xgmi = None
         self._nccl = None
         self.comm = "local"
@@ -298,10 +299,60 @@ class Solver:
             return c.graph
         return self.mode == "spmd" and self.comm in ("xgmi", "rccl")
 
-    def _make_runner(self):
+    def _fused_plan(self, chunk: int):
+        """(use the fused step, steps per launch) for this run.  The fused
+        SSP-RK3 step (ops/fused.py) is the flagship path: one launch advances
+        a rank by several steps (every block resident, in-launch hand-offs), the
+        reference's "one compiled program" (PY:238-246; PDF s.10) driven from the
+        solver (PDF s.6 pipeline).  auto: shallow water + SSP-RK3 + PLR, one GPU
+        or SPMD ranks with the direct xGMI exchange, and at most two passes of
+        blocks over the CUs (one step per launch beyond one pass)."""
+        from .ops.fused import fused_block, fused_supported
+        c = self.cfg.runtime
+        e = self.engines[0]
+        if c.fused == "off" or e.device.type != "cuda":
+            return False, 1
+        if not (self.mode == "single" or (self.mode == "spmd" and self.comm == "xgmi")):
+            if c.fused == "on":
+                raise ValueError(f"runtime.fused = on needs one GPU or the xgmi exchange (mode {self.mode}, "
+                                 f"comm {self.comm})")
+            return False, 1
+        why = fused_supported(e)
+        if why:
+            if c.fused == "on":
+                raise ValueError(why)
+            return False, 1
+        B = fused_block(e.plan.n)
+        nb = len(e.plan.tiles) * (e.plan.n // B) ** 2
+        cus = torch.cuda.get_device_properties(e.device).multi_processor_count
+        if c.fused == "auto" and nb > (2 * cus if self.mode == "single" else cus):
+            return False, 1
+        if nb > cus:
+            return True, 1                     # one step per launch (blocks not all resident)
+        spl = c.steps_per_launch
+        if spl <= 0:
+            k = max(1, chunk)
+            divs = [s for s in range(2, 41, 2) if k % s == 0]
+            spl = max(divs) if divs else (min(40, k - k % 2) if k >= 2 else 1)
+        if spl > 1 and spl % 2:
+            raise ValueError("runtime.steps_per_launch must be even")
+        return True, spl
+
+    def _make_runner(self, chunk: int = 20):
         from .ops.native_runtime import NativeStepper, create_nccl_comm
         e = self.engines[0]
         c = self.cfg.runtime
+        use_fused, spl = self._fused_plan(chunk)
+        self.fused = None
+        if use_fused:
+            from .ops.fused import FusedKernel
+            fk = FusedKernel(e)                  # collective with several ranks (xGMI ring setup)
+            self.fused = fk
+            self.xgmi = fk if self.mode == "spmd" else None
+            self._log(f"Runtime: fused SSP-RK3 step, {fk.plan.nb} blocks of {fk.plan.B}x{fk.plan.B}, "
+                      f"{spl} step(s) per launch, " + ("direct launches" if self.mode == "single" else "graph replay"))
+            return NativeStepper(e, use_graph=True, steps_per_graph=c.steps_per_graph, fused=fk,
+                                 steps_per_launch=spl, direct=self.mode == "single")
         xg = nc = None
         if self.mode == "spmd" and self.comm == "xgmi":
             from .ops.xgmi import XgmiHalo
@@ -412,8 +463,6 @@ class Solver:
                 self._snapshot_history(hist, 0, pending, async_copy=False)
                 drain(block=True)
             if self._use_native() and nsteps > 0:
-                if self.runner is None:
-                    self.runner = self._make_runner()
                 lens, p, it = [], 0, 0
                 while p < end and it < 100000:        # the chunk sequence of a run without recovery
                     k = chunk_at(p, SUB)
@@ -421,6 +470,8 @@ class Solver:
                         lens.append(k)
                     p += k * SUB
                     it += 1
+                if self.runner is None:
+                    self.runner = self._make_runner(chunk=lens[0])
                 per = self.runner.period
                 self.runner.graph_periods = max(1, min(max(lens), 512) // per)
                 for k in lens[:8]:
@@ -497,6 +548,10 @@ class Solver:
                    "sim_days_per_day": ((self.time - t0) / DAY) / max(wall / DAY, 1e-30),
                    "recoveries": recoveries, "dt_final": self.dt,
                    "graph_steps": (self.runner.stats["graph_steps"] if self.runner is not None else 0),
+                   "runtime": ("fused" if getattr(self, "fused", None) is not None else
+                               "native" if self.runner is not None else "eager"),
+                   "fused_direct_steps": (self.runner.stats["direct_steps"] if self.runner is not None else 0),
+                   "kernel_launches": (self.runner.stats["launches"] if self.runner is not None else 0),
                    "phase_s": dict(ph.times)}
         summary.update(self.diagnostics())
         norms = self.error_norms()

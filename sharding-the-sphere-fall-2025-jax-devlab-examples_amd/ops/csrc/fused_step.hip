@@ -58,8 +58,16 @@ struct FD {
   static constexpr int H1 = B + 4 * (NS - 1);
   static constexpr int NFX = H1 * (H1 + 1);
   static constexpr int NFL = 2 * NFX;
-  static constexpr int NT = 1024;
-  static_assert(W * W <= NT, "one owner thread per window cell");
+  // Threads: 768 (12 waves, 3 per SIMD, up to 168 VGPRs) where the cells
+  // stage 1 updates fit, else 1024 (128 VGPRs).  At 1024 threads the kernel
+  // spilled 36-58 VGPRs, some of them reloaded inside the face loops (a
+  // vmcnt wait per reload); the face work per SIMD is the same either way.
+  // Each thread owns one window cell in owner order; the outer-ring cells
+  // beyond NT (loaded each step, never updated) are "tail" cells of threads
+  // [NU, NT).
+  static constexpr int NU = H1 * H1;               // cells stage 1 updates
+  static constexpr int NT = NU <= 768 ? 768 : 1024;
+  static_assert(NU <= NT && W * W <= 2 * NT, "owner threads for every updated cell");
   static_assert(GMAX <= NT, "one fix-up thread per ghost entry");
   static constexpr int CMAX = 32;
 };
@@ -227,10 +235,10 @@ __device__ __forceinline__ int ncode(unsigned long long c, int side) {
 }
 
 template <typename T, int LIM, int NS, int B, bool XG, bool MULTI>
-__global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
+__global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a) {
   using D = FD<NS, B>;
   constexpr int W = D::W, WS = D::WS, WW = D::WW, GB = D::GB, R = D::R, L1 = D::L1, H1 = D::H1;
-  constexpr int NFX = D::NFX, NFL = D::NFL, NT = D::NT;
+  constexpr int NFX = D::NFX, NFL = D::NFL, NT = D::NT, NU = D::NU;
   constexpr int NN = 2 * 5 * 3 * (W + 1);
   // primitives h, vx, vy, vz and sound speed of the window cells, then (fields
   // 0-3) the values of the block's ghost entries, refreshed before each stage's faces
@@ -247,6 +255,7 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   // a0 X term of SSP-RK3; in LDS rather than registers (register pressure)
   constexpr int NX2 = NS > 1 ? (B + 4 * (NS - 2)) * (B + 4 * (NS - 2)) : 1;
   __shared__ T s_x[4][NX2];
+  __shared__ int s_gdone;                  // ghost waves done, cumulative over the launch's stages
 
   const int tid = threadIdx.x;
   const int bid = xcd_remap(blockIdx.x, a.nblocks);
@@ -255,6 +264,9 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   const int X0 = og[0], Y0 = og[1], tile = og[2], ow = og[3];
   const int xo = ow & 0xFFF, yo = (ow >> 12) & 0xFFF, flags = (ow >> 24) & 0x1F;   // face: bits 29..31
   const bool edge = (flags & 0x1E) != 0;                 // a side region is present (block-uniform)
+  const int ngw = edge ? (a.G + 63) >> 6 : 0;            // ghost waves
+  int gtarget = 0;                                       // s_gdone once this stage's entries are written
+  if (tid == 0) s_gdone = 0;
   const T* wf = &s_w[0];
   FSTAMP(0);
   FSTAMP_RT(14);
@@ -273,20 +285,22 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   const bool epoch_on = XG || MULTI;
   if (epoch_on) xe = a.epoch[bid];
   const int n = a.n;
-  // own cell: panel and panel-local index (cube topology)
-  int cg_ = 0, cI = 0, cJ = 0;
-  const bool cvalid = owner && window_cell((int)((unsigned)ow >> 29), X0 + u, Y0 + v, N, a.links, cg_, cI, cJ);
-  int src = -1;
-  if (cvalid) {
-    if (a.local_src) {  // computed: no dependent table load in front of the window load
+  // a window cell's panel and panel-local index (cube topology) and its
+  // storage offset: computed when one rank holds every tile in id order (no
+  // dependent table load in front of the window load), else the host table
+  const int face0 = (int)((unsigned)ow >> 29);
+  auto cell_src = [&](int cu, int cv, int& g_, int& I_, int& J_) -> int {
+    if (!window_cell(face0, X0 + cu, Y0 + cv, N, a.links, g_, I_, J_)) return -1;
+    if (a.local_src) {
       const int t = N / n;
-      const int ti = a.mdiv_n ? (int)__umulhi((unsigned)cI, a.mdiv_n) : cI / n;
-      const int tj = a.mdiv_n ? (int)__umulhi((unsigned)cJ, a.mdiv_n) : cJ / n;
-      src = (((cg_ * t + tj) * t + ti) * a.pw + (cJ - tj * n) + a.mg) * a.pw + (cI - ti * n) + a.mg;
-    } else {
-      src = a.src[(long)bid * W * W + v * W + u];
+      const int ti = a.mdiv_n ? (int)__umulhi((unsigned)I_, a.mdiv_n) : I_ / n;
+      const int tj = a.mdiv_n ? (int)__umulhi((unsigned)J_, a.mdiv_n) : J_ / n;
+      return (((g_ * t + tj) * t + ti) * a.pw + (J_ - tj * n) + a.mg) * a.pw + (I_ - ti * n) + a.mg;
     }
-  }
+    return a.src[(long)bid * W * W + cv * W + cu];
+  };
+  int cg_ = 0, cI = 0, cJ = 0;
+  const int src = owner ? cell_src(u, v, cg_, cI, cJ) : -1;
   // edge / corner tables into registers
   unsigned long long cdv = 0;
   int gs0 = 0, gs1 = 0;
@@ -334,10 +348,13 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   // (axis, line) < 2 (W + 1)), else the block's table (thread per value)
   T nrv = T(0);
   const bool nr_ld = flags == 1 ? tid < 2 * (W + 1) : tid < NN;
+  T nrv2 = T(0);                                         // a second table value (NN > NT)
   if (nr_ld) {
     if (flags == 1) nrv = a.tane[(tid < W + 1 ? X0 + tid : Y0 + tid - (W + 1))];
     else nrv = a.nrm[(long)bid * NN + tid];
   }
+  static_assert(NN <= 2 * NT, "line-normal table: two values per thread at most");
+  if (NN > NT && flags != 1 && tid + NT < NN) nrv2 = a.nrm[(long)bid * NN + tid + NT];
   // own window cell: state (+ geometry for the cells stage 1 updates)
   T Q[4];
   T iA = T(0), r0 = T(0), r1 = T(0), r2 = T(0), gb0 = T(0), gb1 = T(0), gb2 = T(0), S0 = T(0), S1 = T(0),
@@ -347,7 +364,8 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
   // state of the own window cell at the start of a step: another rank's cell
   // from the xGMI ring, else the state buffer (sc1 loads: with several steps
   // per launch the producer may sit on another XCD)
-  auto load_state = [&](const T* Qin, int xe_) {
+  auto load_state_of = [&](int src, T (&Q)[4], const T* Qin, int xe_) {
+    const bool loaded = src >= 0 || (XG && src <= -2);
     if (XG && src <= -2) {
       // another rank's cell: spin on its granules in ring slot xe % SLOTS until
       // every tag carries this step (xe + 1); a timeout sets err and falls through
@@ -389,6 +407,7 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
       for (int f = 0; f < 4; ++f) Q[f] = T(0);
     }
   };
+  auto load_state = [&](const T* Qin, int xe_) { load_state_of(src, Q, Qin, xe_); };
   T* const buf[2] = {const_cast<T*>(a.Q), a.out};
   load_state(buf[0], xe);
   if (loaded && in1) {
@@ -437,6 +456,7 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
       (&s_nrm[0][0][0][0])[tid] = nrv;
     }
   }
+  if (NN > NT && flags != 1 && tid + NT < NN) (&s_nrm[0][0][0][0])[tid + NT] = nrv2;
   if (edge) {
     if (owner) s_code[v * W + u] = cdv;
     if (tid < a.G) { s_gs[tid][0] = (short)gs0; s_gs[tid][1] = (short)gs1; s_gt[tid] = gtv; }
@@ -445,7 +465,7 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
       for (int k = 0; k < 4; ++k) { s_ct[tid][k] = ct4[k]; s_cg[tid][k] = cg4[k]; }
     }
   }
-  auto put = [&](const T (&q)[4]) {
+  auto put_at = [&](int wi, const T (&q)[4]) {
     const T inv = q[0] != T(0) ? trcp(q[0]) : T(0);
     T* p = &s_w[0] + wi;
     p[0] = q[0];
@@ -453,6 +473,21 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
     p[2 * WW] = q[2] * inv;
     p[3 * WW] = q[3] * inv;
     p[4 * WW] = tsqrt(a.g * tmax(q[0], T(0)));
+  };
+  auto put = [&](const T (&q)[4]) { put_at(wi, q); };
+  // tail cells (outer ring beyond NT, see FD): load and put, every step
+  auto tail = [&](const T* Qin, int xe_, bool first) {
+    if constexpr (NT < W * W) {
+      for (int idx = NT + tid - NU; tid >= NU && idx < W * W; idx += NT - NU) {
+        int tu, tv, g_, I_, J_;
+        owner_cell<NS, B>(idx, tu, tv);
+        const int ts = cell_src(tu, tv, g_, I_, J_);
+        if (first && edge) s_code[tv * W + tu] = a.code[(long)bid * W * W + tv * W + tu];
+        T q[4];
+        load_state_of(ts, q, Qin, xe_);
+        put_at(tv * WS + tu, q);
+      }
+    }
   };
   // panel-edge lines in the window (block-uniform): x-lines X = 0 (W) / X = N
   // (E), y-lines Y = 0 (S) / Y = N (N); far away when absent
@@ -480,6 +515,9 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
     }
     __syncthreads();
     if (tid >= B * B) load_state(buf[it & 1], xe);   // the own cells' new state is still in Q
+    tail(buf[it & 1], xe, false);
+  } else {
+    tail(buf[0], xe, true);
   }
   if (tid < NX2) {
 #pragma unroll
@@ -496,7 +534,11 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
     const int nr = hi - lo, nl = nr + 1, nx = nr * nl;
     // ---- ghost entries of this stage's input (edge blocks) ----------------------
     // the Putman-Lin interpolation of the neighbour panel's edge cells onto each
-    // reader's grid line, one entry per thread; faces then read it like a cell
+    // reader's grid line, one entry per thread; faces then read it like a cell.
+    // No block barrier: the ghost waves (the first ceil(G / 64), the oldest)
+    // count themselves done in s_gdone, and only a wave with a face next to a
+    // panel-edge line (or a cube-corner face) waits for the count before its
+    // first ghost read; every other wave starts its faces at once.
     if (edge) {
       if (tid < a.G) {
         const int i0 = s_gs[tid][0], i1 = s_gs[tid][1];
@@ -507,8 +549,16 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
           s_w[f * WW + GB + tid] = x0 + t * (x1 - x0);
         }
       }
-      __syncthreads();
+      if (tid < ngw * 64 && (tid & 63) == 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's entries are in LDS
+        __hip_atomic_fetch_add(&s_gdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      gtarget += ngw;
     }
+    auto gwait = [&]() {
+      while (__hip_atomic_load(&s_gdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gtarget)
+        __builtin_amdgcn_s_sleep(0);
+    };
     // ---- faces ---------------------------------------------------------------
     // EDGE (blocks with a side region): the face's normal is that of the lower
     // cell's region; only faces within one line of a panel edge line (a few
@@ -525,6 +575,7 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
         const int e0 = ax ? ky0 : kx0, e1 = ax ? ky1 : kx1;
         const bool near = (unsigned)(k - e0 + 1) <= 2u || (unsigned)(k - e1 + 1) <= 2u;
         wnear = __builtin_amdgcn_ballot_w64(near) != 0;
+        if (wnear) gwait();                                  // this wave reads ghost entries
         if (near) {
           const int sm = ax ? 2 : 0;                         // side index of -axis; +axis = sm + 1
           const int ci = fv * W + fu, cj = ci - (ax ? W : 1);  // window indices of b and a
@@ -562,13 +613,18 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) s_fl[f][fslot] = fl[f];
     };
-    // corner faces start on a wave boundary (a wave runs every branch its lanes take)
-    const int p3 = (2 * nx + 63) & ~63;
-    const int ntask = ncor ? p3 + ncor : 2 * nx;
+    // cube-corner faces (corner blocks only) are wave 0's tasks, alone: the
+    // oldest wave wins the issue arbitration, so their long dependency chain
+    // (two reconstructions from the codes, one flux) runs beside the regular
+    // faces instead of after them (round 3 had them on the wave after the last
+    // regular face: 4k cycles, the slowest wave of the stage-3 face phase)
+    const int c0 = ncor ? 64 : 0;
+    const int ntask = c0 + 2 * nx;
     for (int task = tid; task < ntask; task += NT) {
-      if (task < 2 * nx) {
-        const bool ax = task >= nx;                          // false: x-face, true: y-face
-        const int t2 = ax ? task - nx : task;
+      if (task >= c0) {
+        const int tf = task - c0;
+        const bool ax = tf >= nx;                            // false: x-face, true: y-face
+        const int t2 = ax ? tf - nx : tf;
         int fu, fv, k;
         if (!ax) {                                           // line-major, like the y-faces: the faces
           const int c = t2 / nr, r = t2 - c * nr;            // near an edge line fill few waves
@@ -579,9 +635,10 @@ __global__ __launch_bounds__(1024) void fused_step_kernel(FArgs<T> a) {
         }
         if (edge) face(ax, fu, fv, k, std::true_type{});
         else face(ax, fu, fv, k, std::false_type{});
-      } else if (task >= p3) {
+      } else if (task < ncor) {
         // cube-corner face j: cell c's face on side_c meets cell d's face on side_d
-        const int j = task - p3;
+        const int j = task;
+        gwait();
         const int ec = s_ct[j][0], ed = s_ct[j][1];
         T fv2[2][4], cc[2][5];
 #pragma unroll
@@ -764,24 +821,36 @@ int launch_fused(const FusedDesc* d, hipStream_t s) {
                 d->K <= 0))
     return -6;
   const dim3 grid(d->nblocks), block(D::NT);
+  if (d->limiter < 0 || d->limiter > 3) return -4;
   if (a.nsteps > 1) {
-    // every block must be resident at once (a waiting block holds its CU)
-    // (the residency query is cached per device and variant: it costs host
-    // microseconds on every launch of the bench's timed region otherwise)
-    static int cdev[2] = {-1, -1}, ccap[2] = {0, 0};
+    // every block must be resident at once (a waiting block holds its CU).
+    // The query runs on the very instance that is launched (limiter, xg) and
+    // is cached per (device, instance): it costs host microseconds on every
+    // launch of the bench's timed region otherwise.  Another process sharing
+    // the GPU (STSP_SHARE_GPU rehearsals) is not seen by it: the in-kernel
+    // waits are bounded and set err instead of hanging.
+    static int cdev[2][4] = {{-1, -1, -1, -1}, {-1, -1, -1, -1}}, ccap[2][4] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -8;
-    const int xi = d->xg ? 1 : 0;
-    if (cdev[xi] != dev) {
+    const int xi = d->xg ? 1 : 0, li = d->limiter;
+    if (cdev[xi][li] != dev) {
       int cus = 0, per = 0;
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -8;
-      const void* kf = d->xg ? (const void*)fused_step_kernel<T, 0, NS, B, true, true>
-                             : (const void*)fused_step_kernel<T, 0, NS, B, false, true>;
+      const void* kf = nullptr;
+#define FUSED_KF(L_) kf = d->xg ? (const void*)fused_step_kernel<T, L_, NS, B, true, true> \
+                                : (const void*)fused_step_kernel<T, L_, NS, B, false, true>
+      switch (li) {
+        case 0: FUSED_KF(0); break;
+        case 1: FUSED_KF(1); break;
+        case 2: FUSED_KF(2); break;
+        default: FUSED_KF(3); break;
+      }
+#undef FUSED_KF
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kf, D::NT, 0) != hipSuccess) return -8;
-      ccap[xi] = per * cus;
-      cdev[xi] = dev;
+      ccap[xi][li] = per * cus;
+      cdev[xi][li] = dev;
     }
-    if (ccap[xi] < d->nblocks) return -9;
+    if (ccap[xi][li] < d->nblocks) return -9;
   }
 #define FUSED_LAUNCH(L_)                                                                                  \
   if (a.nsteps > 1) {                                                                                     \

@@ -1089,6 +1089,9 @@ class FusedKernel:
         d = self._multi.get(nsteps)
         if d is None:
             d = self._multi[nsteps] = self._desc(0, 1, nsteps)
+        # follow the engine's current buffer order (step() swaps the pool)
+        from . import native
+        d.Q, d.out = native.ptr(self.e.pool[0]), native.ptr(self.e.pool[1])
         return d
 
     # ---- several ranks: delivery of the current state, error check ----------

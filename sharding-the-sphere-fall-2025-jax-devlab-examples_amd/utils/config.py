@@ -88,6 +88,10 @@ class RuntimeConfig:
     watchdog_interval: int = 0         # steps; 0 = off
     canary: bool = False               # NaN-prefill ghost slots and check after exchanges (debug)
     block: Optional[List[int]] = None
+    # fused SSP-RK3 step (ops/fused.py, one launch for several steps): auto = where
+    # the shallow-water setup supports it and every block of a rank is resident
+    fused: str = "auto"                # auto | on | off
+    steps_per_launch: int = 0          # fused multi-step launches; 0 = from the run's chunk length
 
 
 @dataclass

@@ -202,6 +202,45 @@ def test_fused_multi_step_launch_equals_single_steps(N, t, spl, nsteps):
     r.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_fused_back_to_back_multi_step_launches(dtype):
+    """Three back-to-back 8-step launches (the per-block step counters keep
+    counting across launches, the ping-pong buffers are reused) equal 24
+    single-step launches bit for bit, in fp64 and fp32, and no wait timed out."""
+    from stsphere.ops.fused import FusedKernel
+    _, a = _gpu_pair(96, 2, dtype=dtype)
+    _, b = _gpu_pair(96, 2, dtype=dtype)
+    b.dt = a.dt
+    FusedKernel(a).step(24)
+    fk = FusedKernel(b)
+    for _ in range(3):
+        fk.launch(0, nsteps=8)
+    torch.cuda.synchronize()
+    fk.check()
+    assert int(fk.tens["epoch"].min()) == int(fk.tens["epoch"].max()) == 24
+    assert torch.equal(a.pool[0], b.pool[0])
+
+
+@pytest.mark.gpu
+def test_fused_multi_step_after_odd_single_steps():
+    """A multi-step launch after an odd number of eager step() calls (which
+    swap the engine's buffers) starts from the current state: its descriptor
+    follows the engine's buffer order."""
+    from stsphere.ops.fused import FusedKernel
+    _, a = _gpu_pair(32, 2)
+    _, b = _gpu_pair(32, 2)
+    b.dt = a.dt
+    FusedKernel(a).step(7)
+    fk = FusedKernel(b)
+    fk.launch(0, nsteps=2)          # builds (and caches) the 2-step descriptor
+    fk.step(1)                      # odd: pool order swapped
+    fk.launch(0, nsteps=4)
+    torch.cuda.synchronize()
+    fk.check()
+    assert torch.equal(a.pool[0], b.pool[0])
+
+
 @pytest.mark.parametrize("N,t,R", [(32, 2, 2), (32, 2, 8), (48, 1, 6), (32, 2, 3)])
 def test_fused_exchange_ranks_equal_one_rank(N, t, R):
     """Several ranks (FusedExchangePlan): each rank's window reads its remote

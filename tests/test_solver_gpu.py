@@ -136,3 +136,37 @@ def test_solver_run_replays_graphs_for_io_intervals(tmp_path):
     t = zarr_lite.read_array(str(tmp_path / "history.zarr"), "time")
     assert h.shape[0] == 4 and np.isfinite(h).all() and np.allclose(t, np.arange(4) * 12 * s.dt)
     assert [r["step"] for r in read_metrics(str(tmp_path / "metrics.jsonl"))][-1] == 40
+
+
+def test_solver_run_uses_fused_multi_step_launches(tmp_path):
+    """Solver.run at C96 TC5 (tiles of 48, B = 16) steps with the fused
+    SSP-RK3 kernel: chunks between history / checkpoint / metrics / watchdog
+    intervals are whole multi-step launches (direct, no graph), the history and
+    checkpoints are written, and the state equals the launch-per-stage path
+    (runtime.fused = off) to 1e-11."""
+    from stsphere.utils import checkpoint as ckpt
+    from stsphere.utils.history import read_history
+    c = _cfg(1, 2, N=96, out=str(tmp_path / "f"), dt=None)
+    c["time"].pop("dt")
+    c["io"].update(history_interval=20, metrics_interval=10, checkpoint_interval=40)
+    c["runtime"].update(watchdog_interval=10)
+    s = Solver(c, verbose=False)
+    s.initialize()
+    out = s.run(nsteps=80)
+    assert out["runtime"] == "fused", out
+    st = s.runner.stats
+    assert st["direct_steps"] == 80 and st["graph_steps"] == 0 and st["eager_steps"] == 0, st
+    assert st["launches"] == 8, st             # chunks of 10 steps: one 10-step launch each
+    s.runner.check()
+    c2 = _cfg(1, 2, N=96, out=str(tmp_path / "s"), dt=s.dt)
+    c2["runtime"].update(fused="off")
+    r = Solver(c2, verbose=False)
+    r.initialize()
+    o2 = r.run(nsteps=80)
+    assert o2["runtime"] == "native"
+    a, b = s.gather_global(), r.gather_global()
+    err = max(np.abs(a[f] - b[f]).max() / np.abs(b[f]).max() for f in range(4))
+    assert err < 1e-11, err
+    h = read_history(str(tmp_path / "f" / "history.zarr"), "h")
+    assert h.shape[0] == 5 and np.isfinite(h).all()
+    assert ckpt.list_checkpoints(s.checkpoint_root())[-1] == 80

@@ -104,15 +104,17 @@ def main():
         for _ in range(3):
             fk.launch(0)
         torch.cuda.synchronize()
-        v = st.cpu().numpy().astype(np.int64)
+        v = st.cpu().numpy().astype(np.float64)
         for d in fk.descs:
             d.stamps = 0
-        # stamps [block][wave][phase]: phase time of a block = its last wave's stamp
+        # stamps [block][wave][phase]: phase time of a block = its last wave's stamp;
+        # waves that do not exist (768-thread blocks: 12 waves) or phases a wave
+        # never stamped stay 0 -> NaN
         nw = 16
-        v = v.reshape(nb, nw, 16)
-        t0 = v[:, :, 0].min(1)
+        v = np.where(v == 0, np.nan, v).reshape(nb, nw, 16)
+        t0 = np.nanmin(v[:, :, 0], 1)
         rel = v - t0[:, None, None]
-        blk = rel.max(1)                    # [nb, phase]: slowest wave of each block
+        blk = np.nanmax(rel, 1)             # [nb, phase]: slowest wave of each block
         W = fk.plan.d.W
         reg = fk.plan.reg.reshape(nb, W, W)
         edge = (reg > 0).any(axis=(1, 2))
@@ -134,12 +136,12 @@ def main():
         out["phases_cycles"] = ph
         P = fk.plan
         # shader clock from the (memtime, memrealtime) pairs at block start / end
-        dt_rt = (v[:, :, 15] - v[:, :, 14]).astype(np.float64) / 100e6     # seconds (100 MHz)
-        dt_sc = (v[:, :, 9] - v[:, :, 0]).astype(np.float64)
-        ok = dt_rt > 0
+        dt_rt = (v[:, :, 15] - v[:, :, 14]) / 100e6     # seconds (100 MHz)
+        dt_sc = (v[:, :, 9] - v[:, :, 0])
+        ok = np.isfinite(dt_rt) & np.isfinite(dt_sc) & (dt_rt > 0)
         out["shader_clock_ghz"] = float(np.median(dt_sc[ok] / dt_rt[ok]) / 1e9) if ok.any() else None
-        rt0 = v[:, :, 14][v[:, :, 14] > 0].min()
-        out["kernel_span_us_rt"] = float((v[:, :, 15].max() - rt0) / 100.0)
+        rt0 = np.nanmin(v[:, :, 14])
+        out["kernel_span_us_rt"] = float((np.nanmax(v[:, :, 15]) - rt0) / 100.0)
         out["ghost_entries_max"] = int(P.gcnt.max())
         # the same inside a 20-step launch: phases of the last step, from its loop top
         st.zero_()
@@ -149,9 +151,10 @@ def main():
         torch.cuda.synchronize()
         md.stamps = 0
         fk.check()
-        v2 = st.cpu().numpy().astype(np.int64).reshape(nb, nw, 16)
-        top = v2[:, :, 13].min(1)
-        rel2 = (v2 - top[:, None, None]).max(1)
+        v2 = st.cpu().numpy().astype(np.float64).reshape(nb, nw, 16)
+        v2 = np.where(v2 == 0, np.nan, v2)
+        top = np.nanmin(v2[:, :, 13], 1)
+        rel2 = np.nanmax(v2 - top[:, None, None], 1)
         idx = [13, 1, 2, 3, 4, 5, 6, 7, 8, 9]
         nm2 = ["loop_top", "wait_load_put", "bar"] + sum([[f"s{s}_faces", f"s{s}_upd"] for s in range(1, 4)], []) + ["end"]
         # per-wave face-phase time (from the stage's start barrier to the wave's last
@@ -159,15 +162,16 @@ def main():
         starts = {1: 2, 2: 4, 3: 6}
         pw = {}
         for s_ in (1, 2, 3):
-            dtw = v2[:, :, 9 + s_] - v2[:, :, starts[s_]].max(1)[:, None]
-            pw[f"s{s_}"] = {"int": [int(x) for x in dtw[~edge].mean(0)], "corner": [int(x) for x in dtw[corner].mean(0)]}
+            dtw = v2[:, :, 9 + s_] - np.nanmax(v2[:, :, starts[s_]], 1)[:, None]
+            pw[f"s{s_}"] = {"int": [None if np.isnan(x) else int(x) for x in np.nanmean(dtw[~edge], 0)],
+                            "corner": [None if np.isnan(x) else int(x) for x in np.nanmean(dtw[corner], 0)]}
         out["multi_wave_face_cycles"] = pw
         out["multi_last_step_cycles"] = {n_: {"int": mean2(rel2, ~edge, k), "edge": mean2(rel2, side, k),
                                               "corner": mean2(rel2, corner, k), "max": float(rel2[:, k].max())}
                                          for n_, k in zip(nm2, idx)}
         out["corner_faces_max"] = int(P.ccnt.max())
-        out["start_spread"] = float(t0.max() - t0.min())
-        out["end_max"] = float((v[:, :, 9].max(1) - t0.min()).max())
+        out["start_spread"] = float(np.nanmax(t0) - np.nanmin(t0))
+        out["end_max"] = float(np.nanmax(np.nanmax(v[:, :, 9], 1) - np.nanmin(t0)))
         out["edge_blocks"] = int(edge.sum())
     print(json.dumps(out), flush=True)
 
