@@ -307,12 +307,14 @@ class LowRankDiffusion:
 
     def __init__(self, N: int, L: float = 1.0, kappa: float = 1.0, bc: str = "dirichlet",
                  eps: float = 1e-10, max_rank: Optional[int] = None, dtype=torch.float64, device="cpu",
-                 backend: str = "torch", substeps: int = 1, qr: str = "cholqr3"):
+                 backend: str = "torch", substeps: int = 1, qr: str = "cholqr3n"):
         self.h = L / (N + 1) if bc == "dirichlet" else L / N
-        # hip recompression: "cholqr3" (device CholeskyQR3, machine-precision
-        # factors, one host transfer of the k x k core; composed in Python),
-        # "cholqr3n" (the same in one native call, stsp_tt_lr_step3) or "gram"
-        # (the native Gram/eigen step, ~sqrt(eps) accuracy; kept for comparison)
+        # hip recompression: "cholqr3n" (default: device CholeskyQR3,
+        # machine-precision factors, the whole step in one native call,
+        # stsp_tt_lr_step3, 181 -> 115 us with 2 substeps against ~540 us
+        # composed in Python, profiles/r3_tt), "cholqr3" (the same composed in
+        # Python, recompress_many) or "gram" (the native Gram/eigen step,
+        # ~sqrt(eps) accuracy; kept for comparison)
         if qr not in ("cholqr3", "cholqr3n", "gram"):
             raise ValueError(f"unknown qr {qr!r}")
         self.qr = qr
@@ -373,10 +375,14 @@ class LowRankDiffusion:
         B = U.B if U.B.stride(1) == 1 else U.B.contiguous()
         dev, dt_ = A.device, A.dtype
         k = r << ns
-        key = ("cqr", N, r, ns, dt_, dev)
+        # workspace for the widest step this solver can take (64 columns):
+        # allocated once, never per rank change (pinning host memory costs
+        # milliseconds, the step ~100 us)
+        key = ("cqr", N, ns, dt_, dev)
         if getattr(self, "_wkey3", None) != key:
-            self._ws3 = torch.empty(L.stsp_tt_step_workspace3(N, r, ns), dtype=dt_, device=dev)
-            self._hbuf3 = torch.empty(8 * k * k + 8, dtype=torch.float64).pin_memory()
+            rc = 64 >> ns
+            self._ws3 = torch.empty(L.stsp_tt_step_workspace3(N, rc, ns), dtype=dt_, device=dev)
+            self._hbuf3 = torch.empty(8 * 64 * 64 + 8, dtype=torch.float64).pin_memory()
             self._wkey3 = key
         rmax = k if self.max_rank is None else min(k, self.max_rank)
         out = torch.empty((2, N, rmax), dtype=dt_, device=dev)
@@ -422,10 +428,10 @@ class LowRankDiffusion:
         B = U.B if U.B.stride(1) == 1 else U.B.contiguous()
         dev, dt_ = A.device, A.dtype
         k = r << ns
-        key = (N, r, ns, dt_, dev)
+        key = (N, ns, dt_, dev)                  # sized for 64 columns, once (see _step_hip_cqr_native)
         if getattr(self, "_wkey", None) != key:
-            self._ws = torch.empty(L.stsp_tt_step_workspace2(N, r, ns), dtype=dt_, device=dev)
-            self._hbuf = torch.empty(4 * k * k, dtype=torch.float64).pin_memory()
+            self._ws = torch.empty(L.stsp_tt_step_workspace2(N, 64 >> ns, ns), dtype=dt_, device=dev)
+            self._hbuf = torch.empty(4 * 64 * 64, dtype=torch.float64).pin_memory()
             self._wkey = key
         rmax = k if self.max_rank is None else min(k, self.max_rank)
         out = torch.empty((2, N, rmax), dtype=dt_, device=dev)
@@ -792,6 +798,135 @@ class CubedSphereLowRankAdvection:
     @staticmethod
     def to_dense(F: Sequence[LowRankField]) -> torch.Tensor:
         return torch.stack([f.dense() for f in F])
+
+
+def _cdiff(X: torch.Tensor, h: float) -> torch.Tensor:
+    """Periodic central difference of a factor's rows, (X[i+1] - X[i-1]) / 2h."""
+    return (torch.roll(X, -1, 0) - torch.roll(X, 1, 0)) * (0.5 / h)
+
+
+class LowRankShallowWater:
+    """Linearised rotating shallow water on a doubly periodic N x N square,
+    carried entirely in factored form: the Cartesian 2-D SWEs the slides cite
+    for the 124x TT speed-up (PDF s.3, LANL, Danis et al. 2024),
+    the research target the reference's FV solver is the baseline for
+    (PDF s.5, s.19).
+
+        h_t = -H (u_x + v_y),   u_t = -g h_x + f v,   v_t = -g h_y - f u
+
+    on a C-free collocated grid (rows y, columns x, spacing L / N), second-order
+    central differences, SSP-RK3.  Every field is F = A B^T; x derivatives act
+    on the column factor (A (D B)^T), y derivatives on the row factor
+    ((D A) B^T), so the right-hand side of each field is a sum of two rank-r
+    products and a stage is one concatenation of factors:
+
+        L_h = [-H A_u, -H D A_v] [D B_u, B_v]^T
+        L_u = [-g A_h,   f A_v ] [D B_h, B_v]^T
+        L_v = [-g D A_h, -f A_u] [B_h,   B_u]^T
+
+    followed by a recompression to ``eps`` (backend "torch": thin QRs + a k x k
+    SVD; "hip": CholeskyQR3 of every factor on the gfx950 kernels, the three
+    fields' cores in one host transfer, ``recompress_many``).  The scheme
+    conserves the total of h exactly (periodic central differences) and the
+    energy g h^2 / 2 + H (u^2 + v^2) / 2 up to the SSP-RK3 dissipation.
+    ``dense_step`` is the N x N reference of the same discrete operator; the
+    semi-discrete dispersion relation omega^2 = f^2 + g H (k_x'^2 + k_y'^2),
+    k' = sin(k dx) / dx, is the analytic check (tests/test_tt_and_models.py)."""
+
+    def __init__(self, N: int, L: float = 1.0, g: float = 1.0, H: float = 1.0, f: float = 0.0,
+                 eps: float = 1e-12, max_rank: Optional[int] = None, dtype=torch.float64, device="cpu",
+                 backend: str = "torch"):
+        if backend not in ("torch", "hip"):
+            raise ValueError(f"unknown backend {backend!r}")
+        self.N, self.L, self.h = N, L, L / N
+        self.g, self.H, self.f = g, H, f
+        self.eps, self.max_rank, self.backend = eps, max_rank, backend
+        self.dtype, self.device = dtype, torch.device(device)
+        c = math.sqrt(g * H)
+        self.dt_max = self.h / (c * math.sqrt(2.0) + abs(f) * self.h + 1e-300)
+        self.stats = {"recompressions": 0, "max_k": 0}
+
+    # ---- factored operator ----------------------------------------------------
+    def rhs_factors(self, F):
+        """Factors (A, B) of L_h, L_u, L_v (each two rank-r blocks)."""
+        h_, u_, v_ = F
+        H, g, f, dx = self.H, self.g, self.f, self.h
+        Lh = (torch.cat([-H * u_.A, -H * _cdiff(v_.A, dx)], 1), torch.cat([_cdiff(u_.B, dx), v_.B], 1))
+        Lu = (torch.cat([-g * h_.A, f * v_.A], 1), torch.cat([_cdiff(h_.B, dx), v_.B], 1))
+        Lv = (torch.cat([-g * _cdiff(h_.A, dx), -f * u_.A], 1), torch.cat([h_.B, u_.B], 1))
+        return [Lh, Lu, Lv]
+
+    def _recompress(self, pairs) -> List[LowRankField]:
+        self.stats["recompressions"] += 1
+        self.stats["max_k"] = max(self.stats["max_k"], max(A.shape[1] for A, _ in pairs))
+        if self.backend == "hip":
+            return recompress_many([(A.contiguous(), B.contiguous()) for A, B in pairs], self.eps, self.max_rank,
+                                   "hip")
+        return [recompress(A, B, self.eps, self.max_rank) for A, B in pairs]
+
+    def _combo(self, terms) -> List[LowRankField]:
+        """sum_i a_i X_i (+ b L(Y)) per field, as one recompression of the
+        concatenated factors.  terms: list of (coef, fields) or (coef, 'L', Lfactors)."""
+        pairs = []
+        for q in range(3):
+            As, Bs = [], []
+            for t in terms:
+                if t[1] == "L":
+                    As.append(t[0] * t[2][q][0])
+                    Bs.append(t[2][q][1])
+                else:
+                    As.append(t[0] * t[1][q].A)
+                    Bs.append(t[1][q].B)
+            pairs.append((torch.cat(As, 1), torch.cat(Bs, 1)))
+        return self._recompress(pairs)
+
+    def step(self, F: Sequence[LowRankField], dt: float) -> List[LowRankField]:
+        """One SSP-RK3 step of (h, u, v); three recompressions (one per stage)."""
+        U1 = self._combo([(1.0, F), (dt, "L", self.rhs_factors(F))])
+        U2 = self._combo([(0.75, F), (0.25, U1), (0.25 * dt, "L", self.rhs_factors(U1))])
+        return self._combo([(1.0 / 3.0, F), (2.0 / 3.0, U2), (2.0 / 3.0 * dt, "L", self.rhs_factors(U2))])
+
+    # ---- dense reference ---------------------------------------------------------
+    def dense_rhs(self, W: torch.Tensor) -> torch.Tensor:
+        """W [3, N, N] = (h, u, v), rows y, columns x."""
+        h_, u_, v_ = W
+        dx = self.h
+        ddx = lambda X: (torch.roll(X, -1, 1) - torch.roll(X, 1, 1)) * (0.5 / dx)
+        ddy = lambda X: (torch.roll(X, -1, 0) - torch.roll(X, 1, 0)) * (0.5 / dx)
+        return torch.stack([-self.H * (ddx(u_) + ddy(v_)), -self.g * ddx(h_) + self.f * v_,
+                            -self.g * ddy(h_) - self.f * u_])
+
+    def dense_step(self, W: torch.Tensor, dt: float) -> torch.Tensor:
+        W1 = W + dt * self.dense_rhs(W)
+        W2 = 0.75 * W + 0.25 * (W1 + dt * self.dense_rhs(W1))
+        return W / 3.0 + (2.0 / 3.0) * (W2 + dt * self.dense_rhs(W2))
+
+    # ---- conversions / diagnostics ------------------------------------------------
+    def to_factored(self, W: torch.Tensor) -> List[LowRankField]:
+        return [LowRankField.from_dense(W[q].to(device=self.device, dtype=self.dtype), min(self.eps, 1e-14),
+                                        self.max_rank) for q in range(3)]
+
+    @staticmethod
+    def to_dense(F: Sequence[LowRankField]) -> torch.Tensor:
+        return torch.stack([f.dense() for f in F])
+
+    def energy(self, W: torch.Tensor) -> float:
+        h_, u_, v_ = W
+        return float((0.5 * self.g * h_ * h_ + 0.5 * self.H * (u_ * u_ + v_ * v_)).sum() * self.h * self.h)
+
+    def gravity_wave(self, kx: int, ky: int, amp: float = 0.1):
+        """Initial state of one standing inertia-gravity mode (h = amp cos(kx x)
+        cos(ky y), u = v = 0) and the semi-discrete frequency omega of the
+        scheme's central differences: h(t) = h(0) (f^2 + g H k'^2 cos(omega t))
+        / omega^2 for the rotating case."""
+        N, L = self.N, self.L
+        x = (torch.arange(N, dtype=torch.float64) + 0.5) * self.h
+        ax, ay = 2 * math.pi * kx / L, 2 * math.pi * ky / L
+        h0 = amp * torch.outer(torch.cos(ay * x), torch.cos(ax * x))
+        W = torch.stack([h0, torch.zeros_like(h0), torch.zeros_like(h0)])
+        kpx, kpy = math.sin(ax * self.h) / self.h, math.sin(ay * self.h) / self.h
+        omega = math.sqrt(self.f ** 2 + self.g * self.H * (kpx ** 2 + kpy ** 2))
+        return W.to(self.dtype), omega, (kpx, kpy)
 
 
 def compress_cubed_sphere(field: np.ndarray, eps: float = 1e-6, qtt: bool = False) -> List[dict]:

@@ -4,8 +4,9 @@
     python -m stsphere.ops.build --force
 
 Produces ``ops/libstsp.so`` next to the sources, so it travels with the repo
-snapshot to the GPU box.  Links RCCL (``librccl.so.1``; at run time the process
-shares the copy that PyTorch already loaded, same SONAME) and roctx.
+snapshot to the GPU box.  Links roctx; RCCL is resolved at run time from the
+``librccl.so.1`` the process already holds (PyTorch's copy) and its version is
+checked against the API subset ``csrc/rccl_abi.h`` declares.
 """
 from __future__ import annotations
 
@@ -18,7 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libstsp.so")
 SOURCES = ["stage_kernel.hip", "march_kernel.hip", "fused_step.hip", "tt_kernels.hip", "runtime.cpp"]
-HEADERS = ["stsp_kernels.h", "stage_common.h", "runtime.h"]
+HEADERS = ["stsp_kernels.h", "stage_common.h", "runtime.h", "rccl_abi.h"]
 ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
 # library variants: "" = production; "diag" = in-kernel phase stamps (-DSTSP_STAMPS);
 # "xgc" = the arrival-counter hand-off of the xGMI halo instead of tagged granules
@@ -100,8 +101,10 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
             os.replace(op + ".tmp", op)
     if failed:
         raise RuntimeError("hipcc failed")
+    # RCCL is not linked: the runtime resolves it from the librccl.so.1 the
+    # process already holds (PyTorch's) and checks its version (rccl_abi.h)
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib + ".tmp", "-L/opt/rocm/lib",
-           "-l:librccl.so.1", "-lrocprofiler-sdk-roctx"]
+           "-ldl", "-lrocprofiler-sdk-roctx"]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)

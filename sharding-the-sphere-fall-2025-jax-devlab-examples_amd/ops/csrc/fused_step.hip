@@ -494,38 +494,143 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   const int kx0 = (flags & 2) ? -X0 : -1000, kx1 = (flags & 4) ? N - X0 : -1000;
   const int ky0 = (flags & 8) ? -Y0 : -1000, ky1 = (flags & 16) ? N - Y0 : -1000;
 
+  auto gwait = [&]() {
+    while (__hip_atomic_load(&s_gdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gtarget)
+      __builtin_amdgcn_s_sleep(0);
+  };
+  // ---- faces ---------------------------------------------------------------
+  // EDGE (blocks with a side region): the face's normal is that of the lower
+  // cell's region; only faces within one line of a panel edge line (a few
+  // lanes) take their stencil neighbours from the codes (window cell or ghost
+  // entry) -- a short divergent branch instead of a second face body.
+  auto face = [&](bool ax, int fu, int fv, int k, auto edge_c) {
+    constexpr bool EDGE = decltype(edge_c)::value;
+    const int st = ax ? WS : 1;
+    const int fslot = ax ? NFX + (k - L1) * H1 + (fu - L1) : (fv - L1) * (H1 + 1) + (k - L1);
+    const int ib = fv * WS + fu, ia = ib - st;
+    int iam = ia - st, iap = ib, ibm = ia, ibp = ib + st, ra = 0;
+    bool wnear = false;                                    // some lane of this wave is near an edge line
+    if constexpr (EDGE) {
+      const int e0 = ax ? ky0 : kx0, e1 = ax ? ky1 : kx1;
+      const bool near = (unsigned)(k - e0 + 1) <= 2u || (unsigned)(k - e1 + 1) <= 2u;
+      wnear = __builtin_amdgcn_ballot_w64(near) != 0;
+      if (wnear) gwait();                                  // this wave reads ghost entries
+      if (near) {
+        const int sm = ax ? 2 : 0;                         // side index of -axis; +axis = sm + 1
+        const int ci = fv * W + fu, cj = ci - (ax ? W : 1);  // window indices of b and a
+        const unsigned long long ca = s_code[cj], cb = s_code[ci];
+        const int eam = ncode(ca, sm), eap = ncode(ca, sm + 1);
+        const int ebm = ncode(cb, sm), ebp = ncode(cb, sm + 1);
+        if (eam == -3 || ebm == -3) return;                // a cell is missing: a corner face
+        if (eam >= 0) iam = GB + eam;
+        if (eap >= 0) iap = GB + eap;
+        if (ebm >= 0) ibm = GB + ebm;
+        if (ebp >= 0) ibp = GB + ebp;
+      }
+      ra = fregion(X0 + fu - (ax ? 0 : 1), Y0 + fv - (ax ? 1 : 0), N);
+      ra = ra < 0 ? 0 : ra;                                // a missing: junk face, never read
+    }
+    T wl[4], wr[4], cl[5], cr[5];
+#pragma unroll
+    for (int f = 0; f < 5; ++f) { cl[f] = wf[f * WW + ia]; cr[f] = wf[f * WW + ib]; }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const T am = wf[f * WW + iam], bp = wf[f * WW + ibp];
+      T ap = cr[f], bm = cl[f];
+      if constexpr (EDGE) {
+        if (wnear) {                                       // wave-uniform: most waves skip these loads
+          ap = wf[f * WW + iap];
+          bm = wf[f * WW + ibm];
+        }
+      }
+      wl[f] = cl[f] + half_slope<LIM>(cl[f] - am, ap - cl[f]);
+      wr[f] = cr[f] - half_slope<LIM>(cr[f] - bm, bp - cr[f]);
+    }
+    const T* m = &s_nrm[ax ? 1 : 0][ra][0][k];
+    T fl[4];
+    swe_flux<T>(wl, wr, cl, cr, m[0], m[W + 1], m[2 * (W + 1)], s_len[fslot], a.g, fl);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) s_fl[f][fslot] = fl[f];
+  };
+  // Stage-1 faces whose whole stencil lies in the block's own cells ("inner":
+  // lines k in [R+2, R+B-2] x the block's B rows, both axes): a multi-step
+  // launch computes them while it waits for its producers (the own cells'
+  // next state is already in registers), the rest of the stage-1 face set
+  // ("outer") after the ring has arrived.  Inner faces are never next to a
+  // panel-edge line (those lie on block boundaries) and are region P.
+  constexpr int NIL = B - 3, NI = 2 * NIL * B;            // inner lines per axis, inner faces
+  constexpr int OL0 = R + 2 - L1, OL1 = (W - L1) - (R + B - 1) + 1;   // outer lines below / above
+  constexpr int NR1 = H1, NOR = H1 - B;                    // rows per line; rows outside the block
+  constexpr int NOA = (OL0 + OL1) * NR1, NOX = NOA + NIL * NOR;       // outer faces per axis
+  static_assert(NOX + NIL * B == H1 * (H1 + 1), "inner + outer = the stage-1 face set");
+  auto inner_face = [&](int t) {
+    const bool ax = t >= NIL * B;
+    const int t2 = ax ? t - NIL * B : t;
+    const int k = R + 2 + t2 / B, p = R + t2 % B;
+    if (ax) face(true, p, k, k, std::false_type{});
+    else face(false, k, p, k, std::false_type{});
+  };
+  // outer face t of one axis -> (line k, position along it)
+  auto outer_face = [&](int t, int& k, int& p) {
+    if (t < NOA) {
+      const int li = t / NR1, r = t - li * NR1;
+      k = li < OL0 ? L1 + li : R + B - 1 + (li - OL0);
+      p = L1 + r;
+    } else {
+      const int t2 = t - NOA, li = t2 / NOR, r = t2 - li * NOR;
+      k = R + 2 + li;
+      p = r < R - L1 ? L1 + r : R + B + (r - (R - L1));
+    }
+  };
+  auto enter_cell = [&]() {
+    if (tid < NX2) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) s_x[f][tid] = Q[f];
+    }
+    if (owner) put(Q);
+  };
+
   for (int it = 0; it < nsteps; ++it) {
   FSTAMP(13);
-  if (it > 0) {
-    // wait for the producers' previous step (wave 0 polls, the barrier releases
-    // the others), then load this step's window
-    if (tid < 64) {
-      const int p = tid < a.PM ? a.prod[(long)bid * a.PM + tid] : -1;
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      for (;;) {
-        const bool ok = p < 0 || __hip_atomic_load(a.epoch + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= xe;
-        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-        if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
-        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
-          if (tid == 0) __hip_atomic_store((gu32*)a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    __syncthreads();
-    if (tid >= B * B) load_state(buf[it & 1], xe);   // the own cells' new state is still in Q
-    tail(buf[it & 1], xe, false);
+  const bool wait = MULTI && it > 0;
+  // the own cells (first step: every cell) enter the window
+  if (wait) {
+    if (tid < B * B) enter_cell();
   } else {
     tail(buf[0], xe, true);
+    enter_cell();
   }
-  if (tid < NX2) {
-#pragma unroll
-    for (int f = 0; f < 4; ++f) s_x[f][tid] = Q[f];
+  __syncthreads();
+  if (wait && tid < 64) {
+    // wait for the producers' previous step (wave 0 polls) ...
+    const int p = tid < a.PM ? a.prod[(long)bid * a.PM + tid] : -1;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      const bool ok = p < 0 || __hip_atomic_load(a.epoch + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= xe;
+      if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+      if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
+        if (tid == 0) __hip_atomic_store((gu32*)a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  } else {
+    // ... while the other waves compute the inner stage-1 faces
+    const int t0 = wait ? tid - 64 : tid, dt_ = wait ? NT - 64 : NT;
+    for (int t = t0; t < NI; t += dt_) inner_face(t);
   }
-  if (owner) put(Q);
   FSTAMP(1);
   __syncthreads();
+  if (wait) {
+    // this step's ring (the own cells' new state is still in Q)
+    if (tid >= B * B) {
+      load_state(buf[it & 1], xe);
+      enter_cell();
+    }
+    tail(buf[it & 1], xe, false);
+    __syncthreads();
+  }
   FSTAMP(2);
 
 #pragma unroll
@@ -555,84 +660,28 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       }
       gtarget += ngw;
     }
-    auto gwait = [&]() {
-      while (__hip_atomic_load(&s_gdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gtarget)
-        __builtin_amdgcn_s_sleep(0);
-    };
-    // ---- faces ---------------------------------------------------------------
-    // EDGE (blocks with a side region): the face's normal is that of the lower
-    // cell's region; only faces within one line of a panel edge line (a few
-    // lanes) take their stencil neighbours from the codes (window cell or ghost
-    // entry) -- a short divergent branch instead of a second face body.
-    auto face = [&](bool ax, int fu, int fv, int k, auto edge_c) {
-      constexpr bool EDGE = decltype(edge_c)::value;
-      const int st = ax ? WS : 1;
-      const int fslot = ax ? NFX + (k - L1) * H1 + (fu - L1) : (fv - L1) * (H1 + 1) + (k - L1);
-      const int ib = fv * WS + fu, ia = ib - st;
-      int iam = ia - st, iap = ib, ibm = ia, ibp = ib + st, ra = 0;
-      bool wnear = false;                                    // some lane of this wave is near an edge line
-      if constexpr (EDGE) {
-        const int e0 = ax ? ky0 : kx0, e1 = ax ? ky1 : kx1;
-        const bool near = (unsigned)(k - e0 + 1) <= 2u || (unsigned)(k - e1 + 1) <= 2u;
-        wnear = __builtin_amdgcn_ballot_w64(near) != 0;
-        if (wnear) gwait();                                  // this wave reads ghost entries
-        if (near) {
-          const int sm = ax ? 2 : 0;                         // side index of -axis; +axis = sm + 1
-          const int ci = fv * W + fu, cj = ci - (ax ? W : 1);  // window indices of b and a
-          const unsigned long long ca = s_code[cj], cb = s_code[ci];
-          const int eam = ncode(ca, sm), eap = ncode(ca, sm + 1);
-          const int ebm = ncode(cb, sm), ebp = ncode(cb, sm + 1);
-          if (eam == -3 || ebm == -3) return;                // a cell is missing: a corner face
-          if (eam >= 0) iam = GB + eam;
-          if (eap >= 0) iap = GB + eap;
-          if (ebm >= 0) ibm = GB + ebm;
-          if (ebp >= 0) ibp = GB + ebp;
-        }
-        ra = fregion(X0 + fu - (ax ? 0 : 1), Y0 + fv - (ax ? 1 : 0), N);
-        ra = ra < 0 ? 0 : ra;                                // a missing: junk face, never read
-      }
-      T wl[4], wr[4], cl[5], cr[5];
-#pragma unroll
-      for (int f = 0; f < 5; ++f) { cl[f] = wf[f * WW + ia]; cr[f] = wf[f * WW + ib]; }
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        const T am = wf[f * WW + iam], bp = wf[f * WW + ibp];
-        T ap = cr[f], bm = cl[f];
-        if constexpr (EDGE) {
-          if (wnear) {                                       // wave-uniform: most waves skip these loads
-            ap = wf[f * WW + iap];
-            bm = wf[f * WW + ibm];
-          }
-        }
-        wl[f] = cl[f] + half_slope<LIM>(cl[f] - am, ap - cl[f]);
-        wr[f] = cr[f] - half_slope<LIM>(cr[f] - bm, bp - cr[f]);
-      }
-      const T* m = &s_nrm[ax ? 1 : 0][ra][0][k];
-      T fl[4];
-      swe_flux<T>(wl, wr, cl, cr, m[0], m[W + 1], m[2 * (W + 1)], s_len[fslot], a.g, fl);
-#pragma unroll
-      for (int f = 0; f < 4; ++f) s_fl[f][fslot] = fl[f];
-    };
     // cube-corner faces (corner blocks only) are wave 0's tasks, alone: the
     // oldest wave wins the issue arbitration, so their long dependency chain
     // (two reconstructions from the codes, one flux) runs beside the regular
     // faces instead of after them (round 3 had them on the wave after the last
     // regular face: 4k cycles, the slowest wave of the stage-3 face phase)
     const int c0 = ncor ? 64 : 0;
-    const int ntask = c0 + 2 * nx;
+    const int nax = s == 0 ? NOX : nx;                       // stage 1: the outer faces only
+    const int ntask = c0 + 2 * nax;
     for (int task = tid; task < ntask; task += NT) {
       if (task >= c0) {
         const int tf = task - c0;
-        const bool ax = tf >= nx;                            // false: x-face, true: y-face
-        const int t2 = ax ? tf - nx : tf;
-        int fu, fv, k;
-        if (!ax) {                                           // line-major, like the y-faces: the faces
-          const int c = t2 / nr, r = t2 - c * nr;            // near an edge line fill few waves
-          fv = lo + r; k = lo + c; fu = k;                   // b = (k, fv), a = (k - 1, fv)
-        } else {
-          const int r = t2 / nr, c = t2 - r * nr;
-          k = lo + r; fu = lo + c; fv = k;                   // b = (fu, k), a = (fu, k - 1)
+        const bool ax = tf >= nax;                           // false: x-face, true: y-face
+        const int t2 = ax ? tf - nax : tf;
+        int fu, fv, k, p;
+        if (s == 0) {
+          outer_face(t2, k, p);
+        } else {                                             // line-major: the faces near an
+          const int c = t2 / nr, r = t2 - c * nr;            // edge line fill few waves
+          k = lo + c; p = lo + r;
         }
+        if (!ax) { fv = p; fu = k; }                         // b = (k, fv), a = (k - 1, fv)
+        else { fu = p; fv = k; }                             // b = (fu, k), a = (fu, k - 1)
         if (edge) face(ax, fu, fv, k, std::true_type{});
         else face(ax, fu, fv, k, std::false_type{});
       } else if (task < ncor) {

@@ -21,7 +21,9 @@
 // so halo traffic is never queued behind interior work.
 #include "runtime.h"
 
-#include <rccl/rccl.h>
+#include "rccl_abi.h"
+
+#include <dlfcn.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <cstdio>
@@ -29,6 +31,65 @@
 #include <cstring>
 #include <string>
 #include <vector>
+
+// ---- RCCL, resolved at run time (rccl_abi.h) -------------------------------------
+
+namespace {
+RcclApi g_rccl{};
+std::string g_rccl_err;
+bool g_rccl_done = false;
+
+template <typename F>
+bool rccl_sym(void* h, const char* name, F& out) {
+  out = reinterpret_cast<F>(dlsym(h, name));
+  if (!out) g_rccl_err = std::string("librccl.so.1 has no ") + name;
+  return out != nullptr;
+}
+}  // namespace
+
+const RcclApi* rccl_api() {
+  if (g_rccl_done) return g_rccl.version ? &g_rccl : nullptr;
+  g_rccl_done = true;
+  // the copy already in the process (PyTorch's), else the one on the search path
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+  g_rccl.path = "librccl.so.1 (already loaded)";
+  if (!h) {
+    h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    g_rccl.path = "librccl.so.1 (dlopen)";
+  }
+  if (!h) {
+    g_rccl_err = std::string("cannot load librccl.so.1: ") + dlerror();
+    return nullptr;
+  }
+  RcclApi a{};
+  a.path = g_rccl.path;
+  if (!rccl_sym(h, "ncclGetVersion", a.GetVersion) || !rccl_sym(h, "ncclGetUniqueId", a.GetUniqueId) ||
+      !rccl_sym(h, "ncclCommInitRank", a.CommInitRank) || !rccl_sym(h, "ncclCommDestroy", a.CommDestroy) ||
+      !rccl_sym(h, "ncclCommUserRank", a.CommUserRank) || !rccl_sym(h, "ncclSend", a.Send) ||
+      !rccl_sym(h, "ncclRecv", a.Recv) || !rccl_sym(h, "ncclGroupStart", a.GroupStart) ||
+      !rccl_sym(h, "ncclGroupEnd", a.GroupEnd) || !rccl_sym(h, "ncclGetErrorString", a.GetErrorString))
+    return nullptr;
+  int v = 0;
+  if (a.GetVersion(&v) != ncclSuccess || v <= 0) {
+    g_rccl_err = "ncclGetVersion failed";
+    return nullptr;
+  }
+  if (v < STSP_RCCL_MIN_VERSION || v > STSP_RCCL_MAX_VERSION) {
+    g_rccl_err = "loaded RCCL version " + std::to_string(v) + " is outside the API range this runtime declares [" +
+                 std::to_string(STSP_RCCL_MIN_VERSION) + ", " + std::to_string(STSP_RCCL_MAX_VERSION) + "]";
+    return nullptr;
+  }
+  a.version = v;
+  g_rccl = a;
+  return &g_rccl;
+}
+
+extern "C" int stsp_rccl_version(void) {
+  const RcclApi* r = rccl_api();
+  return r ? r->version : -1;
+}
+
+extern "C" const char* stsp_rccl_error(void) { return g_rccl_err.c_str(); }
 
 namespace {
 
@@ -61,7 +122,7 @@ struct Runtime {
   do {                                                                                     \
     ncclResult_t r_ = (expr);                                                              \
     if (r_ != ncclSuccess) {                                                               \
-      rt->err = std::string(#expr) + ": " + ncclGetErrorString(r_);                        \
+      rt->err = std::string(#expr) + ": " + rccl_api()->GetErrorString(r_);                \
       return -2;                                                                           \
     }                                                                                      \
   } while (0)
@@ -96,16 +157,17 @@ int run_op(Runtime* rt, const StspOp& op) {
       RT_CHECK(hipStreamWaitEvent(rt->comm_stream, rt->ev_fork, 0));
       const size_t eb = elem_bytes(op.dtype);
       const ncclDataType_t ty = nccl_type(op.dtype);
-      NC_CHECK(ncclGroupStart());
+      const RcclApi* R = rccl_api();       // non-null: the communicator was made through it
+      NC_CHECK(R->GroupStart());
       for (int k = 0; k < op.npeers; ++k) {
         const char* p = static_cast<const char*>(op.sendbuf) + (size_t)op.send_off[k] * op.slot_elems * eb;
-        NC_CHECK(ncclSend(p, (size_t)op.send_cnt[k] * op.slot_elems, ty, op.send_peer[k], rt->comm, rt->comm_stream));
+        NC_CHECK(R->Send(p, (size_t)op.send_cnt[k] * op.slot_elems, ty, op.send_peer[k], rt->comm, rt->comm_stream));
       }
       for (int k = 0; k < op.nrecv; ++k) {
         char* p = static_cast<char*>(op.recvbuf) + (size_t)op.recv_off[k] * op.slot_elems * eb;
-        NC_CHECK(ncclRecv(p, (size_t)op.recv_cnt[k] * op.slot_elems, ty, op.recv_peer[k], rt->comm, rt->comm_stream));
+        NC_CHECK(R->Recv(p, (size_t)op.recv_cnt[k] * op.slot_elems, ty, op.recv_peer[k], rt->comm, rt->comm_stream));
       }
-      NC_CHECK(ncclGroupEnd());
+      NC_CHECK(R->GroupEnd());
       return 0;
     }
     case STSP_OP_FUSED: {
@@ -287,41 +349,52 @@ extern "C" int stsp_rt_run(void* p, int nsteps) {
 extern "C" int stsp_nccl_id_bytes(void) { return NCCL_UNIQUE_ID_BYTES; }
 
 extern "C" int stsp_nccl_unique_id(void* out) {
+  const RcclApi* R = rccl_api();
+  if (!R) return -2;
   ncclUniqueId id;
-  if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
+  if (R->GetUniqueId(&id) != ncclSuccess) return -1;
   std::memcpy(out, &id, sizeof(id));
   return 0;
 }
 
 extern "C" void* stsp_nccl_comm_init(int nranks, const void* idbytes, int rank, int device) {
+  const RcclApi* R = rccl_api();
+  if (!R) return nullptr;
   if (hipSetDevice(device) != hipSuccess) return nullptr;
   ncclUniqueId id;
   std::memcpy(&id, idbytes, sizeof(id));
   ncclComm_t comm = nullptr;
-  if (ncclCommInitRank(&comm, nranks, id, rank) != ncclSuccess) return nullptr;
+  const ncclResult_t r = R->CommInitRank(&comm, nranks, id, rank);
+  if (r != ncclSuccess) {
+    g_rccl_err = std::string("ncclCommInitRank: ") + R->GetErrorString(r);
+    return nullptr;
+  }
   return comm;
 }
 
 extern "C" int stsp_nccl_comm_destroy(void* comm) {
   if (!comm) return 0;
-  return ncclCommDestroy(static_cast<ncclComm_t>(comm)) == ncclSuccess ? 0 : -1;
+  const RcclApi* R = rccl_api();
+  return R && R->CommDestroy(static_cast<ncclComm_t>(comm)) == ncclSuccess ? 0 : -1;
 }
 
 extern "C" int stsp_nccl_selftest(void* comm, void* stream) {
   // 1-element send/recv to self through the same grouped path the halo uses.
   ncclComm_t c = static_cast<ncclComm_t>(comm);
+  const RcclApi* R = rccl_api();
+  if (!R) return -5;
   int rank = 0;
-  if (ncclCommUserRank(c, &rank) != ncclSuccess) return -1;
+  if (R->CommUserRank(c, &rank) != ncclSuccess) return -1;
   double* buf = nullptr;
   if (hipMalloc(&buf, 2 * sizeof(double)) != hipSuccess) return -2;
   const double v = 42.0 + rank;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipMemcpyAsync(buf, &v, sizeof(double), hipMemcpyHostToDevice, s);
   hipMemsetAsync(buf + 1, 0, sizeof(double), s);
-  ncclGroupStart();
-  ncclSend(buf, 1, ncclFloat64, rank, c, s);
-  ncclRecv(buf + 1, 1, ncclFloat64, rank, c, s);
-  const ncclResult_t r = ncclGroupEnd();
+  R->GroupStart();
+  R->Send(buf, 1, ncclFloat64, rank, c, s);
+  R->Recv(buf + 1, 1, ncclFloat64, rank, c, s);
+  const ncclResult_t r = R->GroupEnd();
   double out = 0;
   hipMemcpyAsync(&out, buf + 1, sizeof(double), hipMemcpyDeviceToHost, s);
   hipStreamSynchronize(s);

@@ -124,6 +124,10 @@ def _declare_runtime(L):
     L.stsp_nccl_unique_id.restype = ci
     L.stsp_nccl_id_bytes.argtypes = []
     L.stsp_nccl_id_bytes.restype = ci
+    L.stsp_rccl_version.argtypes = []
+    L.stsp_rccl_version.restype = ci
+    L.stsp_rccl_error.argtypes = []
+    L.stsp_rccl_error.restype = ctypes.c_char_p
     L.stsp_roctx_push.argtypes = [ctypes.c_char_p]
     L.stsp_roctx_push.restype = ci
     L.stsp_roctx_pop.argtypes = []

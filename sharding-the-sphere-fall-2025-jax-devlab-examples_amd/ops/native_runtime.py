@@ -86,6 +86,7 @@ def create_nccl_comm(rank: int, world: int, device_index: int, group=None) -> in
     over the existing torch.distributed process group."""
     import torch.distributed as dist
     L = lib()
+    rccl_version()                      # raises (on every rank alike) when RCCL is unusable
     nb = L.stsp_nccl_id_bytes()
     buf = (ctypes.c_char * nb)()
     if rank == 0:
@@ -98,8 +99,21 @@ def create_nccl_comm(rank: int, world: int, device_index: int, group=None) -> in
     idbuf = (ctypes.c_char * nb).from_buffer_copy(raw)
     comm = L.stsp_nccl_comm_init(world, idbuf, rank, device_index)
     if not comm:
-        raise RuntimeError("ncclCommInitRank failed")
+        raise RuntimeError(f"ncclCommInitRank failed: {L.stsp_rccl_error().decode()}")
     return comm
+
+
+def rccl_version() -> int:
+    """Version code (major * 10000 + minor * 100 + patch) of the librccl.so.1
+    this process runs (PyTorch's copy when torch is imported first).  Raises
+    when it cannot be loaded or lies outside the API range the runtime
+    declares (csrc/rccl_abi.h): a header/library mismatch fails loudly here,
+    at communicator creation, instead of inside a send."""
+    L = lib()
+    v = int(L.stsp_rccl_version())
+    if v < 0:
+        raise RuntimeError(f"RCCL unusable: {L.stsp_rccl_error().decode()}")
+    return v
 
 
 def nccl_selftest(comm: int) -> None:

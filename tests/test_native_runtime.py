@@ -124,3 +124,4 @@ def test_rccl_loopback_full_multigpu_path(nccl_comm, use_graph, phys):
     torch.cuda.synchronize()
     assert torch.equal(ref.tiles_view(), e.tiles_view())
     ns.close()
+

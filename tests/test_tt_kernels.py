@@ -265,18 +265,46 @@ def test_cube_low_rank_diffusion_hip_cholqr3_machine_precision():
 
 
 @pytest.mark.gpu
-def test_native_cholqr3_step_matches_python_composition():
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-12), (torch.float32, 1e-5)])
+def test_native_cholqr3_step_matches_python_composition(dtype, tol):
     """stsp_tt_lr_step3 (one native call) and the Python-composed CholeskyQR3
-    step give the same factored field (to rounding), fp64 and 2 substeps."""
+    step give the same factored field (to rounding), 1 and 2 substeps, fp64
+    and fp32 (the fp32 branch packs floats into the host buffer and uses the
+    fp32 shift).  Repeated steps at changing rank reuse one
+    workspace."""
     N = 384
     U = _panel(N)
     for ns in (1, 2):
-        s = tt.LowRankDiffusion(N, kappa=1.0, eps=1e-12, max_rank=16 if ns == 2 else None, backend="hip", substeps=ns,
-                                qr="cholqr3n")
-        lr = tt.LowRankField.from_dense(U.cuda(), eps=1e-14)
+        s = tt.LowRankDiffusion(N, kappa=1.0, eps=1e-12 if dtype == torch.float64 else 1e-6,
+                                max_rank=16 if ns == 2 else None, backend="hip", substeps=ns, qr="cholqr3n",
+                                dtype=dtype)
+        lr = tt.LowRankField.from_dense(U.cuda().to(dtype), eps=1e-14 if dtype == torch.float64 else 1e-7)
         dt = 0.5 * s.dt_max
         a = s.step(lr, dt)
         b = s._step_hip_cqr_py(lr, dt)
         torch.cuda.synchronize()
-        da, db = a.dense(), b.dense()
-        assert float((da - db).norm() / db.norm()) < 1e-12
+        da, db = a.dense().double(), b.dense().double()
+        assert float((da - db).norm() / db.norm()) < tol
+        ws = s._ws3.data_ptr()
+        for _ in range(3):
+            a = s.step(a, dt)
+        assert s._ws3.data_ptr() == ws
+
+
+@pytest.mark.gpu
+def test_lowrank_shallow_water_hip_matches_dense():
+    """The factored SWE on the gfx950 recompression (CholeskyQR3 kernels, one
+    host transfer of the three cores per stage) against the dense operator."""
+    import math
+    sw = tt.LowRankShallowWater(256, g=1.0, H=1.0, f=2.0, eps=1e-13, device="cuda", backend="hip")
+    W, _, _ = sw.gravity_wave(1, 2, amp=0.1)
+    W2, _, _ = sw.gravity_wave(5, 3, amp=0.05)
+    W = (W + W2).cuda()
+    F, D = sw.to_factored(W), W.clone()
+    dt = 0.5 * sw.dt_max
+    for _ in range(30):
+        F, D = sw.step(F, dt), sw.dense_step(D, dt)
+    torch.cuda.synchronize()
+    R = sw.to_dense(F)
+    assert float((R - D).norm() / D.norm()) < 1e-10
+    assert max(f.rank for f in F) <= 8
