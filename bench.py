@@ -245,9 +245,9 @@ def main():
                 # where launches and hand-offs dominate (every block resident, so
                 # several steps run per launch); larger grids keep the stage path
                 from stsphere.ops.fused import fused_block
-                B = fused_block(layout.n)
-                nb = len(layout.plan(rank).tiles) * (layout.n // B) ** 2
                 cus = torch.cuda.get_device_properties(device).multi_processor_count if device.type == "cuda" else 256
+                B = fused_block(layout.n, len(layout.plan(rank).tiles), cus)
+                nb = len(layout.plan(rank).tiles) * (layout.n // B) ** 2
                 # one GPU up to two passes over the CUs: one fused launch per step still
                 # beats three stage launches (C180, 3 tiles per edge, 486 blocks: 38.6 vs
                 # 44.5 us/step, profiles/r3_march/c180_fused_b20.log)

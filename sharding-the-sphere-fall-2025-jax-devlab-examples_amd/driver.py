@@ -312,7 +312,8 @@ class Solver:
         e = self.engines[0]
         if c.fused == "off" or e.device.type != "cuda":
             return False, 1
-        if not (self.mode == "single" or (self.mode == "spmd" and self.comm == "xgmi")):
+        # auto: one GPU; several ranks (the xGMI ring inside the fused kernel) on request
+        if not (self.mode == "single" or (self.mode == "spmd" and self.comm == "xgmi" and c.fused == "on")):
             if c.fused == "on":
                 raise ValueError(f"runtime.fused = on needs one GPU or the xgmi exchange (mode {self.mode}, "
                                  f"comm {self.comm})")
@@ -322,9 +323,9 @@ class Solver:
             if c.fused == "on":
                 raise ValueError(why)
             return False, 1
-        B = fused_block(e.plan.n)
-        nb = len(e.plan.tiles) * (e.plan.n // B) ** 2
         cus = torch.cuda.get_device_properties(e.device).multi_processor_count
+        B = fused_block(e.plan.n, len(e.plan.tiles), cus)
+        nb = len(e.plan.tiles) * (e.plan.n // B) ** 2
         if c.fused == "auto" and nb > (2 * cus if self.mode == "single" else cus):
             return False, 1
         if nb > cus:
@@ -345,8 +346,9 @@ class Solver:
         use_fused, spl = self._fused_plan(chunk)
         self.fused = None
         if use_fused:
-            from .ops.fused import FusedKernel
-            fk = FusedKernel(e)                  # collective with several ranks (xGMI ring setup)
+            from .ops.fused import FusedKernel, fused_block
+            cus = torch.cuda.get_device_properties(e.device).multi_processor_count
+            fk = FusedKernel(e, B=fused_block(e.plan.n, len(e.plan.tiles), cus))   # collective with several ranks
             self.fused = fk
             self.xgmi = fk if self.mode == "spmd" else None
             self._log(f"Runtime: fused SSP-RK3 step, {fk.plan.nb} blocks of {fk.plan.B}x{fk.plan.B}, "

@@ -46,6 +46,9 @@
 
 namespace {
 
+// cube-corner face table widths (ops/fused.py::corner_tables)
+constexpr int CT_INTS = 16, CT_FLAGS = 12, CG_VALS = 8;
+
 template <int NS, int B>
 struct FD {
   static constexpr int R = 2 * NS;
@@ -249,8 +252,13 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   __shared__ unsigned long long s_code[W * W];   // neighbour codes (edge blocks)
   __shared__ short s_gs[D::GMAX][2];       // ghost entry: interpolation pair (LDS window index)
   __shared__ T s_gt[D::GMAX];              //              and weight
-  __shared__ int s_ct[D::CMAX][4];
-  __shared__ T s_cg[D::CMAX][4];
+  // cube-corner faces, resolved on the host (ops/fused.py::corner_tables):
+  // per side q of the face: the cell's LDS index, its across / inward stencil
+  // neighbours as an LDS index pair and a weight (a ghost entry's
+  // interpolation, evaluated here instead of read from the ghost pass), face
+  // slots and flags; weights after the normal and length
+  __shared__ int s_ct[D::CMAX][CT_INTS];
+  __shared__ T s_cg[D::CMAX][CG_VALS];
   // step-start state of the cells stages 2.. update (owners [0, NX2)): the
   // a0 X term of SSP-RK3; in LDS rather than registers (register pressure)
   constexpr int NX2 = NS > 1 ? (B + 4 * (NS - 2)) * (B + 4 * (NS - 2)) : 1;
@@ -306,8 +314,8 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   int gs0 = 0, gs1 = 0;
   T gtv = T(0);
   int ncor = 0;
-  int ct4[4] = {0, 0, 0, 0};
-  T cg4[4] = {T(0), T(0), T(0), T(0)};
+  int ctv[CT_INTS];
+  T cgv[CG_VALS];
   if (edge) {
     if (owner) cdv = a.code[(long)bid * W * W + v * W + u];
     if (tid < a.G) {
@@ -317,10 +325,12 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     }
     ncor = a.ccnt[bid];
     if (tid < ncor) {
-      const int* ct = a.ctab + ((long)bid * a.C + tid) * 8;
-      const T* cg = a.cgf + ((long)bid * a.C + tid) * 4;
+      const int* ct = a.ctab + ((long)bid * a.C + tid) * CT_INTS;
+      const T* cg = a.cgf + ((long)bid * a.C + tid) * CG_VALS;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { ct4[k] = ct[k]; cg4[k] = cg[k]; }
+      for (int k = 0; k < CT_INTS; ++k) ctv[k] = ct[k];
+#pragma unroll
+      for (int k = 0; k < CG_VALS; ++k) cgv[k] = cg[k];
     }
   }
   // face lengths of the stage-1 face set: region of the face's lower cell (else
@@ -462,7 +472,9 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     if (tid < a.G) { s_gs[tid][0] = (short)gs0; s_gs[tid][1] = (short)gs1; s_gt[tid] = gtv; }
     if (tid < ncor) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { s_ct[tid][k] = ct4[k]; s_cg[tid][k] = cg4[k]; }
+      for (int k = 0; k < CT_INTS; ++k) s_ct[tid][k] = ctv[k];
+#pragma unroll
+      for (int k = 0; k < CG_VALS; ++k) s_cg[tid][k] = cgv[k];
     }
   }
   auto put_at = [&](int wi, const T (&q)[4]) {
@@ -685,36 +697,35 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         if (edge) face(ax, fu, fv, k, std::true_type{});
         else face(ax, fu, fv, k, std::false_type{});
       } else if (task < ncor) {
-        // cube-corner face j: cell c's face on side_c meets cell d's face on side_d
+        // cube-corner face j: cell c's face on side_c meets cell d's face on
+        // side_d; every stencil index comes from the host table (no codes, no
+        // wait for the ghost pass: an interpolated neighbour is evaluated here
+        // with the ghost pass's formula, x0 + t (x1 - x0), so bit for bit)
         const int j = task;
-        gwait();
-        const int ec = s_ct[j][0], ed = s_ct[j][1];
+        const int* ct = s_ct[j];
+        const int fl_ = ct[CT_FLAGS];
         T fv2[2][4], cc[2][5];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const int e = q ? ed : ec;
-          const int cu = e & 0xFF, cv = (e >> 8) & 0xFF, side = (e >> 16) & 3;
-          const int plus = side & 1;
-          const int st = (side >> 1) ? WS : 1;
-          const int ic = cv * WS + cu;
-          const unsigned long long cd = s_code[cv * W + cu];
-          const int eac = ncode(cd, side), ein = ncode(cd, side ^ 1);
-          const int iac = eac >= 0 ? GB + eac : ic;
-          const int iin = ein >= 0 ? GB + ein : (plus ? ic - st : ic + st);
+          const int ic = ct[5 * q], a0 = ct[5 * q + 1], a1 = ct[5 * q + 2], n0 = ct[5 * q + 3], n1 = ct[5 * q + 4];
+          const bool plus = (fl_ >> (4 + q)) & 1, ai = (fl_ >> (2 * q)) & 1, ni = (fl_ >> (2 * q + 1)) & 1;
+          const T ta = s_cg[j][4 + 2 * q], tn = s_cg[j][5 + 2 * q];
 #pragma unroll
           for (int f = 0; f < 5; ++f) cc[q][f] = wf[f * WW + ic];
 #pragma unroll
           for (int f = 0; f < 4; ++f) {
             const T c0 = cc[q][f];
-            const T across = wf[f * WW + iac], inward = wf[f * WW + iin];
+            const T xa = wf[f * WW + a0], xn = wf[f * WW + n0];
+            const T across = ai ? xa + ta * (wf[f * WW + a1] - xa) : xa;
+            const T inward = ni ? xn + tn * (wf[f * WW + n1] - xn) : xn;
             fv2[q][f] = plus ? c0 + half_slope<LIM>(c0 - inward, across - c0)
                              : c0 - half_slope<LIM>(c0 - across, inward - c0);
           }
         }
         T fl[4];
         swe_flux<T>(fv2[0], fv2[1], cc[0], cc[1], s_cg[j][0], s_cg[j][1], s_cg[j][2], s_cg[j][3], a.g, fl);
-        const int fc = s_ct[j][2], fd = s_ct[j][3];
-        const bool pc = ((ec >> 16) & 1) != 0, pd = ((ed >> 16) & 1) != 0;
+        const int fc = ct[10], fd = ct[11];
+        const bool pc = (fl_ >> 4) & 1, pd = (fl_ >> 5) & 1;
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
           if (fc >= 0) s_fl[f][fc] = pc ? fl[f] : -fl[f];
@@ -922,12 +933,20 @@ int launch_fused(const FusedDesc* d, hipStream_t s) {
 
 }  // namespace
 
-// Block sizes: 16 (C96: tiles of 48, C48, C32) and 18 (C180 at tiles_per_edge 2:
-// tiles of 90; C720: 360, 180); the window of W = B + 12 cells must fit one
-// owner thread per cell (W^2 <= 1024).
+// Block sizes: 8 and 12 for ranks that hold few blocks (a rank's share of a
+// multi-GPU run: C96 over 8 GPUs is 3 tiles of 48 per rank, 108 blocks of 8;
+// the per-block latency, which sets the step while every block is resident,
+// falls with the window: 1000 faces per step at B = 8 against 2584 at 16),
+// 16 (C96 on one GPU: 216 blocks), 18 and 20 (C180 tiles).
 extern "C" int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stream) {
   if (d->ns != 3) return -1;
-  if (d->B == 16) {
+  if (d->B == 8) {
+    if (dtype == 1) return launch_fused<double, 3, 8>(d, stream);
+    if (dtype == 0) return launch_fused<float, 3, 8>(d, stream);
+  } else if (d->B == 12) {
+    if (dtype == 1) return launch_fused<double, 3, 12>(d, stream);
+    if (dtype == 0) return launch_fused<float, 3, 12>(d, stream);
+  } else if (d->B == 16) {
     if (dtype == 1) return launch_fused<double, 3, 16>(d, stream);
     if (dtype == 0) return launch_fused<float, 3, 16>(d, stream);
   } else if (d->B == 18) {

@@ -98,8 +98,9 @@ typedef struct FusedDesc {
   const void* code;     // [nb][W*W] u64: 4 x int16 neighbour codes per window cell and side (-1, entry, -3)
   const int* gtab;      // [nb][G][2] LDS index of the interpolation pair
   const void* gw;       // [nb][G] interpolation weights
-  const int* ctab;      // [nb][C][8] corner faces: cu | cv << 8 | side_c << 16, du | dv << 8 | side_d << 16, fslot_c, fslot_d
-  const void* cgf;      // [nb][C][4] normal out of c, length
+  const int* ctab;      // [nb][C][16] corner faces (ops/fused.py::corner_tables): per side q (c, d) the cell's
+                        // LDS index and its across / inward stencil pairs (5 ints), face slots c, d, flags
+  const void* cgf;      // [nb][C][8] normal out of c, length, the four stencil weights
   const int* ccnt;      // [nb]
   const int* push;      // [T][4][mg][n] push map (same-rank ghost slot fed by a strip cell, or -1)
   int G, C;

@@ -184,7 +184,7 @@ class FusedPlan:
     """
 
     def __init__(self, layout: TileLayout, rank: int, grid, B: int = 16, ns: int = 3,
-                 source=None):
+                 source=None, other_tiles_remote: bool = False):
         self.layout = layout
         self.rank = rank
         self.grid = grid
@@ -201,8 +201,11 @@ class FusedPlan:
         self.T = len(self.tiles)
         self.nbx = self.nby = n // B
         self.nb = self.T * self.nbx * self.nby
-        # where a global cell lives: padded local offset (>= 0) or receive code
+        # where a global cell lives: padded local offset (>= 0) or receive code;
+        # other_tiles_remote (loopback rehearsal): a block reads every cell of
+        # another tile as a remote cell (-2), through the rank's own ring
         self._source = source or (lambda g: layout.local_flat(g))
+        self._other_remote = other_tiles_remote
         self._lx = grid.x_edge_lengths()
         self._ly = grid.y_edge_lengths()
         self._mx = grid.x_edge_normals()
@@ -312,6 +315,9 @@ class FusedPlan:
                     gv = g.reshape(-1)
                     m = gv >= 0
                     srcv[m] = self._source(gv[m])
+                    if self._other_remote:
+                        ot = L.locate(gv[m])[0] != tid
+                        srcv[np.flatnonzero(m)[ot]] = -2
                     assert (srcv[m] != -1).all()
                     self.src[bid] = srcv
                     self.gid[bid] = gv
@@ -862,15 +868,25 @@ class FusedTorch:
 # Device tables + descriptors of the gfx950 kernel (fused_step.hip)
 # ---------------------------------------------------------------------------
 
-FUSED_BLOCKS = (16, 18, 20)  # block sizes the kernel is instantiated for (preference order)
+FUSED_BLOCKS = (8, 12, 16, 18, 20)  # block sizes the kernel is instantiated for
 
 
-def fused_block(n: int) -> Optional[int]:
-    """Block size of the fused kernel for tiles of n x n cells (None: none fits)."""
-    for B in FUSED_BLOCKS:
-        if n % B == 0:
-            return B
-    return None
+def fused_block(n: int, tiles: Optional[int] = None, cus: Optional[int] = None) -> Optional[int]:
+    """Block size of the fused kernel for ``tiles`` tiles of n x n cells
+    (None: none divides n).  With the tile count and the GPU's CU count: the
+    smallest block whose blocks are all resident (one per CU: the step is one
+    block's latency, which falls with the block; several steps per launch need
+    every block resident), else the largest (one step per launch, fewest
+    blocks).  Without them: the largest."""
+    fits = [B for B in FUSED_BLOCKS if n % B == 0]
+    if not fits:
+        return None
+    if tiles is not None and cus is not None:
+        for B in fits:
+            if tiles * (n // B) ** 2 <= cus:
+                return B
+    return fits[-1]
+
 
 
 def fused_supported(engine, B: Optional[int] = None) -> Optional[str]:
@@ -883,8 +899,8 @@ def fused_supported(engine, B: Optional[int] = None) -> Optional[str]:
         return "fused step: PLR limiters only (PPM runs stage by stage)"
     if e.integ.name != "ssprk3":
         return "fused step: SSP-RK3 only"
-    if e.layout.loopback:
-        return "fused step: no loopback layouts"
+    if e.layout.loopback and e.layout.num_ranks > 1:
+        return "fused step: loopback layouts are one-rank rehearsals"
     B = B or fused_block(e.plan.n)
     if B is None or e.plan.n % B:
         return f"fused step: tile size {e.plan.n} is not a multiple of {' or '.join(map(str, FUSED_BLOCKS))}"
@@ -912,7 +928,11 @@ class FusedKernel:
         why = fused_supported(engine, B)
         if why:
             raise RuntimeError(why)
-        B = B or fused_block(engine.plan.n)
+        if B is None:
+            cus = None
+            if engine.device.type == "cuda":
+                cus = torch.cuda.get_device_properties(engine.device).multi_processor_count
+            B = fused_block(engine.plan.n, len(engine.plan.tiles), cus)
         e = engine
         self.e = e
         self.group = group
@@ -920,7 +940,7 @@ class FusedKernel:
         world = e.layout.num_ranks
         self.world = world
         X = None
-        if world > 1:
+        if world > 1 or e.layout.loopback:
             X = FusedExchangePlan(e.layout, e.grid, B, ns=3)
             P = X.plans[e.rank]
         else:
@@ -951,13 +971,7 @@ class FusedKernel:
         gpair = np.zeros((nb, G, 2), dtype=np.int32)
         gpair[..., 0] = ld(P.gtab[..., 2])
         gpair[..., 1] = ld(P.gtab[..., 3])
-        ct = np.zeros((nb, C, 8), dtype=np.int32)
-        for b in range(nb):
-            for j in range(int(P.ccnt[b])):
-                sc, side_c, sd, side_d, fc, fd = (int(x) for x in P.ctab[b, j])
-                ct[b, j, 0] = (sc % W) | ((sc // W) << 8) | (side_c << 16)
-                ct[b, j, 1] = (sd % W) | ((sd // W) << 8) | (side_d << 16)
-                ct[b, j, 2], ct[b, j, 3] = fc, fd
+        ct, cgw = corner_tables(P, code, gpair)
         org = P.org.copy()
         for b in range(nb):
             regs = set(int(x) for x in np.unique(P.reg[b]) if x >= 0)
@@ -977,7 +991,7 @@ class FusedKernel:
             "tane": t(kg["tane"]), "crec": t(kg["crec"]), "lxt": t(kg["lxt"]),
             "src": t(P.src, torch.int32), "org": t(org, torch.int32),
             "code": t(code.view(np.int64), torch.int64), "gtab": t(gpair, torch.int32), "gw": t(P.gt),
-            "ctab": t(ct, torch.int32), "cgf": t(P.cgeo), "ccnt": t(P.ccnt, torch.int32),
+            "ctab": t(ct, torch.int32), "cgf": t(cgw), "ccnt": t(P.ccnt, torch.int32),
             "push": torch.as_tensor(e.plan.push_map, dtype=torch.int32, device=dev).contiguous(),
         }
         rec_g = global_cell_records(e)
@@ -1063,7 +1077,8 @@ class FusedKernel:
         d.g = float(e.physics.g)
         d.omega2 = 2.0 * float(e.physics.omega)
         # one rank with every tile in id order: window sources computed in the kernel
-        d.local_src = 1 if (self.world == 1 and list(e.plan.tiles) == list(range(e.layout.num_tiles))) else 0
+        d.local_src = 1 if (self.world == 1 and not e.layout.loopback
+                            and list(e.plan.tiles) == list(range(e.layout.num_tiles))) else 0
         for f in range(6):
             d.links[f] = face_links(f)
         d.epoch = p(tn["epoch"])
@@ -1231,6 +1246,57 @@ def neighbour_codes(P: "FusedPlan") -> np.ndarray:
     return out.reshape(nb, W * W)
 
 
+def corner_tables(P: "FusedPlan", code: np.ndarray, gpair: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """Cube-corner faces resolved for the kernel (fused_step.hip, CT_INTS /
+    CG_VALS): ([nb, C, 16] int32, [nb, C, 8]).
+
+    Per face j and side q (0: cell c, 1: cell d): ints 5q .. 5q+4 = the cell's
+    LDS index, its "across" stencil neighbour as an LDS pair, its "inward"
+    neighbour as a pair; 10, 11 = face slots of c and d; 12 = flags (bit 2q:
+    across interpolated, 2q+1: inward interpolated, 4 + q: the face is on the
+    cell's + side).  Floats: normal out of c (3), length, then the weights
+    (across_c, inward_c, across_d, inward_d).  Across is the cell's neighbour
+    beyond the face in its own frame (a ghost entry -> its interpolation pair
+    and weight; a missing neighbour -> the cell itself), inward the one on the
+    other side (the window neighbour or a ghost entry): what the kernel
+    resolved from the codes at run time before round 4."""
+    d = P.d
+    W, WS, nb = d.W, d.W + 1, P.nb
+    C = P.ctab.shape[1]
+    ld = lambda s_: (s_ // W) * WS + s_ % W
+    ct = np.zeros((nb, C, 16), dtype=np.int32)
+    cg = np.zeros((nb, C, 8))
+    for b in range(nb):
+        for j in range(int(P.ccnt[b])):
+            sc, side_c, sd, side_d, fc, fd = (int(x) for x in P.ctab[b, j])
+            flags = 0
+            for q, (cell, side) in enumerate(((sc, side_c), (sd, side_d))):
+                plus = side & 1
+                st = WS if side >> 1 else 1
+                ic = ld(cell)
+                cd = int(code[b, cell])
+                nc = lambda sd_: int(np.int16(np.uint16((cd >> (16 * sd_)) & 0xFFFF)))
+                eac, ein = nc(side), nc(side ^ 1)
+                if eac >= 0:
+                    a0, a1, ta = int(gpair[b, eac, 0]), int(gpair[b, eac, 1]), float(P.gt[b, eac])
+                    flags |= 1 << (2 * q)
+                else:
+                    a0 = a1 = ic
+                    ta = 0.0
+                if ein >= 0:
+                    n0, n1, tn = int(gpair[b, ein, 0]), int(gpair[b, ein, 1]), float(P.gt[b, ein])
+                    flags |= 1 << (2 * q + 1)
+                else:
+                    n0 = n1 = ic - st if plus else ic + st
+                    tn = 0.0
+                flags |= plus << (4 + q)
+                ct[b, j, 5 * q:5 * q + 5] = (ic, a0, a1, n0, n1)
+                cg[b, j, 4 + 2 * q], cg[b, j, 5 + 2 * q] = ta, tn
+            ct[b, j, 10], ct[b, j, 11], ct[b, j, 12] = fc, fd, flags
+            cg[b, j, :4] = P.cgeo[b, j]
+    return ct, cg
+
+
 def producer_table(P: "FusedPlan") -> np.ndarray:
     """[nb, PM] int32: the blocks of this rank whose cells each block's window
     loads (its producers for a step inside a multi-step launch), made
@@ -1292,6 +1358,10 @@ class FusedExchangePlan:
         world = L.num_ranks
         owner = np.asarray(L.owner)
         self.world = world
+        # loopback (one rank, layout.loopback): the window cells of every other
+        # tile travel through the rank's own ring, so one GPU runs the whole
+        # xGMI protocol (tagged granules, ring slots, remote-cell geometry)
+        self.loopback = bool(L.loopback) and world == 1
 
         def source_for(p):
             def src(g):
@@ -1300,7 +1370,8 @@ class FusedExchangePlan:
                 return np.where(owner[tid] == p, loc, -2)
             return src
 
-        self.plans = [FusedPlan(L, p, grid, B=B, ns=ns, source=source_for(p)) for p in range(world)]
+        self.plans = [FusedPlan(L, p, grid, B=B, ns=ns, source=source_for(p), other_tiles_remote=self.loopback)
+                      for p in range(world)]
         self.need_remote: List[np.ndarray] = []
         for p, P in enumerate(self.plans):
             m = P.need[:, 0] & (P.src == -2)
@@ -1328,7 +1399,7 @@ class FusedExchangePlan:
         ent: Dict[int, List[int]] = {}
         psrc, pcode = [], []
         for p in range(self.world):
-            if p == rank:
+            if p == rank and not self.loopback:
                 continue
             g = self.need_remote[p]
             tid, i, j = L.locate(g)

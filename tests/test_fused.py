@@ -76,8 +76,9 @@ def test_fused_supported_reasons():
     assert "PLR" in fused_supported(e)
     e = Engine(ShallowWater("tc5"), L, integrator="rk4")
     assert "SSP-RK3" in fused_supported(e)
-    e = Engine(ShallowWater("tc5"), TileLayout(24, 2, 1, ng=2))
-    assert "multiple of 16 or 18 or 20" in fused_supported(e)
+    e = Engine(ShallowWater("tc5"), TileLayout(28, 2, 1, ng=2))
+    assert "multiple of 8 or 12 or 16 or 18 or 20" in fused_supported(e)
+    assert fused_supported(Engine(ShallowWater("tc5"), TileLayout(24, 2, 1, ng=2))) is None   # B = 12
     assert fused_supported(Engine(ShallowWater("tc5"), TileLayout(36, 2, 1, ng=2))) is None   # B = 18
     assert fused_supported(Engine(ShallowWater("tc5"), TileLayout(40, 2, 1, ng=2))) is None   # B = 20
     e = Engine(ShallowWater("tc5"), TileLayout(32, 2, 1, ng=2))
@@ -99,8 +100,11 @@ def _gpu_pair(N, t, dtype=torch.float64, case="tc5", lim=2):
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,t,case,lim", [(32, 2, "tc5", 2), (48, 1, "tc5", 1), (96, 2, "tc5", 2),
                                           (48, 3, "tc6", 3), (32, 1, "tc2", 0), (36, 2, "tc5", 2),
-                                          (54, 1, "tc2", 1), (40, 2, "tc5", 2), (60, 3, "tc6", 2)])
+                                          (54, 1, "tc2", 1), (40, 2, "tc5", 2), (60, 3, "tc6", 2),
+                                          (48, 4, "tc5", 2), (72, 3, "tc5", 2)])
 def test_fused_kernel_fp64_matches_oracle(N, t, case, lim):
+    """Every block size through the residency-aware choice: 8 ((32, 2), (48, 1),
+    (48, 3), (32, 1)), 12 ((48, 4), (72, 3)), 16 (96, 2), 18 ((36, 2), (54, 1)), 20."""
     from stsphere.ops.fused import FusedKernel
     ref, hip = _gpu_pair(N, t, case=case, lim=lim)
     fk = FusedKernel(hip)
@@ -303,6 +307,26 @@ def test_kernel_tables_cpu():
     assert (c[np.broadcast_to(~valid[:, None], c.shape)] == -3).all()
     ok = np.broadcast_to(valid[:, None], c.shape)
     assert np.array_equal(np.where(ok, c, -1), np.where(ok, sub, -1))
+    # cube-corner faces resolved on the host: every stencil index is a window
+    # cell (interpolation pairs of ghost entries included), the plain ones are
+    # the cell itself (across) or its window neighbour (inward)
+    from stsphere.ops.fused import corner_tables
+    WS = W + 1
+    ld = lambda s_: (s_ // W) * WS + s_ % W
+    gpair = np.stack([ld(P.gtab[..., 2]), ld(P.gtab[..., 3])], -1)
+    ct, cg = corner_tables(P, codes, gpair)
+    assert P.ccnt.max() > 0
+    for b in range(P.nb):
+        for j in range(int(P.ccnt[b])):
+            r = ct[b, j]
+            assert ((r[:10] >= 0) & (r[:10] < W * WS)).all()
+            assert (r[10], r[11]) == (P.ctab[b, j, 4], P.ctab[b, j, 5])
+            for q in range(2):
+                ic, a0, a1, n0, n1 = r[5 * q:5 * q + 5]
+                if not (r[12] >> (2 * q)) & 1:
+                    assert a0 == a1 == ic and cg[b, j, 4 + 2 * q] == 0.0
+                if not (r[12] >> (2 * q + 1)) & 1:
+                    assert n0 == n1 and abs(int(n0) - int(ic)) in (1, WS)
     rec = global_cell_records(e)
     loc = e.geo.gather_global(rec[:, 7:10].reshape(6, N, N, 3))          # [T,n,n,3]
     sbal = e.tens["sbal"].permute(1, 2, 3, 0).numpy()                    # 0.5 g S / A
@@ -361,3 +385,53 @@ def test_kernel_geometry_reconstruction_cpu(N, t, B):
                 m = _to_global(int(kg["frames"][face]), 0.0 if ax else rn, rn if ax else 0.0, -tn * rn)
                 assert np.allclose(m, P.nrm[b, ax, 0, k], atol=1e-14), (b, ax, k)
     assert inner > 0
+
+
+@pytest.mark.parametrize("N,t,B", [(32, 2, 8), (48, 1, 16), (24, 2, 12)])
+def test_fused_loopback_plan_equals_one_rank_cpu(N, t, B):
+    """Loopback rehearsal (one rank, layout.loopback): every window cell of
+    another tile is a remote cell read from the rank's own ring.  With the
+    ring filled from the current state (what the producers' ring stores
+    deliver), the PyTorch rendering equals the plain one-rank fused step bit
+    for bit, and every ring slot has exactly one producer entry."""
+    from stsphere.ops.fused import FusedExchangePlan
+    grid = CubedSphereGrid(N)
+    L1 = TileLayout(N, t, 1, ng=2)
+    one = Engine(ShallowWater("tc5"), L1, grid=grid)
+    f1 = FusedTorch(one, FusedPlan(L1, 0, grid, B=B))
+    Llb = TileLayout(N, t, 1, ng=2, loopback=True)
+    X = FusedExchangePlan(Llb, grid, B)
+    assert X.loopback and (X.plans[0].src <= -2).any()
+    _, _, pcode = X.producer(0)
+    assert sorted(pcode.tolist()) == list(range(len(X.need_remote[0])))
+    lb = Engine(ShallowWater("tc5"), Llb, grid=grid, dt=one.dt)
+    flb = FusedTorch(lb, X.plans[0], remote_cells=X.need_remote[0])
+    off = Llb.local_flat(X.need_remote[0])
+    for _ in range(2):
+        f1.step()
+        recv = lb.pool[0][:, torch.as_tensor(off)].t()
+        flb.step(recv)
+    assert torch.equal(one.tiles_view(), lb.tiles_view())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,t", [(32, 2), (96, 2)])
+def test_fused_loopback_kernel_equals_one_rank(N, t):
+    """The gfx950 fused kernel on a loopback layout (the xGMI ring protocol
+    through the rank's own ring, tagged granules every step, one and several
+    steps per launch) equals the plain one-rank fused step bit for bit."""
+    from stsphere.ops.fused import FusedKernel
+    grid = CubedSphereGrid(N)
+    _, a = _gpu_pair(N, t)
+    Llb = TileLayout(N, t, 1, ng=2, loopback=True)
+    b = Engine(ShallowWater("tc5"), Llb, grid=grid, dtype=torch.float64, device="cuda", backend="hip", dt=a.dt)
+    fa, fb = FusedKernel(a), FusedKernel(b, B=fa.plan.B)
+    assert fb.mem is not None
+    fa.step(3)
+    fb.step(3)
+    fa.launch(0, nsteps=4)
+    fb.launch(0, nsteps=4)
+    torch.cuda.synchronize()
+    fb.check()
+    assert torch.equal(a.tiles_view(), b.tiles_view())
+    fb.close()

@@ -120,7 +120,7 @@ def test_solver_run_replays_graphs_for_io_intervals(tmp_path):
     from stsphere.utils.history import read_history, read_metrics
     c = _cfg(1, 2, N=48, out=str(tmp_path))
     c["io"].update(history_interval=12, metrics_interval=6)
-    c["runtime"].update(watchdog_interval=6, steps_per_graph=30)
+    c["runtime"].update(watchdog_interval=6, steps_per_graph=30, fused="off")   # the stage path's graphs
     s = Solver(c, verbose=False)
     s.initialize()
     out = s.run(nsteps=40)

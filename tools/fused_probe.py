@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--stage", action="store_true", help="also time the launch-per-stage step")
+    ap.add_argument("--B", type=int, default=0, help="block size (0: the residency-aware choice)")
+    ap.add_argument("--loopback", action="store_true",
+                    help="every other tile's window cells through the rank's own xGMI ring (tagged granules)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -32,10 +35,10 @@ def main():
     from stsphere.ops.native_runtime import NativeStepper
     from stsphere.parallel.layout import TileLayout
     dt = torch.float64 if a.dtype == "fp64" else torch.float32
-    L = TileLayout(a.N, a.t, 1, ng=2)
+    L = TileLayout(a.N, a.t, 1, ng=2, loopback=a.loopback)
     e = Engine(ShallowWater("tc5"), L, grid=CubedSphereGrid(a.N), dtype=dt, device="cuda", backend="hip")
-    fk = FusedKernel(e)
-    out = {"N": a.N, "t": a.t, "dtype": a.dtype, "blocks": fk.plan.nb, "B": fk.plan.B}
+    fk = FusedKernel(e, B=a.B or None)
+    out = {"N": a.N, "t": a.t, "dtype": a.dtype, "blocks": fk.plan.nb, "B": fk.plan.B, "loopback": a.loopback}
     fk.step(4)
     torch.cuda.synchronize()
     s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
