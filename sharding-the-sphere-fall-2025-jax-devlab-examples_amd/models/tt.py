@@ -183,7 +183,18 @@ class LowRankField:
 
     @classmethod
     def from_dense(cls, U: torch.Tensor, eps: float = 1e-10, max_rank: Optional[int] = None) -> "LowRankField":
-        u, s, vh = torch.linalg.svd(U, full_matrices=False)
+        """Truncated SVD of a dense field (setup, not a step).  rocSOLVER's
+        gesvd gives up on exactly-zero inputs (a field at rest): those are the
+        rank-1 zero field, and a device SVD that fails to converge is redone on
+        the host in fp64."""
+        if not bool(U.any()):
+            z = torch.zeros((U.shape[0], 1), dtype=U.dtype, device=U.device)
+            return cls(z, torch.zeros((U.shape[1], 1), dtype=U.dtype, device=U.device))
+        try:
+            u, s, vh = torch.linalg.svd(U, full_matrices=False)
+        except RuntimeError:
+            Uh = U.detach().to(device="cpu", dtype=torch.float64)
+            u, s, vh = (x.to(device=U.device, dtype=U.dtype) for x in torch.linalg.svd(Uh, full_matrices=False))
         r = _trunc_rank(s, eps * float(torch.linalg.norm(U)), max_rank)
         return cls(u[:, :r] * s[:r], vh[:r].T.contiguous())
 

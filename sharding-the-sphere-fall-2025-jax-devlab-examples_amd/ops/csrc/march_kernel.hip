@@ -27,9 +27,13 @@
 //     last rows of the tile.
 //
 // Same inputs and outputs as one stage_kernel launch (StageDesc), same push map
-// for the same-rank ghost strips; PLR limiters only (PPM keeps the block kernel),
-// one rank without remote ghosts.  Compared with the fp64 PyTorch oracle in
-// tests/test_march.py.
+// for the same-rank ghost strips; PLR limiters only (PPM keeps the block kernel).
+// Several ranks (XG): the direct xGMI exchange of the block kernel, tagged
+// granules (ops/xgmi.py): a ghost cell that belongs to another rank is read
+// from this rank's receive ring (spin until its granules carry this stage's
+// tag), and a cell that is another rank's ghost is stored into that rank's
+// ring (push-map entries <= -2); each wave (job) keeps its own stage count.
+// Compared with the fp64 PyTorch oracle in tests/test_march.py.
 #include "stage_common.h"
 
 namespace {
@@ -89,7 +93,7 @@ __device__ __forceinline__ void frame_to_global(int fr, T xi, T xj, T xn, T& o0,
 // edge lengths by panel-local index) instead of the per-tile records, and the
 // topography gradient formed from b itself (104 instead of 176 B per fp64 cell
 // through HBM; the shared tables are read by all six panels)
-template <typename T, int LIM, int R, bool ACC, bool CG>
+template <typename T, int LIM, int R, bool ACC, bool CG, bool XG>
 __global__ __launch_bounds__(MW * MWPB) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 8 ? STSP_MARCH_WPE64 : STSP_MARCH_WPE32)))
 void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   pin_args(a);
@@ -121,6 +125,52 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
 #pragma unroll
     for (int f = 0; f < 4; ++f) q[f] = bld<T>(rQ, pa * ES, f * fs);
   };
+  // XG: this job's stage count (tags), and the cell load that takes a remote
+  // ghost from the receive ring
+  int xe = 0;
+  if constexpr (XG) xe = a.epoch[gw];
+  auto ldc = [&](int cx, int y, T (&q)[4]) {
+    if constexpr (XG) {
+      const bool gx = (unsigned)cx >= (unsigned)n, gy = (unsigned)y >= (unsigned)n;
+      if (gx != gy) {                              // an edge ghost (corners are never remote)
+        const int side = gx ? (cx < 0 ? 0 : 1) : (y < 0 ? 2 : 3);
+        const int layer = gx ? (cx < 0 ? -1 - cx : cx - n) : (y < 0 ? -1 - y : y - n);
+        const int pos = gx ? y : cx;
+        const int m = layer < mg ? a.gmap[((tile * 4 + side) * mg + layer) * n + pos] : 0;
+        if (m < 0) {                               // remote slot -1 - m: spin on its granules
+          constexpr int G = sizeof(T) / 4;
+          const gu64* rp = ((const gu64*)(a.recv)) + (long)(xe % STSP_XG_SLOTS) * a.ring + (long)(-1 - m) * (4 * G);
+          const unsigned want = (unsigned)xe + 1u;
+          unsigned long long gr[4 * G];
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          for (;;) {
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < 4 * G; ++k) {
+              gr[k] = __hip_atomic_load(rp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              ok &= (unsigned)(gr[k] >> 32) == want;
+            }
+            if (ok) break;
+            if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+            if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
+              __hip_atomic_store((gu32*)a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+#pragma unroll
+          for (int f = 0; f < 4; ++f) {
+            if constexpr (G == 2)
+              q[f] = __builtin_bit_cast(T, (gr[2 * f + 1] << 32) | (gr[2 * f] & 0xFFFFFFFFull));
+            else
+              q[f] = __builtin_bit_cast(T, (unsigned)gr[f]);
+          }
+          return;
+        }
+      }
+    }
+    ldq(cell(cx, y), q);
+  };
   // primitive (h, v) + sound speed, as the block kernel's put()
   auto prim = [&](const T (&q)[4], T (&w)[5]) {
     const T inv = q[0] != T(0) ? trcp(q[0]) : T(0);
@@ -131,10 +181,10 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
     w[4] = tsqrt(g * tmax(q[0], T(0)));
   };
   // linear interpolation between the primitives of two cells
-  auto interp2 = [&](unsigned p0, unsigned p1, T t, T (&o)[4]) {
+  auto interp2 = [&](int x0_, int y0_, int x1_, int y1_, T t, T (&o)[4]) {
     T q0[4], q1[4], w0[5], w1[5];
-    ldq(p0, q0);
-    ldq(p1, q1);
+    ldc(x0_, y0_, q0);
+    ldc(x1_, y1_, q1);
     prim(q0, w0);
     prim(q1, w1);
 #pragma unroll
@@ -157,7 +207,7 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
     const unsigned ti = tab(side, inx ? x : 0);
     const int b = a.pe_base[ti];
     const T t = a.pe_t[ti];
-    interp2(cell(b, y), cell(b + 1, y), t, o);
+    interp2(b, y, b + 1, y, t, o);
   };
   // W / E strips (along y, one table entry per row): every lane interpolates its
   // own column between rows b and b + 1
@@ -165,7 +215,7 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
     const unsigned ti = tab(side, j);
     const int b = a.pe_base[ti];
     const T t = a.pe_t[ti];
-    interp2(cell(xc, b), cell(xc, b + 1), t, o);
+    interp2(xc, b, xc, b + 1, t, o);
   };
 
   // the primitives a row offers to its y-neighbours' slopes: the raw cells,
@@ -227,10 +277,10 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   T Ls;                                              // length of the face below row j
   {
     T q[4], cm2[5], cm1[5];
-    ldq(cell(xc, y0 - 2), q); prim(q, cm2);
-    ldq(cell(xc, y0 - 1), q); prim(q, cm1);
-    ldq(cell(xc, y0), q);     prim(q, cA);
-    ldq(cell(xc, y0 + 1), q); prim(q, cB);
+    ldc(xc, y0 - 2, q); prim(q, cm2);
+    ldc(xc, y0 - 1, q); prim(q, cm1);
+    ldc(xc, y0, q);     prim(q, cA);
+    ldc(xc, y0 + 1, q); prim(q, cB);
     T wsm2[4], wsm1[4], ws0[4], ws1[4];
     wsrow(y0 - 2, cm2, wsm2);
     wsrow(y0 - 1, cm1, wsm1);
@@ -249,7 +299,7 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
     swe_flux<T>(wl, wr, cm1, cA, myt[0 * (n + 1) + y0], myt[1 * (n + 1) + y0], myt[2 * (n + 1) + y0], Ls, g, Gs);
   }
   T qn[4];                                           // raw row j + 2, loaded one step ahead
-  ldq(cell(xc, y0 + 2), qn);
+  ldc(xc, y0 + 2, qn);
   T bS = T(0), bA = T(0), bB = T(0), bn = T(0);       // topography of rows j - 1 .. j + 2 (CG)
   if (topo) {
     bS = bld<T>(rB, cell(xc, y0 - 1) * ES, 0);
@@ -263,13 +313,13 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
     prim(qn, cC);
     const T bC = bn;
     if (j + 1 < y1) {                                // prefetch (row j + 3 <= n + 1)
-      ldq(cell(xc, j + 3), qn);
+      ldc(xc, j + 3, qn);
       if (topo) bn = bld<T>(rB, cell(xc, j + 3) * ES, 0);
     }
     // own-row operands of row j (needed after the fluxes)
     const unsigned pc = cell(xc, j);
     T qo[4], xs[4], acs[ACC ? 4 : 1], rec[8];
-    ldq(pc, qo);
+    ldc(xc, j, qo);
 #pragma unroll
     for (int f = 0; f < 4; ++f) xs[f] = T(0);
     if (need_x) {
@@ -442,6 +492,24 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
         if (pt[k] >= 0) {
 #pragma unroll
           for (int f = 0; f < 4; ++f) bst<0>(o[f], rO, (unsigned)pt[k] * ES, f * fs);
+        } else if (XG && pt[k] <= -2) {
+          // another rank's ghost: its ring slot (xe + 1) % SLOTS, tag xe + 2
+          constexpr int G = sizeof(T) / 4;
+          const int code = -2 - pt[k];
+          gu64* dst = ((gu64*)(a.peer_ring[code >> 24])) + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring +
+                      (long)(code & 0xFFFFFF) * (4 * G);
+          const unsigned long long tag = (unsigned long long)((unsigned)xe + 2u) << 32;
+#pragma unroll
+          for (int f = 0; f < 4; ++f) {
+            if constexpr (G == 2) {
+              const unsigned long long bits = __builtin_bit_cast(unsigned long long, o[f]);
+              __hip_atomic_store(dst + 2 * f, tag | (bits & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(dst + 2 * f + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+              __hip_atomic_store(dst + f, tag | __builtin_bit_cast(unsigned, o[f]), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+          }
         }
       }
     }
@@ -453,6 +521,9 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
     Ls = Ln;
     bS = bA; bA = bB; bB = bC;
   }
+  if constexpr (XG) {
+    if (lane == 0) a.epoch[gw] = xe + 1;           // read again at the next stage's launch
+  }
 }
 
 template <typename T, int LIM, int R>
@@ -462,12 +533,21 @@ int march_l(const StageDesc* d, hipStream_t s) {
   const int njobs = d->ntile * ncs * nrs;
   const int nb = (njobs + MWPB - 1) / MWPB;
   const bool cg = d->crec && d->lxt && d->torg;
+  if (d->xg) {      // several ranks, direct xGMI exchange (SSP-RK3 / Euler stages, rows R = 4)
+    if constexpr (R == 4) {
+      if (d->acc_out) return -13;
+      if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, false, true, true>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+      else hipLaunchKernelGGL((march_kernel<T, LIM, R, false, false, true>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+      return (int)hipGetLastError();
+    }
+    return -13;
+  }
   if (d->acc_out) {
-    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, true, true>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
-    else hipLaunchKernelGGL((march_kernel<T, LIM, R, true, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, true, true, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+    else hipLaunchKernelGGL((march_kernel<T, LIM, R, true, false, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
   } else {
-    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, false, true>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
-    else hipLaunchKernelGGL((march_kernel<T, LIM, R, false, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, false, true, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+    else hipLaunchKernelGGL((march_kernel<T, LIM, R, false, false, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
   }
   return (int)hipGetLastError();
 }
@@ -506,10 +586,14 @@ __global__ void dpp_probe_kernel(const double* in, double* out, float* outf) {
 
 }  // namespace
 
-// Rows per wave `rows` (4, 8, 16, 32).  Shallow water, PLR, one rank with every
-// ghost local (no remote ghosts, no xGMI, no block list).
+// Rows per wave `rows` (4, 8, 16, 32).  Shallow water, PLR; remote ghosts only
+// through the direct xGMI exchange with tagged granules (d->xg, rows 4; the
+// epoch array has one count per job), never through a receive buffer or a
+// block list.
 extern "C" int stsp_march_launch(int dtype, int rows, const StageDesc* d, hipStream_t stream) {
-  if (d->xg || d->remote || d->blocks) return -13;
+  if (d->remote || d->blocks) return -13;
+  if (d->xg && (!STSP_XG_TAG || !d->recv || !d->peer_ring || !d->epoch || !d->err || !d->gmap || d->ring <= 0))
+    return -13;
   if (d->pw != d->n + 2 * d->mg || d->mg < 2 || d->n < 2) return -5;
   if (!d->pedge || !d->pe_base || !d->pe_t || !d->push || !d->mx || !d->my) return -12;
   const bool cg = d->crec && d->lxt && d->torg;

@@ -21,8 +21,9 @@ from ..models.integrators import Stage
 
 BLOCK_SHAPES = ((16, 16), (32, 8), (16, 8), (8, 16), (8, 8))
 # The streaming stage (ops/csrc/march_kernel.hip): (64, R) = one wave marches 60
-# columns up R rows of a tile.  Shallow water with a PLR limiter, one rank
-# without remote ghosts.
+# columns up R rows of a tile.  Shallow water with a PLR limiter; remote ghosts
+# only through the direct xGMI exchange (XgmiHalo switches a rank to it,
+# rows 4), never through RCCL's receive buffer and block lists.
 MARCH_SHAPES = ((64, 4), (64, 8), (64, 16), (64, 32))
 
 
@@ -30,8 +31,8 @@ MARCH_AUTO = (64, 4)
 MARCH_CELLS_PER_CU = 8192
 
 
-def march_supported(phys_id: int, limiter: int, remote: bool) -> bool:
-    return phys_id == 2 and limiter != 4 and not remote
+def march_supported(phys_id: int, limiter: int, remote: bool, xgmi: bool = False) -> bool:
+    return phys_id == 2 and limiter != 4 and (not remote or xgmi)
 
 
 def march_tables(engine) -> dict:
@@ -53,14 +54,23 @@ def march_tables(engine) -> dict:
     if gf is not None:
         b = np.asarray(gf(e.grid)[2], dtype=np.float64)
         if np.any(b != 0):
+            from ..parallel.layout import ghost_xy
             n, P, ng = plan.n, plan.P, plan.ng
             bp = np.zeros((plan.T, P, P))
             for li, tid in enumerate(plan.tiles):
                 f, I0, J0 = lay.tile_origin(tid)
                 bp[li, ng:ng + n, ng:ng + n] = b[f, J0:J0 + n, I0:I0 + n]
-            flat = bp.reshape(-1)
-            flat[plan.halo_dst] = flat[plan.halo_src]
-            out["bpad"] = t(flat)
+            # every edge ghost from its global source (same-rank and remote alike:
+            # the topography is static, so no exchange carries it)
+            gs = lay.ghost_sources(e.rank)                       # [T, 4, ng, n]
+            bg = b.reshape(-1)
+            pos = np.arange(n)
+            for li in range(plan.T):
+                for side in range(4):
+                    for k in range(ng):
+                        x, y = ghost_xy(side, k, pos, n)
+                        bp[li, y + ng, x + ng] = bg[gs[li, side, k]]
+            out["bpad"] = t(bp.reshape(-1))
     return out
 
 
@@ -163,37 +173,33 @@ class HipCompute:
         self.phys_id = phys.kernel_id
         self.dcode = native.dtype_code(e.dtype)
         n, T = plan.n, plan.T
+        self.march_wanted = False       # the size rule picks the streaming stage (XgmiHalo may switch)
         if e.block is None:
             cus = torch.cuda.get_device_properties(e.device).multi_processor_count
             bx, by = choose_block(n, T, cus, getattr(phys, "limiter", 0), torch.tensor([], dtype=e.dtype).element_size())
             # streaming stage once the rank streams: measured C720 (3.1M cells, 12k per CU)
             # fp64 423 vs 467 us/step, fp32 190 vs 252 (64 x 4; 64 x 8: 431 / 203); C360 (3k per CU) a tie,
             # C180 the block kernel (43 vs 75): too few marches to hide their latency
-            if march_supported(self.phys_id, int(phys.kernel_params().get("limiter", 0)), plan.num_recv > 0) \
-                    and T * n * n >= MARCH_CELLS_PER_CU * cus:
+            lim = int(phys.kernel_params().get("limiter", 0))
+            self.march_wanted = march_supported(self.phys_id, lim, False) and T * n * n >= MARCH_CELLS_PER_CU * cus
+            if self.march_wanted and march_supported(self.phys_id, lim, plan.num_recv > 0):
                 bx, by = MARCH_AUTO
         else:
             bx, by = e.block
         self.march = (bx, by) in MARCH_SHAPES
         if self.march:
-            if not march_supported(self.phys_id, int(phys.kernel_params().get("limiter", 0)), plan.num_recv > 0):
-                raise ValueError("the streaming stage (block (64, R)) runs shallow water with a PLR limiter "
-                                 "on a rank without remote ghosts")
+            if not march_supported(self.phys_id, int(phys.kernel_params().get("limiter", 0)), False) or \
+                    (plan.num_recv > 0 and by != 4):
+                raise ValueError("the streaming stage (block (64, R)) runs shallow water with a PLR limiter; "
+                                 "a rank with remote ghosts marches 4 rows per wave through the xGMI exchange")
         elif (bx, by) not in BLOCK_SHAPES:
             raise ValueError(f"unsupported block shape {(bx, by)}")
-        self.bx, self.by = bx, by
-        if self.march:   # jobs: (tile, 60-column strip, R-row segment), four per workgroup
-            self.nbx, self.nby = -(-n // 60), -(-n // by)
-        else:
-            self.nbx, self.nby = -(-n // bx), -(-n // by)
-        self.nblocks = T * self.nbx * self.nby
+        self._shape(bx, by)
         # streaming stage geometry: compact (panel-shared tables, grad b from b) for fp64,
         # per-tile records for fp32 (C720 64x4: fp64 409 vs 415 us/step, fp32 225 vs 195,
         # where the compact path spills; profiles/r3_march/sizes_compact_geometry_ab.log);
         # STSP_MARCH_COMPACT=0/1 overrides
-        import os
-        cg = os.environ.get("STSP_MARCH_COMPACT", "1" if e.dtype == torch.float64 else "0") != "0"
-        self.mt = march_tables(e) if self.march and cg else None
+        self._tables()
         t = e.tens
         F, S = phys.F, plan.S
         # ---- host-side shape contract checks ----------------------------
@@ -240,6 +246,34 @@ class HipCompute:
         self._g = phys.kernel_params().get("g", 0.0)
         self._omega2 = phys.kernel_params().get("omega2", 0.0)
         self._lim = int(phys.kernel_params().get("limiter", 0))
+
+    def _shape(self, bx: int, by: int) -> None:
+        n, T = self.e.plan.n, self.e.plan.T
+        self.bx, self.by = bx, by
+        self.march = (bx, by) in MARCH_SHAPES
+        if self.march:   # jobs: (tile, 60-column strip, R-row segment), four per workgroup
+            self.nbx, self.nby = -(-n // 60), -(-n // by)
+        else:
+            self.nbx, self.nby = -(-n // bx), -(-n // by)
+        self.nblocks = T * self.nbx * self.nby
+
+    def _tables(self) -> None:
+        import os
+        e = self.e
+        cg = os.environ.get("STSP_MARCH_COMPACT", "1" if e.dtype == torch.float64 else "0") != "0"
+        self.mt = march_tables(e) if self.march and cg else None
+
+    def use_march_with_xgmi(self) -> bool:
+        """Switch a rank with remote ghosts to the streaming stage when the size
+        rule wants it: the direct xGMI exchange (XgmiHalo) delivers its remote
+        ghosts inside the march kernel (rows 4).  True if the rank marches."""
+        if self.march:
+            return True
+        if not self.march_wanted or self.e.block is not None:
+            return False
+        self._shape(*MARCH_AUTO)
+        self._tables()
+        return True
 
     def desc(self, st: Stage, dt: float, blocks: Optional[torch.Tensor], nblocks: int,
              remote: bool = False) -> native.StageDesc:

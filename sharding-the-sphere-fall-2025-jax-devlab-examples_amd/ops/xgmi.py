@@ -197,6 +197,7 @@ class XgmiHalo:
         world = e.layout.num_ranks
         self.world = world
         self.rank = e.rank
+        hc.use_march_with_xgmi()         # large ranks stream (march_kernel.hip reads the ring itself)
         self.xp = XgmiPlan(e.layout, e.rank, hc.bx, hc.by, e.physics.halo)
         self._check_chain(e.integ)
         dev = e.device
@@ -225,7 +226,9 @@ class XgmiHalo:
         self.peer_cnt = torch.as_tensor(pc, device=dev)
         self.nprod = torch.as_tensor(self.xp.nprod, device=dev)
         self.bmask = torch.as_tensor(self.xp.bmask, device=dev)
-        self.epoch = torch.zeros(self.xp.nblocks, dtype=torch.int32, device=dev)
+        # per-block (stage kernel) or per-job (march kernel) stage counts
+        assert hc.march or hc.nblocks == self.xp.nblocks
+        self.epoch = torch.zeros(hc.nblocks, dtype=torch.int32, device=dev)
         self.err = torch.zeros(4, dtype=torch.int32, device=dev)
         self.push = torch.as_tensor(self.xp.push, device=dev)
         self.prime_src = torch.as_tensor(self.xp.prime_src, device=dev)

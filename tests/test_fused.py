@@ -425,7 +425,8 @@ def test_fused_loopback_kernel_equals_one_rank(N, t):
     _, a = _gpu_pair(N, t)
     Llb = TileLayout(N, t, 1, ng=2, loopback=True)
     b = Engine(ShallowWater("tc5"), Llb, grid=grid, dtype=torch.float64, device="cuda", backend="hip", dt=a.dt)
-    fa, fb = FusedKernel(a), FusedKernel(b, B=fa.plan.B)
+    fa = FusedKernel(a)
+    fb = FusedKernel(b, B=fa.plan.B)
     assert fb.mem is not None
     fa.step(3)
     fb.step(3)

@@ -90,7 +90,34 @@ def test_xgmi_loopback_advection_and_reprime():
     xg.close()
 
 
-def _worker(rank, world, port, N, t, steps, outdir):
+@pytest.mark.parametrize("N,t,dtype", [(24, 2, torch.float64), (48, 1, torch.float64), (32, 2, torch.float32)])
+def test_xgmi_loopback_march_matches_single(N, t, dtype):
+    """The streaming stage (march_kernel.hip, 64 x 4) with the direct xGMI
+    exchange: every ghost of a loopback rank is read from its own ring by the
+    march's halo lanes and edge rows and stored into it by the cells that feed
+    it (tagged granules), against the one-rank march: bit for bit."""
+    from stsphere.ops.native_runtime import NativeStepper
+    from stsphere.ops.xgmi import XgmiHalo
+    g = CubedSphereGrid(N)
+    a = Engine(ShallowWater("tc5"), TileLayout(N, t, 1, ng=2), grid=g, device="cuda", backend="hip", dtype=dtype,
+               block=(64, 4))
+    L = TileLayout(N, t, 1, ng=2, loopback=True)
+    b = Engine(ShallowWater("tc5"), L, grid=g, device="cuda", backend="hip", dtype=dtype, dt=a.dt, block=(64, 4),
+               transport=NativeBuffers(L.plan(0), 4, dtype, torch.device("cuda")))
+    assert a.compute.march and b.compute.march
+    xg = XgmiHalo(b, timeout_s=1.0)
+    ns = NativeStepper(b, use_graph=True, steps_per_graph=4, xgmi=xg)
+    a.step(8)
+    ns.run(8)
+    torch.cuda.synchronize()
+    ns.check()
+    assert torch.equal(a.tiles_view(), b.tiles_view())
+    assert int(xg.epoch.min()) == int(xg.epoch.max()) >= 8 * len(b.integ.stages)
+    ns.close()
+    xg.close()
+
+
+def _worker(rank, world, port, N, t, steps, outdir, block=None):
     import torch.distributed as dist
     from stsphere.ops.native_runtime import NativeStepper
     from stsphere.ops.xgmi import XgmiHalo
@@ -100,7 +127,7 @@ def _worker(rank, world, port, N, t, steps, outdir):
     try:
         L = TileLayout(N, t, world, ng=2)
         dev = torch.device("cuda:0")
-        e = Engine(ShallowWater("tc5"), L, rank, device=dev, backend="hip", dt=200.0,
+        e = Engine(ShallowWater("tc5"), L, rank, device=dev, backend="hip", dt=200.0, block=block,
                    transport=NativeBuffers(L.plan(rank), 4, torch.float64, dev))
         xg = XgmiHalo(e, timeout_s=5.0)
         ns = NativeStepper(e, use_graph=True, steps_per_graph=5, xgmi=xg)
@@ -122,6 +149,23 @@ def test_xgmi_multiprocess_one_gpu(world, t):
     mp.spawn(_worker, args=(world, _free_port(), N, t, steps, out), nprocs=world, join=True)
     g = CubedSphereGrid(N)
     single = Engine(ShallowWater("tc5"), TileLayout(N, t, 1, ng=2), grid=g, device="cuda", backend="hip", dt=200.0)
+    single.step(steps)
+    L = TileLayout(N, t, world, ng=2)
+    for f in range(4):
+        glob = assemble_global(L, {r: np.load(os.path.join(out, f"r{r}.npy"))[f] for r in range(world)})
+        assert np.array_equal(glob, single.global_field(f)), f
+
+
+def test_xgmi_multiprocess_one_gpu_march():
+    """Two processes sharing one GPU, both marching (64 x 4): each rank's remote
+    ghosts arrive through the other's stores into its ring; the assembled state
+    equals the one-rank march bit for bit."""
+    N, t, world, steps = 24, 2, 2, 8
+    out = tempfile.mkdtemp()
+    mp.spawn(_worker, args=(world, _free_port(), N, t, steps, out, (64, 4)), nprocs=world, join=True)
+    g = CubedSphereGrid(N)
+    single = Engine(ShallowWater("tc5"), TileLayout(N, t, 1, ng=2), grid=g, device="cuda", backend="hip", dt=200.0,
+                    block=(64, 4))
     single.step(steps)
     L = TileLayout(N, t, world, ng=2)
     for f in range(4):
