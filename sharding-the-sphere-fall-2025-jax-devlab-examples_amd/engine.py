@@ -40,7 +40,7 @@ class TorchCompute:
         phys = e.physics
         Q = e.pool[st.Q]
         g = phys.halo
-        qe = extend(Q, recv, e.gmap, e.plan.T, e.plan.n, g)
+        qe = extend(Q, recv, e.gmap, e.plan.T, e.plan.n, g, cmap=e.cmap)
         Qi = e.interior(Q)
         Xi = e.interior(e.pool[st.X])
         dq = phys.rhs(qe, Qi, e.tens, e.plan.n, g)
@@ -76,6 +76,7 @@ class Engine:
         self.geo = RankGeometry(self.grid, layout, rank)
         self.tens: Dict[str, torch.Tensor] = physics.setup(self.geo, dtype, self.device)
         self.gmap = torch.as_tensor(self.plan.ghost_map, device=self.device)
+        self.cmap = torch.as_tensor(self.plan.corner_map, device=self.device)
         self.integ: Integrator = get_integrator(integrator)
         F, S = physics.F, self.plan.S
         # padded storage, zero-initialised (corner ghost blocks are never written
@@ -123,8 +124,9 @@ class Engine:
         return self.interior(self.state if q is None else q)
 
     def corner_slots(self) -> torch.Tensor:
-        """Flat padded-storage indices of the tile-corner ghost blocks (both
-        coordinates outside the tile).  No exchange writes them: at a cube
+        """Flat padded-storage indices of the tile-corner ghost slots (both
+        coordinates outside the tile) that no exchange writes: all but the
+        carried panel-edge strip ends (``RankPlan.corner_map``).  At a cube
         corner three panels meet and the block has no single source.  The
         dimension-split stencils never read them (x-sweeps read ghost
         columns of the tile's own rows, y-sweeps ghost rows of its own
@@ -135,7 +137,15 @@ class Engine:
         out = (c < mg) | (c >= n + mg)
         m2 = out[:, None] & out[None, :]
         idx = torch.nonzero(m2.reshape(-1)).reshape(-1)
-        return (torch.arange(T)[:, None] * pw * pw + idx[None, :]).reshape(-1).to(self.device)
+        allc = (torch.arange(T)[:, None] * pw * pw + idx[None, :]).reshape(-1)
+        from .parallel.layout import corner_xy
+        cm = self.plan.corner_carried
+        if cm.any():
+            t, q, a, b = np.nonzero(cm)
+            x, y = corner_xy(q, a, b, n)
+            carried = torch.as_tensor((t * pw + y + mg) * pw + x + mg)
+            allc = allc[~torch.isin(allc, carried)]
+        return allc.to(self.device)
 
     def poison_corners(self) -> None:
         """Fill every corner ghost slot of every buffer with NaN: a stencil

@@ -61,10 +61,16 @@ def panel_edge_tables(N: int, layout: TileLayout, tiles, layers: int):
     """Linear interpolation tables along the ghost strips that lie on panel
     edges: for tile side s (W, E, S, N), ghost layer k and strip cell j,
     the interpolated ghost is  x[b] + t (x[b+1] - x[b])  over the raw strip x
-    of that layer (tile-local b in [0, n-2]: the stencil never leaves the
-    tile's own strip, so no corner ghost is read and both panels of an edge use
-    the same stencil).  Returns (base [T,4,layers,n] int32, t [T,4,layers,n])."""
-    n = layout.n
+    of that layer.  The pair is chosen on the whole panel edge (global
+    b in [0, N-2]), so both panels of an edge use the same stencil and the
+    result does not depend on the decomposition.  Tile-local b can leave
+    [0, n-2] by up to k + 1 cells (the pull toward the edge middle, k + 1/2
+    cells at most); x[-1], x[-2], ... and x[n], x[n+1], ... are then the strip
+    cells beyond the tile ends, the carried corner ghosts
+    (parallel/layout.py::corner_sources).  At a cube corner the target is
+    pulled into the strip, so no pair crosses it.
+    Returns (base [T,4,layers,n] int32, t [T,4,layers,n])."""
+    n, N = layout.n, layout.N
     T = len(tiles)
     base = np.zeros((T, 4, layers, n), dtype=np.int32)
     frac = np.zeros((T, 4, layers, n))
@@ -73,9 +79,9 @@ def panel_edge_tables(N: int, layout: TileLayout, tiles, layers: int):
         for side in range(4):
             o = J0 if side < 2 else I0
             for k in range(layers):
-                u = panel_edge_target(N, o + np.arange(n), k) - o
-                b = np.clip(np.floor(u).astype(np.int64), 0, max(n - 2, 0))
-                base[li, side, k] = b
+                u = panel_edge_target(N, o + np.arange(n), k)
+                b = np.clip(np.floor(u).astype(np.int64), 0, max(N - 2, 0))
+                base[li, side, k] = b - o
                 frac[li, side, k] = u - b
     return base, frac
 
@@ -183,29 +189,44 @@ class RankGeometry:
 # Torch reference helpers
 # ----------------------------------------------------------------------------
 
+def _pull(q: torch.Tensor, recv: Optional[torch.Tensor], m: torch.Tensor) -> torch.Tensor:
+    """Values [F, *m.shape] of ghost-map codes m (>= 0: padded offset in q,
+    < 0: receive slot -1 - m)."""
+    vals = q[:, m.clamp(min=0)]
+    if recv is not None and recv.numel() > 0:
+        rv = recv[(-1 - m).clamp(min=0)]
+        vals = torch.where((m >= 0).unsqueeze(0), vals, rv.movedim(-1, 0))
+    return vals
+
+
 def extend(q: torch.Tensor, recv: Optional[torch.Tensor], gmap: torch.Tensor, T: int, n: int, g: int,
-           ng: Optional[int] = None) -> torch.Tensor:
+           ng: Optional[int] = None, cmap: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Padded state q [F, T*P*P] (P = n + 2 ng) + recv [R, F] -> extended
     window [F, T, n+2g, n+2g] with every ghost strip gathered through the ghost
-    map (pull).  Corner blocks are whatever the storage holds (never read by the
-    dimension-split stencils).  ``gmap`` is [T, 4, ng, n]; its first g layers
-    are used."""
+    map (pull).  ``gmap`` is [T, 4, ng, n]; its first g layers are used.
+    Corner blocks: the carried corner ghosts (panel-edge strip ends,
+    ``RankPlan.corner_map`` [T, 4, ng, ng]) are gathered the same way; the rest
+    is whatever the storage holds (never read by the dimension-split
+    stencils)."""
     F = q.shape[0]
     ng = gmap.shape[2] if ng is None else ng
     P = n + 2 * ng
     o = ng - g
     qe = q.view(F, T, P, P)[:, :, o:o + n + 2 * g, o:o + n + 2 * g].clone()
-    gm = gmap[:, :, :g, :].long()
-    loc = gm >= 0
-    vals = q[:, gm.clamp(min=0)]                               # [F,T,4,g,n]
-    if recv is not None and recv.numel() > 0:
-        rv = recv[(-1 - gm).clamp(min=0)].permute(4, 0, 1, 2, 3)  # [F,T,4,g,n]
-        vals = torch.where(loc.unsqueeze(0), vals, rv)
+    vals = _pull(q, recv, gmap[:, :, :g, :].long())               # [F,T,4,g,n]
     for k in range(g):
         qe[:, :, g:g + n, g - 1 - k] = vals[:, :, 0, k, :]
         qe[:, :, g:g + n, g + n + k] = vals[:, :, 1, k, :]
         qe[:, :, g - 1 - k, g:g + n] = vals[:, :, 2, k, :]
         qe[:, :, g + n + k, g:g + n] = vals[:, :, 3, k, :]
+    if cmap is not None:
+        cv = _pull(q, recv, cmap[:, :, :g, :g].long())             # [F,T,4,g,g] (quad, a, b)
+        for quad in range(4):
+            # rows a beyond the corner (S: down, N: up), columns b (W: left, E: right)
+            ys = [g - 1 - a if not quad & 2 else g + n + a for a in range(g)]
+            xs = [g - 1 - b if not quad & 1 else g + n + b for b in range(g)]
+            for a in range(g):
+                qe[:, :, ys[a], xs] = cv[:, :, quad, a, :]
     return qe
 
 
@@ -312,20 +333,35 @@ def _strip(w: torch.Tensor, side: int, k: int, g: int, n: int) -> torch.Tensor:
     return w[..., g + n + k, g:g + n]
 
 
-def _own(w: torch.Tensor, side: int, k: int, g: int, n: int) -> torch.Tensor:
-    """The tile's own cells at depth k from side (k = 0: the edge cells)."""
+def _strip_ext(w: torch.Tensor, side: int, k: int, g: int, n: int) -> torch.Tensor:
+    """Ghost layer k of a side over the whole window, [..., T, n + 2g]: along
+    positions -g .. n+g-1 (the ends are corner ghosts, carried on panel
+    edges)."""
     if side == 0:
-        return w[..., g:g + n, g + k]
+        return w[..., :, g - 1 - k]
     if side == 1:
-        return w[..., g:g + n, g + n - 1 - k]
+        return w[..., :, g + n + k]
     if side == 2:
-        return w[..., g + k, g:g + n]
-    return w[..., g + n - 1 - k, g:g + n]
+        return w[..., g - 1 - k, :]
+    return w[..., g + n + k, :]
+
+
+def _own_ext(w: torch.Tensor, side: int, k: int, g: int, n: int) -> torch.Tensor:
+    """The cells at depth k from side (k = 0: the edge cells) over the whole
+    window, along positions -g .. n+g-1 (the ends are the neighbouring tiles'
+    ghosts), [..., T, n + 2g]."""
+    if side == 0:
+        return w[..., :, g + k]
+    if side == 1:
+        return w[..., :, g + n - 1 - k]
+    if side == 2:
+        return w[..., g + k, :]
+    return w[..., g + n - 1 - k, :]
 
 
 def _interp(x: torch.Tensor, b: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
-    """x [..., T, n]; b, t [T, n]: x[b] + t (x[b+1] - x[b]) along the last axis."""
-    idx = b.long().expand(x.shape)
+    """x [..., T, m]; b, t [T, n]: x[b] + t (x[b+1] - x[b]) along the last axis."""
+    idx = b.long().expand(x.shape[:-1] + b.shape[-1:])
     x0 = x.gather(-1, idx)
     x1 = x.gather(-1, idx + 1)
     return x0 + t * (x1 - x0)
@@ -388,11 +424,13 @@ def reconstruct(w: torch.Tensor, tens: Dict[str, torch.Tensor], g: int, n: int, 
         mk = m[:, None]
         gp, raw = [], []
         for k in range(g):
-            b, t = base[:, side, k], frac[:, side, k]
+            # pair (b, b + 1), tile-local b >= -g: index b + g of the whole
+            # window line
+            b, t = base[:, side, k] + g, frac[:, side, k]
             x = _strip(w, side, k, g, n)
             raw.append(x)
-            _strip(wi, side, k, g, n).copy_(torch.where(mk, _interp(x, b, t), x))
-            gp.append(_interp(_own(w, side, k, g, n), b, t))
+            _strip(wi, side, k, g, n).copy_(torch.where(mk, _interp(_strip_ext(w, side, k, g, n), b, t), x))
+            gp.append(_interp(_own_ext(w, side, k, g, n), b, t))
         line = torch.stack(gp[::-1] + raw, -1)              # [F,T,n,2g]
         faces[side] = (m, _inner_face(line, lim), raw[0])
     xL, xR = plr_x(wi, g, n, lim)

@@ -145,6 +145,7 @@ struct FArgs {
   const T* cgf;
   const int* ccnt;
   const int* push;
+  const int* cpush;
   int G, C, nblocks, n, N, S, mg, pw;
   int links[6];           // per face: 4 x (nbr face | nbr edge << 3 | reversed << 5), sides W E S N (6 bits each)
   int local_src;          // 1: one rank holding every tile in id order -> window sources computed, no table
@@ -800,6 +801,11 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       if (x >= n - mg) pt[1] = pm[(1 * mg + (n - 1 - x)) * n + y];
       if (y < mg) pt[2] = pm[(2 * mg + y) * n + x];
       if (y >= n - mg) pt[3] = pm[(3 * mg + (n - 1 - y)) * n + x];
+      if (a.cpush && (x < mg || x >= n - mg) && (y < mg || y >= n - mg)) {   // carried corner ghost
+        const int qx = x < mg ? 0 : 1, qy = y < mg ? 0 : 1;
+        const int c = a.cpush[((tile * 4 + (qx | (qy << 1))) * mg + (qy ? n - 1 - y : y)) * mg + (qx ? n - 1 - x : x)];
+        if (c != -1) pt[qx ^ 1] = c;
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if (pt[k] >= 0) {
@@ -861,7 +867,7 @@ int launch_fused(const FusedDesc* d, hipStream_t s) {
   if (!a.len || !a.nrm || !a.tane || !a.crec || !a.lxt) return -4;
   a.code = (const unsigned long long*)d->code; a.gtab = d->gtab;
   a.gw = (const T*)d->gw;
-  a.ctab = d->ctab; a.cgf = (const T*)d->cgf; a.ccnt = d->ccnt; a.push = d->push;
+  a.ctab = d->ctab; a.cgf = (const T*)d->cgf; a.ccnt = d->ccnt; a.push = d->push; a.cpush = d->cpush;
   a.G = d->G; a.C = d->C; a.nblocks = d->nblocks; a.n = d->n; a.N = d->N; a.S = d->S; a.mg = d->mg; a.pw = d->pw;
   for (int k = 0; k < 4; ++k) {
     a.a0[k] = (T)d->a0[k]; a.a1[k] = (T)d->a1[k]; a.a2[k] = (T)d->a2[k];

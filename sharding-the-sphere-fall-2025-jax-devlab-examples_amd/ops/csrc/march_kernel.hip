@@ -132,11 +132,17 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   auto ldc = [&](int cx, int y, T (&q)[4]) {
     if constexpr (XG) {
       const bool gx = (unsigned)cx >= (unsigned)n, gy = (unsigned)y >= (unsigned)n;
-      if (gx != gy) {                              // an edge ghost (corners are never remote)
-        const int side = gx ? (cx < 0 ? 0 : 1) : (y < 0 ? 2 : 3);
-        const int layer = gx ? (cx < 0 ? -1 - cx : cx - n) : (y < 0 ? -1 - y : y - n);
-        const int pos = gx ? y : cx;
-        const int m = layer < mg ? a.gmap[((tile * 4 + side) * mg + layer) * n + pos] : 0;
+      if (gx || gy) {                              // an edge ghost, or a tile-corner ghost (carried ones may be remote)
+        int m = 0;
+        if (gx != gy) {
+          const int side = gx ? (cx < 0 ? 0 : 1) : (y < 0 ? 2 : 3);
+          const int layer = gx ? (cx < 0 ? -1 - cx : cx - n) : (y < 0 ? -1 - y : y - n);
+          const int pos = gx ? y : cx;
+          if (layer < mg) m = a.gmap[((tile * 4 + side) * mg + layer) * n + pos];
+        } else if (a.cgmap) {
+          const int ca = y < 0 ? -1 - y : y - n, cb = cx < 0 ? -1 - cx : cx - n;
+          if (ca < mg && cb < mg) m = a.cgmap[((tile * 4 + (cx >= n ? 1 : 0) + (y >= n ? 2 : 0)) * mg + ca) * mg + cb];
+        }
         if (m < 0) {                               // remote slot -1 - m: spin on its granules
           constexpr int G = sizeof(T) / 4;
           const gu64* rp = ((const gu64*)(a.recv)) + (long)(xe % STSP_XG_SLOTS) * a.ring + (long)(-1 - m) * (4 * G);
@@ -487,6 +493,11 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
       if (x >= n - mg) pt[1] = pm[(1 * mg + (n - 1 - x)) * n + j];
       if (j < mg) pt[2] = pm[(2 * mg + j) * n + x];
       if (j >= n - mg) pt[3] = pm[(3 * mg + (n - 1 - j)) * n + x];
+      if (a.cpush && (x < mg || x >= n - mg) && (j < mg || j >= n - mg)) {   // carried corner ghost (block kernel)
+        const int qx = x < mg ? 0 : 1, qy = j < mg ? 0 : 1;
+        const int v = a.cpush[((tile * 4 + (qx | (qy << 1))) * mg + (qy ? n - 1 - j : j)) * mg + (qx ? n - 1 - x : x)];
+        if (v != -1) pt[qx ^ 1] = v;
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if (pt[k] >= 0) {

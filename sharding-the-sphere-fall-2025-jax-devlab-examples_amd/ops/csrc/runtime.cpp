@@ -84,6 +84,11 @@ const RcclApi* rccl_api() {
   return &g_rccl;
 }
 
+// sizes of the C ABI descriptors, checked against the ctypes mirrors (ops/native.py)
+extern "C" int stsp_desc_size(int which) {
+  return which == 0 ? (int)sizeof(StageDesc) : which == 1 ? (int)sizeof(FusedDesc) : -1;
+}
+
 extern "C" int stsp_rccl_version(void) {
   const RcclApi* r = rccl_api();
   return r ? r->version : -1;

@@ -346,6 +346,8 @@ struct Args {
   const T* bpad;
   int Nf;
   unsigned long long frames;   // 9 bits per panel (ops/fused.py::frame_code)
+  const int* cgmap;            // carried corner ghosts (stsp_kernels.h)
+  const int* cpush;
 };
 
 #ifdef STSP_STAMPS
@@ -498,6 +500,8 @@ Args<T> make_args(const StageDesc* d) {
   a.lxt = (const T*)d->lxt;
   a.bpad = (const T*)d->bpad;
   a.Nf = d->Nf;
+  a.cgmap = d->cgmap;
+  a.cpush = d->cpush;
   a.frames = 0;
   for (int k = 0; k < 6; ++k) a.frames |= (unsigned long long)(d->frames[k] & 511) << (9 * k);
   return a;

@@ -210,6 +210,10 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
         else if (y < 0) { side = 2; layer = -1 - y; pos = x; }
         else { side = 3; layer = y - n; pos = x; }
         wgm = a.gmap[((tile * 4 + side) * mg + layer) * n + pos];
+      } else if (x < n + NG && y < n + NG && oxx && a.cgmap) {   // a tile-corner ghost: carried ones may be remote
+        const int ca = y < 0 ? -1 - y : y - n, cb = x < 0 ? -1 - x : x - n;
+        if (ca < mg && cb < mg)
+          wgm = a.cgmap[(((tile * 4 + (x >= n ? 1 : 0) + (y >= n ? 2 : 0)) * mg + ca) * mg + cb)];
       }
     }
   }
@@ -259,6 +263,14 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
     if (cx >= n - mg) pt[1] = *o32(pm, (unsigned)((1 * mg + (n - 1 - cx)) * n + cy));
     if (cy < mg) pt[2] = *o32(pm, (unsigned)((2 * mg + cy) * n + cx));
     if (cy >= n - mg) pt[3] = *o32(pm, (unsigned)((3 * mg + (n - 1 - cy)) * n + cx));
+    // a cell of a tile-corner block may also feed a carried corner ghost
+    // (layout: only when n >= 2 mg, so its x push on the far side is unused)
+    if (a.cpush && (cx < mg || cx >= n - mg) && (cy < mg || cy >= n - mg)) {
+      const int qx = cx < mg ? 0 : 1, qy = cy < mg ? 0 : 1;
+      const int cb = qx ? n - 1 - cx : cx, ca = qy ? n - 1 - cy : cy;
+      const int v = *o32(a.cpush, (unsigned)(((tile * 4 + (qx | (qy << 1))) * mg + ca) * mg + cb));
+      if (v != -1) pt[qx ^ 1] = v;
+    }
   }
   // edge normals of this block's columns / rows: into a register now, into LDS
   // only after the window loads are issued (an LDS store of a global load makes
@@ -466,11 +478,15 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
       if (bsides && !own && !pew) {  // a raw panel-edge ghost the fix-up interpolates from
         const int x = x0 + wlx - NG, y = y0 + wly - NG;
         const bool inx = (x >= 0) & (x < n), iny = (y >= 0) & (y < n);
+        // strip cells, and the tile-corner cells beyond the strip ends (carried
+        // corner ghosts, read by the interpolation pairs of the end cells):
+        // filed under the side that is a panel edge
         int side = -1, k = 0, al = 0;
-        if (iny && x < 0) { side = 0; k = -1 - x; al = wly; }
-        else if (iny && x >= n) { side = 1; k = x - n; al = wly; }
-        else if (inx && y < 0) { side = 2; k = -1 - y; al = wlx; }
-        else if (inx && y >= n) { side = 3; k = y - n; al = wlx; }
+        if (!inx) {
+          side = x < 0 ? 0 : 1; k = x < 0 ? -1 - x : x - n; al = wly;
+          if (!(k < KG && ((bsides >> side) & 1))) side = -1;
+        }
+        if (side < 0 && !iny) { side = y < 0 ? 2 : 3; k = y < 0 ? -1 - y : y - n; al = wlx; }
         if (side >= 0 && k < KG && ((bsides >> side) & 1)) {
 #pragma unroll
           for (int f = 0; f < F; ++f) s_raw[side][k][f][al] = s_w[f][wly][wlx];   // primitives, as put() stored them

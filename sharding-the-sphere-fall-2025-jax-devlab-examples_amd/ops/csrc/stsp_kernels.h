@@ -68,6 +68,13 @@ typedef struct StageDesc {
   const void* bpad;     // [S] topography in the padded layout, ghost ring filled (null: no topography)
   int Nf;               // cells per panel edge
   int frames[6];        // ops/fused.py::frame_code of each panel
+  // carried tile-corner ghosts (parallel/layout.py::corner_sources): the strip
+  // cells beyond a tile end that the panel-edge interpolation pairs reach.
+  // Corner (quad, a, b): quad = (x side E) | 2 (y side N), a rows and b columns
+  // beyond the tile corner.
+  const int* cgmap;     // [T][4][mg][mg] RankPlan.corner_map: remote slot -1 - m where < 0, else read as stored
+  const int* cpush;     // [T][4][mg][mg] slot fed by the own cell of corner block (quad, a, b): >= 0 same
+                        // rank, < -1 remote code (as push), -1 none (nullable)
 } StageDesc;
 
 int stsp_stage_launch(int phys, int dtype, int bx, int by, const StageDesc* d, hipStream_t stream);
@@ -136,6 +143,7 @@ typedef struct FusedDesc {
   int nsteps;
   const int* prod;
   int PM;
+  const int* cpush;     // [T][4][mg][mg] carried corner ghost pushes (StageDesc::cpush), nullable
 } FusedDesc;
 int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stream);
 int stsp_fused_limits(int* gmax, int* cmax);

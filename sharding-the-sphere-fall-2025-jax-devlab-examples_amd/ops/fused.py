@@ -993,6 +993,7 @@ class FusedKernel:
             "code": t(code.view(np.int64), torch.int64), "gtab": t(gpair, torch.int32), "gw": t(P.gt),
             "ctab": t(ct, torch.int32), "cgf": t(cgw), "ccnt": t(P.ccnt, torch.int32),
             "push": torch.as_tensor(e.plan.push_map, dtype=torch.int32, device=dev).contiguous(),
+            "cpush": torch.as_tensor(e.plan.corner_push, dtype=torch.int32, device=dev).contiguous(),
         }
         rec_g = global_cell_records(e)
         self.tens["gbt"] = None
@@ -1011,7 +1012,7 @@ class FusedKernel:
                 rg[:, :3] = rec_g[X.need_remote[e.rank], 4:7]
                 gbn = np.concatenate([gbn, rg], 0)
             self.tens["gbt"] = t(gbn)
-        assert int(e.plan.push_map.max(initial=-1)) < S
+        assert int(e.plan.push_map.max(initial=-1)) < S and int(e.plan.corner_push.max(initial=-1)) < S
         self.dcode = native.dtype_code(dt)
         self.mem = None
         # per-block step counters (xGMI tags; waits inside a multi-step launch)
@@ -1062,7 +1063,7 @@ class FusedKernel:
         d = native.FusedDesc()
         d.Q, d.out = p(e.pool[qi]), p(e.pool[oi])
         for k in ("len", "nrm", "tane", "crec", "lxt", "src", "org", "code", "gtab", "gw", "ctab", "cgf",
-                  "ccnt", "push"):
+                  "ccnt", "push", "cpush"):
             setattr(d, k, p(tn[k]))
         d.gbt = p(tn["gbt"]) if tn["gbt"] is not None else 0
         for f in range(6):

@@ -214,7 +214,9 @@ class HipCompute:
         if "pe_base" in t:      # panel-edge ghost interpolation tables (models/base.py)
             assert t["pe_base"].dtype == torch.int32 and t["pe_base"].shape == (T, 4, 3, n)
             assert t["pe_t"].dtype == e.dtype and t["pe_t"].shape == (T, 4, 3, n)
-            assert int(t["pe_base"].min()) >= 0 and int(t["pe_base"].max()) <= max(n - 2, 0)
+            # pairs chosen on the whole panel edge: tile-local b leaves [0, n-2] by
+            # up to layer + 1 cells, into the carried corner ghosts (models/base.py)
+            assert int(t["pe_base"].min()) >= -3 and int(t["pe_base"].max()) <= n + 1
             # the kernel reads the interpolation pair (b, b + 1) of ghost layer k < KG
             # from the block's window: -NG <= b - j <= NG - 1 for strip cell j
             # (PLR: NG = 2, one layer; PPM: NG = 3, two layers)
@@ -230,6 +232,13 @@ class HipCompute:
         pm = plan.push_map
         assert pm.shape == (T, 4, plan.ng, n) and pm.max(initial=-1) < S
         self.push = torch.as_tensor(pm, dtype=torch.int32, device=e.device)
+        # carried tile-corner ghosts: pushed by their own table, remote ones read through corner_map
+        cpm, cgm = plan.corner_push, plan.corner_map
+        assert cpm.shape == cgm.shape == (T, 4, plan.ng, plan.ng) and cpm.max(initial=-1) < S and cgm.max() < S
+        assert plan.corner_carried.sum() == 0 or n >= 2 * plan.ng
+        assert (-1 - cgm[cgm < 0]).max(initial=-1) < plan.num_recv
+        self.cpush = torch.as_tensor(cpm, dtype=torch.int32, device=e.device)
+        self.cgmap = torch.as_tensor(cgm, dtype=torch.int32, device=e.device)
         recv = e.transport.recv
         assert recv.shape == (plan.num_recv, F)
         gm = plan.ghost_map
@@ -289,6 +298,8 @@ class HipCompute:
         d.recv = p(e.transport.recv) if e.transport.recv.numel() else 0
         d.gmap = p(e.gmap)
         d.push = p(self.push)
+        d.cpush = p(self.cpush)
+        d.cgmap = p(self.cgmap)
         d.blocks = p(blocks) if blocks is not None else 0
         d.invA = p(t["invA"])
         d.ex = p(t["ex"])

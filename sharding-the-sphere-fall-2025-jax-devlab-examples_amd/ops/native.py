@@ -43,6 +43,8 @@ class StageDesc(ctypes.Structure):
         # streaming stage (march_kernel.hip)
         ("torg", ctypes.c_void_p), ("crec", ctypes.c_void_p), ("lxt", ctypes.c_void_p), ("bpad", ctypes.c_void_p),
         ("Nf", ctypes.c_int), ("frames", ctypes.c_int * 6),
+        # carried tile-corner ghosts (parallel/layout.py::corner_sources)
+        ("cgmap", ctypes.c_void_p), ("cpush", ctypes.c_void_p),
     ]
 
 
@@ -65,6 +67,7 @@ class FusedDesc(ctypes.Structure):
         ("timeout_ticks", ctypes.c_longlong), ("stamps", ctypes.c_void_p),
         ("local_src", ctypes.c_int), ("links", ctypes.c_int * 6),
         ("nsteps", ctypes.c_int), ("prod", ctypes.c_void_p), ("PM", ctypes.c_int),
+        ("cpush", ctypes.c_void_p),
     ]
 
 
@@ -102,6 +105,12 @@ def load(build_if_missing: bool = True):
         L.stsp_fused_limits.restype = ci
         _declare_runtime(L)
         _declare_tt(L)
+        L.stsp_desc_size.argtypes = [ci]
+        L.stsp_desc_size.restype = ci
+        for k, cls in enumerate((StageDesc, FusedDesc)):
+            if L.stsp_desc_size(k) != ctypes.sizeof(cls):
+                raise RuntimeError(f"{cls.__name__}: ctypes mirror is {ctypes.sizeof(cls)} bytes, "
+                                   f"the library's {L.stsp_desc_size(k)} (stale libstsp.so?)")
         _LIB = L
         return L
 

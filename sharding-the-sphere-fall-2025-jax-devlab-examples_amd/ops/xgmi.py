@@ -51,7 +51,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from ..parallel.layout import TileLayout
+from ..parallel.layout import TileLayout, corner_own_index, corner_xy
 
 CNT_BYTES = 256          # counter block at the start of each rank's allocation (<= 32 ranks)
 MAX_WORLD = 32
@@ -121,6 +121,34 @@ class XgmiPlan:
             feed_blk.append((li * self.nby + jj // by) * self.nbx + ii // bx)
             feed_peer.append(np.full(len(c), p, dtype=np.int64))
         self.push = push.astype(np.int32)
+        # carried corner ghosts of peers (parallel/layout.py::corner_sources):
+        # their own push table, with the same remote codes
+        cpush = plan.corner_push.astype(np.int64).copy()
+        for p in plan.send_peers:
+            pp_ = plans[p]
+            cs = L.corner_sources(p)
+            sel = pp_.corner_carried & (pp_.corner_map < 0)
+            if not sel.any():
+                continue
+            c = cs[sel]
+            mine = np.asarray(L.owner)[L.locate(c)[0]] == rank
+            if not mine.any():
+                continue
+            c = c[mine]
+            slot = (-1 - pp_.corner_map[sel][mine]).astype(np.int64)
+            tid2, i2, j2 = L.locate(c)
+            qo, ao, bo = corner_own_index(i2, j2, n, g)
+            li = L._local_arr[tid2]
+            code = (np.int64(p) << SLOT_BITS) | slot
+            cur = cpush[li, qo, ao, bo]
+            if not ((cur == -1) | (cur == -2 - code)).all():
+                raise AssertionError("corner push collision")
+            cpush[li, qo, ao, bo] = -2 - code
+            src_l.append(L.local_flat(c))
+            code_l.append(code)
+            feed_blk.append((li * self.nby + j2 // by) * self.nbx + i2 // bx)
+            feed_peer.append(np.full(len(c), p, dtype=np.int64))
+        self.cpush = cpush.astype(np.int32)
         if src_l:
             src = np.concatenate(src_l)
             code = np.concatenate(code_l)
@@ -142,6 +170,11 @@ class XgmiPlan:
         for p, off, cnt in zip(plan.recv_peers, plan.recv_offsets, plan.recv_counts):
             slot_peer[off:off + cnt] = p
         NG = halo
+        rcorner = plan.remote_corners()
+        cxy = []
+        for t in range(plan.T):
+            qq, aa, bb = np.nonzero(rcorner[t])
+            cxy.append(corner_xy(qq, aa, bb, n))
         for t in range(plan.T):
             for yb in range(self.nby):
                 y0 = yb * by
@@ -159,6 +192,10 @@ class XgmiPlan:
                         parts.append(gm[t, 2, :NG - y0, cols])
                     if y0 + by + NG > n:
                         parts.append(gm[t, 3, :min(NG, y0 + by + NG - n), cols])
+                    cm = plan.corner_map[t][rcorner[t]]
+                    cx, cy = cxy[t]
+                    inw = (cx >= x0 - NG) & (cx < x0 + bx + NG) & (cy >= y0 - NG) & (cy < y0 + by + NG)
+                    parts.append(cm[inw])
                     for q in parts:
                         r = q[q < 0]
                         for p in np.unique(slot_peer[-1 - r]):
@@ -169,9 +206,10 @@ class XgmiPlan:
         # producer blocks of each peer that feed this rank (cells of my ghosts, all layers)
         self.nprod = np.zeros(MAX_WORLD, dtype=np.int64)
         gs = L.ghost_sources(rank)
+        cs = L.corner_sources(rank)
         for p in plan.recv_peers:
             sel = gm < 0
-            c = gs[sel]
+            c = np.concatenate([gs[sel], cs[rcorner]])
             tid, i, j = L.locate(c)
             own = np.asarray(L.owner)[tid]
             c_t, c_i, c_j = tid[own == p], i[own == p], j[own == p]
@@ -231,6 +269,7 @@ class XgmiHalo:
         self.epoch = torch.zeros(hc.nblocks, dtype=torch.int32, device=dev)
         self.err = torch.zeros(4, dtype=torch.int32, device=dev)
         self.push = torch.as_tensor(self.xp.push, device=dev)
+        self.cpush = torch.as_tensor(self.xp.cpush, device=dev)
         self.prime_src = torch.as_tensor(self.xp.prime_src, device=dev)
         self.prime_code = torch.as_tensor(self.xp.prime_code, device=dev)
         assert int(self.xp.push.max(initial=-1)) < e.plan.S
@@ -269,6 +308,7 @@ class XgmiHalo:
         d.ring = self.ring
         d.recv = self.base + CNT_BYTES
         d.push = native.ptr(self.push)
+        d.cpush = native.ptr(self.cpush)
         d.peer_ring = native.ptr(self.peer_ring)
         d.peer_cnt = native.ptr(self.peer_cnt)
         d.cnt = self.base

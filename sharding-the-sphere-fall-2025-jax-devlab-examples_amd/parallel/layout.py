@@ -57,6 +57,27 @@ def ghost_xy(side: int, layer: int, pos: np.ndarray, n: int):
     return pos, np.full_like(pos, n + layer)
 
 
+def corner_xy(quad, a, b, n: int):
+    """Tile-extended coordinates of corner ghost (quad, a, b): quadrant
+    quad = (x side E) | 2 (y side N) (0 SW, 1 SE, 2 NW, 3 NE), a rows and b
+    columns beyond the tile corner."""
+    quad, a, b = np.asarray(quad), np.asarray(a), np.asarray(b)
+    x = np.where(quad & 1, n + b, -1 - b)
+    y = np.where(quad & 2, n + a, -1 - a)
+    return x, y
+
+
+def corner_own_index(i: np.ndarray, j: np.ndarray, n: int, g: int):
+    """Own cell (i, j) inside a g x g tile-corner block -> (quad, a, b), the
+    index of the corner push table (the kernels' rule: W / S when the cell is
+    within g of both ends, which the layout excludes for carried corners)."""
+    qx = np.where(i < g, 0, 1)
+    qy = np.where(j < g, 0, 1)
+    b = np.where(qx == 0, i, n - 1 - i)
+    a = np.where(qy == 0, j, n - 1 - j)
+    return qx | (qy << 1), a, b
+
+
 class TileLayout:
     """Global tiling of a C<N> cubed sphere into 6 t^2 tiles over `num_ranks`."""
 
@@ -143,10 +164,53 @@ class TileLayout:
         self._cache[key] = out
         return out
 
+    def corner_sources(self, rank: int) -> np.ndarray:
+        """[T, 4, ng, ng] global flat source of the *carried* tile-corner
+        ghosts (corner_xy), -1 where none is carried.
+
+        A panel-edge ghost strip is interpolated along the neighbour panel's
+        grid lines (models/base.py::panel_edge_tables), whose target points lie
+        up to (layer + 1/2) sin(2 beta) cells from the strip cell, toward the
+        middle of the panel edge.  Where a tile boundary (not a cube corner)
+        cuts the strip, the interpolation pair of the end cells reaches strip
+        cells beyond the tile: the diagonal neighbour tile's cells.  Carrying
+        them in the tile-corner ghost blocks makes the interpolation, and so
+        the state, independent of the decomposition.
+        A quadrant whose x side is a panel edge and whose y side is not (or
+        the converse) carries its whole ng x ng block: the other panel's
+        cells of ghost layers 0 .. ng-1 at the ng strip positions beyond the
+        tile end.  Quadrants at a cube corner (both sides on panel edges) and
+        inside a panel carry nothing."""
+        key = ("cs", rank)
+        if key in self._cache:
+            return self._cache[key]
+        tiles = self.rank_tiles[rank]
+        n, g, N = self.n, self.ng, self.N
+        out = np.full((len(tiles), 4, g, g), -1, dtype=np.int64)
+        for li, tid in enumerate(tiles):
+            f, I0, J0 = self.tile_origin(tid)
+            for q in range(4):
+                xe = (I0 + n == N) if q & 1 else (I0 == 0)
+                ye = (J0 + n == N) if q & 2 else (J0 == 0)
+                if xe == ye:
+                    continue
+                if n < 2 * g:
+                    raise ValueError(f"tile size n = {n} < 2 ng = {2 * g}: the panel-edge strip ends "
+                                     "of a tile boundary cannot be carried")
+                a, b = np.meshgrid(np.arange(g), np.arange(g), indexing="ij")
+                x, y = corner_xy(q, a, b, n)
+                F, I2, J2 = neighbor_cells(N, f, I0 + x, J0 + y)
+                assert (F >= 0).all()
+                out[li, q, a, b] = self.global_flat(F, I2, J2)
+        self._cache[key] = out
+        return out
+
     def needs(self, rank: int, peer: int) -> np.ndarray:
         """Ordered unique global cells owned by `peer` that `rank` reads as
-        ghosts (first-occurrence order of rank's ghost enumeration)."""
-        src = self.ghost_sources(rank).reshape(-1)
+        ghosts (first-occurrence order of rank's ghost enumeration: the edge
+        strips, then the carried corner ghosts)."""
+        cs = self.corner_sources(rank)
+        src = np.concatenate([self.ghost_sources(rank).reshape(-1), cs[cs >= 0]])
         tid, _, _ = self.locate(src)
         own = np.asarray(self.owner)[tid]
         sel = src[own == peer]
@@ -191,28 +255,45 @@ class RankPlan:
         self.P = self.n + 2 * self.ng
         self.S = self.T * self.P * self.P
         src = L.ghost_sources(self.rank)
-        tid, _, _ = L.locate(src)
-        own = np.asarray(L.owner)[tid]
-        gmap = np.empty(src.shape, dtype=np.int64)
-        local = (own == self.rank) & (not L.loopback)
+        csrc = L.corner_sources(self.rank)
+        cm = csrc >= 0
+        # edge-strip ghosts, then the carried corner ghosts (needs() order)
+        allsrc = np.concatenate([src.reshape(-1), csrc[cm]])
+        tid, _, _ = L.locate(allsrc)
+        own_all = np.asarray(L.owner)[tid]
+        codes = np.empty(allsrc.shape, dtype=np.int64)
+        local = (own_all == self.rank) & (not L.loopback)
         if local.any():
-            gmap[local] = L.local_flat(src[local])
+            codes[local] = L.local_flat(allsrc[local])
         # remote: recv slots, peers in ascending order
-        self.recv_peers: List[int] = sorted(int(p) for p in np.unique(own[~local]))
+        self.recv_peers: List[int] = sorted(int(p) for p in np.unique(own_all[~local]))
         self.recv_counts: List[int] = []
         self.recv_offsets: List[int] = []
         off = 0
         for p in self.recv_peers:
             need = L.needs(self.rank, p)
-            m = own == p
+            m = own_all == p
             sorter = np.argsort(need)
-            k = sorter[np.searchsorted(need[sorter], src[m])]
-            gmap[m] = -1 - (off + k)
+            k = sorter[np.searchsorted(need[sorter], allsrc[m])]
+            codes[m] = -1 - (off + k)
             self.recv_offsets.append(off)
             self.recv_counts.append(len(need))
             off += len(need)
         self.num_recv = off
-        self.ghost_map = gmap.astype(np.int32)
+        ns = src.size
+        self.ghost_map = codes[:ns].reshape(src.shape).astype(np.int32)
+        own = own_all[:ns].reshape(src.shape)
+        # corner_map [T, 4, ng, ng], the ghost_map convention for the tile-corner
+        # ghost blocks: a carried corner's source (padded offset or -1 - recv
+        # slot); any other corner slot names itself (the kernels read it as stored)
+        n_, g_, P_ = self.n, self.ng, self.P
+        qq, aa, bb = np.meshgrid(np.arange(4), np.arange(g_), np.arange(g_), indexing="ij")
+        cx, cy = corner_xy(qq, aa, bb, n_)
+        ident = (np.arange(self.T)[:, None, None, None] * P_ + cy[None] + g_) * P_ + cx[None] + g_
+        cmap = ident.astype(np.int64)
+        cmap[cm] = codes[ns:]
+        self.corner_map = cmap.astype(np.int32)
+        self.corner_carried = cm
         # send lists: what each peer needs from us, in the peer's order
         self.send_peers: List[int] = []
         self.send_counts: List[int] = []
@@ -268,6 +349,28 @@ class RankPlan:
                                 break
                         assert ok, "no strip feeds this ghost slot"
         self.push_map = push.astype(np.int32)
+        # corner_push [T, 4, ng, ng]: the same-rank corner ghost slot (padded
+        # offset) that own cell corner_own_index(...) feeds, or -1.  A carried
+        # corner's source cell lies in a g x g corner block of its own tile and
+        # feeds at most one carried corner (the layout asserts it).
+        cpush = np.full((T, 4, g, g), -1, dtype=np.int64)
+        cm = self.corner_carried
+        cmap = self.corner_map.astype(np.int64)
+        if not L.loopback:
+            csrc = L.corner_sources(self.rank)
+            for t, q, a, b in zip(*np.nonzero(cm & (cmap >= 0))):
+                c = csrc[t, q, a, b]
+                tid2, i2, j2 = L.locate(np.array([c]))
+                assert L.owner[int(tid2[0])] == self.rank
+                qo, ao, bo = corner_own_index(i2, j2, n, g)
+                x, y = corner_xy(q, a, b, n)
+                d = (t * P + int(y) + g) * P + int(x) + g
+                key = (int(L._local_arr[tid2[0]]), int(qo[0]), int(ao[0]), int(bo[0]))
+                assert cpush[key] in (-1, d), "corner push collision"
+                cpush[key] = d
+                hsrc.append(np.array([cmap[t, q, a, b]]))
+                hdst.append(np.array([d]))
+        self.corner_push = cpush.astype(np.int32)
         self.halo_src = (np.concatenate(hsrc) if hsrc else np.zeros(0, np.int64)).astype(np.int32)
         self.halo_dst = (np.concatenate(hdst) if hdst else np.zeros(0, np.int64)).astype(np.int32)
 
@@ -278,6 +381,10 @@ class RankPlan:
     def tile_has_remote(self) -> np.ndarray:
         """[T, 4] True where a tile side reads any remote ghost."""
         return (self.ghost_map < 0).any(axis=(2, 3))
+
+    def remote_corners(self) -> np.ndarray:
+        """[T, 4, ng, ng] True where a carried corner ghost is a remote one."""
+        return self.corner_carried & (self.corner_map < 0)
 
     def block_classes(self, bx: int, by: int) -> Tuple[np.ndarray, np.ndarray]:
         """Split the (tile, block_y, block_x) work items of a bx x by block
@@ -290,6 +397,10 @@ class RankPlan:
         nby = (n + by - 1) // by
         rem = self.ghost_map < 0  # [T,4,g,n]
         interior, boundary = [], []
+        rc = self.remote_corners()
+        cxy = {}
+        for t, q, a, b in zip(*np.nonzero(rc)):
+            cxy.setdefault(int(t), []).append(tuple(int(v) for v in corner_xy(q, a, b, n)))
         for t in range(self.T):
             for yb in range(nby):
                 y0, y1 = yb * by, min(n, (yb + 1) * by)
@@ -304,6 +415,9 @@ class RankPlan:
                         r = True
                     if y1 > n - g and rem[t, 3, : y1 - (n - g), x0:x1].any():
                         r = True
+                    for (cx, cy) in cxy.get(t, ()):
+                        if x0 - g <= cx < x1 + g and y0 - g <= cy < y1 + g:
+                            r = True
                     bid = (t * nby + yb) * nbx + xb
                     (boundary if r else interior).append(bid)
         return np.asarray(interior, dtype=np.int32), np.asarray(boundary, dtype=np.int32)

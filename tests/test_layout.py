@@ -80,7 +80,47 @@ def test_push_map_is_bijection_onto_local_ghosts(N, t, R):
         p = L.plan(r)
         pushed = p.push_map[p.push_map >= 0]
         assert len(np.unique(pushed)) == len(pushed) == (p.ghost_map >= 0).sum()
-        assert set(pushed.tolist()) == set(p.halo_dst.tolist())
+        # carried corner ghosts: pushed by their own table, once each
+        cp = p.corner_push[p.corner_push >= 0]
+        assert len(np.unique(cp)) == len(cp) == (p.corner_carried & (p.corner_map >= 0)).sum()
+        allp = np.concatenate([pushed, cp])
+        assert len(np.unique(allp)) == len(allp)
+        assert set(allp.tolist()) == set(p.halo_dst.tolist())
+
+
+@pytest.mark.parametrize("N,t,R,ng", [(12, 2, 1, 2), (24, 4, 1, 3), (24, 2, 6, 2), (24, 4, 8, 3)])
+def test_corner_ghosts_carry_the_diagonal_strip_cells(N, t, R, ng):
+    """Carried corner ghosts: exactly the quadrants with one panel-edge side,
+    each slot's source is the true neighbour-panel cell at that extended
+    position (tile_extended_index), and every remote one has a receive slot
+    whose sender packs that cell."""
+    L = TileLayout(N, t, R, ng=ng)
+    n = L.n
+    for r in range(R):
+        p = L.plan(r)
+        cs = L.corner_sources(r)
+        for li, tid in enumerate(p.tiles):
+            f, I0, J0 = L.tile_origin(tid)
+            ext = L.tile_extended_index(tid, ng)
+            for q in range(4):
+                xe = (I0 + n == N) if q & 1 else (I0 == 0)
+                ye = (J0 + n == N) if q & 2 else (J0 == 0)
+                assert p.corner_carried[li, q].all() == (xe != ye)
+                assert p.corner_carried[li, q].any() == (xe != ye)
+                for a in range(ng):
+                    for b in range(ng):
+                        x = n + b if q & 1 else -1 - b
+                        y = n + a if q & 2 else -1 - a
+                        if xe != ye:
+                            assert cs[li, q, a, b] == ext[y + ng, x + ng] >= 0
+        rc = p.remote_corners()
+        if rc.any():
+            slots = -1 - p.corner_map[rc]
+            assert (slots < p.num_recv).all()
+            for s, c in zip(slots, cs[rc]):
+                k = int(np.searchsorted(np.asarray(p.recv_offsets), s, side="right")) - 1
+                peer = p.recv_peers[k]
+                assert L.needs(r, peer)[s - p.recv_offsets[k]] == c
 
 
 def test_block_classes_partition_all_blocks():
