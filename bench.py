@@ -238,22 +238,20 @@ def main():
     if runtime == "auto":
         runtime = "native" if (device.type == "cuda" and backend == "hip") else "eager"
         if runtime == "native" and (world == 1 or a.comm in ("auto", "xgmi")):
-            from stsphere.ops.fused import fused_supported
-            probe = Engine(phys_factory(), layout, rank, grid=grid, dtype=dtype, device="cpu", integrator=a.integrator)
-            if fused_supported(probe) is None:
-                # the fused step recomputes a ring of 2 x 3 cells per block: it wins
-                # where launches and hand-offs dominate (every block resident, so
-                # several steps run per launch); larger grids keep the stage path
-                from stsphere.ops.fused import fused_block
-                cus = torch.cuda.get_device_properties(device).multi_processor_count if device.type == "cuda" else 256
-                B = fused_block(layout.n, len(layout.plan(rank).tiles), cus)
-                nb = len(layout.plan(rank).tiles) * (layout.n // B) ** 2
-                # one GPU up to two passes over the CUs: one fused launch per step still
-                # beats three stage launches (C180, 3 tiles per edge, 486 blocks: 38.6 vs
-                # 44.5 us/step, profiles/r3_march/c180_fused_b20.log)
-                if nb <= cus or (world == 1 and nb <= 2 * cus):
-                    runtime = "fused"
-            del probe
+            from stsphere.ops.fused import fused_block, fused_supported_config
+            # the fused step recomputes a ring of 2 x 3 cells per block: it wins
+            # where launches and hand-offs dominate (every block resident, so
+            # several steps run per launch); larger grids keep the stage path.
+            # One GPU up to two passes over the CUs: one fused launch per step still
+            # beats three stage launches (C180, 3 tiles per edge, 486 blocks: 38.6 vs
+            # 44.5 us/step, profiles/r3_march/c180_fused_b20.log)
+            cus = torch.cuda.get_device_properties(device).multi_processor_count if device.type == "cuda" else 256
+            ntl = len(layout.rank_tiles[rank])
+            B = fused_block(layout.n, ntl, cus)
+            nb = ntl * (layout.n // B) ** 2 if B else None
+            if nb is not None and (nb <= cus or (world == 1 and nb <= 2 * cus)) and \
+                    fused_supported_config(phys, a.integrator, layout, B) is None:
+                runtime = "fused"
     comm = a.comm if world > 1 else "none"
     if world > 1 and runtime == "fused":
         comm = "xgmi"                    # remote window cells through the fused kernel's xGMI ring

@@ -891,22 +891,28 @@ def fused_block(n: int, tiles: Optional[int] = None, cus: Optional[int] = None) 
 
 def fused_supported(engine, B: Optional[int] = None) -> Optional[str]:
     """None if ``engine`` can take the fused step, else the reason it cannot."""
-    from ..models.swe import ShallowWater
     e = engine
-    if not isinstance(e.physics, ShallowWater):
+    return fused_supported_config(e.physics, e.integ.name, e.layout, B)
+
+
+def fused_supported_config(physics, integrator: str, layout: TileLayout, B: Optional[int] = None) -> Optional[str]:
+    """``fused_supported`` from the run's configuration alone (no Engine, so no
+    geometry setup: bench.py's runtime choice)."""
+    from ..models.swe import ShallowWater
+    if not isinstance(physics, ShallowWater):
         return "fused step: shallow water only"
-    if int(e.physics.limiter) not in (0, 1, 2, 3):
+    if int(physics.limiter) not in (0, 1, 2, 3):
         return "fused step: PLR limiters only (PPM runs stage by stage)"
-    if e.integ.name != "ssprk3":
+    if integrator != "ssprk3":
         return "fused step: SSP-RK3 only"
-    if e.layout.loopback and e.layout.num_ranks > 1:
+    if layout.loopback and layout.num_ranks > 1:
         return "fused step: loopback layouts are one-rank rehearsals"
-    B = B or fused_block(e.plan.n)
-    if B is None or e.plan.n % B:
-        return f"fused step: tile size {e.plan.n} is not a multiple of {' or '.join(map(str, FUSED_BLOCKS))}"
-    if e.layout.N <= NG_PLR * 3:
-        return f"fused step: C{e.layout.N} is too small for the ring"
-    if e.plan.ng < NG_PLR:
+    B = B or fused_block(layout.n)
+    if B is None or layout.n % B:
+        return f"fused step: tile size {layout.n} is not a multiple of {' or '.join(map(str, FUSED_BLOCKS))}"
+    if layout.N <= NG_PLR * 3:
+        return f"fused step: C{layout.N} is too small for the ring"
+    if layout.ng < NG_PLR:
         return "fused step: needs a ghost ring of 2"
     return None
 
