@@ -44,7 +44,16 @@
 #include <type_traits>
 
 
+// STSP_FUSED_GINL=1: faces next to a panel-edge line evaluate their ghost
+// stencil neighbours themselves (index pair + weight from LDS); 0: a ghost pass
+// per stage writes them into the window's ghost area first (round 3)
+#ifndef STSP_FUSED_GINL
+#define STSP_FUSED_GINL 1
+#endif
+
 namespace {
+
+constexpr bool GINL = STSP_FUSED_GINL != 0;
 
 // cube-corner face table widths (ops/fused.py::corner_tables)
 constexpr int CT_INTS = 16, CT_FLAGS = 12, CG_VALS = 8;
@@ -523,11 +532,12 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     const int ib = fv * WS + fu, ia = ib - st;
     int iam = ia - st, iap = ib, ibm = ia, ibp = ib + st, ra = 0;
     bool wnear = false;                                    // some lane of this wave is near an edge line
+    int gq[4] = {-1, -1, -1, -1};                          // ghost entries at am, ap, bm, bp (GINL)
     if constexpr (EDGE) {
       const int e0 = ax ? ky0 : kx0, e1 = ax ? ky1 : kx1;
       const bool near = (unsigned)(k - e0 + 1) <= 2u || (unsigned)(k - e1 + 1) <= 2u;
       wnear = __builtin_amdgcn_ballot_w64(near) != 0;
-      if (wnear) gwait();                                  // this wave reads ghost entries
+      if (!GINL && wnear) gwait();                         // this wave reads ghost entries
       if (near) {
         const int sm = ax ? 2 : 0;                         // side index of -axis; +axis = sm + 1
         const int ci = fv * W + fu, cj = ci - (ax ? W : 1);  // window indices of b and a
@@ -535,10 +545,14 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         const int eam = ncode(ca, sm), eap = ncode(ca, sm + 1);
         const int ebm = ncode(cb, sm), ebp = ncode(cb, sm + 1);
         if (eam == -3 || ebm == -3) return;                // a cell is missing: a corner face
-        if (eam >= 0) iam = GB + eam;
-        if (eap >= 0) iap = GB + eap;
-        if (ebm >= 0) ibm = GB + ebm;
-        if (ebp >= 0) ibp = GB + ebp;
+        if constexpr (GINL) {
+          gq[0] = eam; gq[1] = eap; gq[2] = ebm; gq[3] = ebp;
+        } else {
+          if (eam >= 0) iam = GB + eam;
+          if (eap >= 0) iap = GB + eap;
+          if (ebm >= 0) ibm = GB + ebm;
+          if (ebp >= 0) ibp = GB + ebp;
+        }
       }
       ra = fregion(X0 + fu - (ax ? 0 : 1), Y0 + fv - (ax ? 1 : 0), N);
       ra = ra < 0 ? 0 : ra;                                // a missing: junk face, never read
@@ -546,18 +560,49 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     T wl[4], wr[4], cl[5], cr[5];
 #pragma unroll
     for (int f = 0; f < 5; ++f) { cl[f] = wf[f * WW + ia]; cr[f] = wf[f * WW + ib]; }
+    if constexpr (EDGE && GINL) {
+      if (wnear) {
+        // the waves with a face next to a panel-edge line evaluate their ghost
+        // stencil neighbours here, with the ghost pass's formula x0 + t (x1 - x0)
+        // (a plain neighbour is the pair (i, i) with t = 0): no ghost pass, no
+        // wait on it, one LDS round trip for the pair instead
+        const int ix[4] = {iam, iap, ibm, ibp};
+        int j0[4], j1[4];
+        T tw[4];
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const T am = wf[f * WW + iam], bp = wf[f * WW + ibp];
-      T ap = cr[f], bm = cl[f];
-      if constexpr (EDGE) {
-        if (wnear) {                                       // wave-uniform: most waves skip these loads
-          ap = wf[f * WW + iap];
-          bm = wf[f * WW + ibm];
+        for (int q = 0; q < 4; ++q) {
+          const int e = gq[q];
+          j0[q] = e >= 0 ? (int)s_gs[e][0] : ix[q];
+          j1[q] = e >= 0 ? (int)s_gs[e][1] : ix[q];
+          tw[q] = e >= 0 ? s_gt[e] : T(0);
+        }
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          T x[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const T x0 = wf[f * WW + j0[q]];
+            x[q] = x0 + tw[q] * (wf[f * WW + j1[q]] - x0);
+          }
+          wl[f] = cl[f] + half_slope<LIM>(cl[f] - x[0], x[1] - cl[f]);
+          wr[f] = cr[f] - half_slope<LIM>(cr[f] - x[2], x[3] - cr[f]);
         }
       }
-      wl[f] = cl[f] + half_slope<LIM>(cl[f] - am, ap - cl[f]);
-      wr[f] = cr[f] - half_slope<LIM>(cr[f] - bm, bp - cr[f]);
+    }
+    if (!(EDGE && GINL) || !wnear) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const T am = wf[f * WW + iam], bp = wf[f * WW + ibp];
+        T ap = cr[f], bm = cl[f];
+        if constexpr (EDGE && !GINL) {
+          if (wnear) {                                     // wave-uniform: most waves skip these loads
+            ap = wf[f * WW + iap];
+            bm = wf[f * WW + ibm];
+          }
+        }
+        wl[f] = cl[f] + half_slope<LIM>(cl[f] - am, ap - cl[f]);
+        wr[f] = cr[f] - half_slope<LIM>(cr[f] - bm, bp - cr[f]);
+      }
     }
     const T* m = &s_nrm[ax ? 1 : 0][ra][0][k];
     T fl[4];
@@ -657,7 +702,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     // count themselves done in s_gdone, and only a wave with a face next to a
     // panel-edge line (or a cube-corner face) waits for the count before its
     // first ghost read; every other wave starts its faces at once.
-    if (edge) {
+    if (!GINL && edge) {
       if (tid < a.G) {
         const int i0 = s_gs[tid][0], i1 = s_gs[tid][1];
         const T t = s_gt[tid];
