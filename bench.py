@@ -77,6 +77,8 @@ def parse(argv=None):
     ap.add_argument("--timeout", type=float, default=float(os.environ.get("STSP_BENCH_TIMEOUT", "480")),
                     help="--gpus N > 1 (self-launched): kill every rank and print a status=timeout JSON line "
                          "after this many seconds (0 = no deadline)")
+    ap.add_argument("--sync", default="spin", choices=["spin", "auto"],
+                    help="host wait mode of the GPU: spin (hipDeviceScheduleSpin) or the runtime default")
     ap.add_argument("--no-verify", action="store_true",
                     help="N > 1: skip the bitwise comparisons with a one-GPU run")
     return ap.parse_args(argv)
@@ -217,6 +219,12 @@ def main():
     # (functional check of the multi-rank paths on a one-GPU box; not a benchmark)
     share = os.environ.get("STSP_SHARE_GPU") == "1"
     cpu = a.backend == "torch" and os.environ.get("STSP_BENCH_DEVICE", "") == "cpu"
+    # host waits spin (set before torch creates the device context): the timed
+    # region ends with a synchronize, and a blocking wait adds its wake-up
+    spin_rc = None
+    if a.sync == "spin" and not cpu and a.backend == "hip" and torch.cuda.device_count() > 0:
+        from stsphere.ops import native as _native
+        spin_rc = int(_native.load(build_if_missing=False).stsp_schedule_spin(0 if share else local))
     use_gpu = (not cpu) and torch.cuda.is_available()
     device = torch.device(f"cuda:{0 if share else local}") if use_gpu else torch.device("cpu")
     if device.type == "cuda":
@@ -481,6 +489,8 @@ def main():
                 "direct_launch_steps": timed.get("direct_steps"),
                 "kernel_launches": timed.get("launches") if timed.get("direct_steps") else None,
                 "eager_steps": timed.get("eager_steps"),
+                "host_sync": a.sync if spin_rc is not None else "auto",
+                "host_sync_rc": spin_rc,
             },
             "simulated_days_per_day": sdpd,
             "finite": finite,

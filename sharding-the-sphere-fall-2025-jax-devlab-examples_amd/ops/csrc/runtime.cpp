@@ -84,6 +84,21 @@ const RcclApi* rccl_api() {
   return &g_rccl;
 }
 
+// Host wait mode of a device: spin (hipDeviceScheduleSpin) instead of the
+// runtime's default, so a synchronize returns as soon as the GPU is done
+// rather than after a yield / interrupt wake-up.  Call before the device's
+// context is created (the first HIP call on it); returns the hipError_t.
+extern "C" int stsp_schedule_spin(int device) {
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipSetDeviceFlags(hipDeviceScheduleSpin);
+}
+
+extern "C" int stsp_device_flags(void) {
+  unsigned f = 0;
+  return hipGetDeviceFlags(&f) == hipSuccess ? (int)f : -1;
+}
+
 // sizes of the C ABI descriptors, checked against the ctypes mirrors (ops/native.py)
 extern "C" int stsp_desc_size(int which) {
   return which == 0 ? (int)sizeof(StageDesc) : which == 1 ? (int)sizeof(FusedDesc) : -1;

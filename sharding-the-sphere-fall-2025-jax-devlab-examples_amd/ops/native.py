@@ -105,6 +105,10 @@ def load(build_if_missing: bool = True):
         L.stsp_fused_limits.restype = ci
         _declare_runtime(L)
         _declare_tt(L)
+        L.stsp_schedule_spin.argtypes = [ci]
+        L.stsp_schedule_spin.restype = ci
+        L.stsp_device_flags.argtypes = []
+        L.stsp_device_flags.restype = ci
         L.stsp_desc_size.argtypes = [ci]
         L.stsp_desc_size.restype = ci
         for k, cls in enumerate((StageDesc, FusedDesc)):

@@ -28,7 +28,12 @@ def main():
     ap.add_argument("--t", type=int, default=2)
     ap.add_argument("--ks", default="2,4,10,20,40,100")
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--sync", default="spin", choices=["spin", "auto"])
     a = ap.parse_args()
+    if a.sync == "spin":
+        from stsphere.ops import native
+        rc = native.load(build_if_missing=False).stsp_schedule_spin(0)
+        print("schedule_spin rc", rc, file=sys.stderr)
     from stsphere.engine import Engine
     from stsphere.models.geometry import CubedSphereGrid
     from stsphere.models.swe import ShallowWater
@@ -42,7 +47,7 @@ def main():
     eng = Engine(ShallowWater("tc5"), L, grid=CubedSphereGrid(a.N), dtype=torch.float64, device=dev, backend="hip")
     fk = FusedKernel(eng, B=fused_block(L.n, 6 * a.t * a.t, cus))
     ks = [int(k) for k in a.ks.split(",")]
-    out = {"N": a.N, "t": a.t, "B": fk.plan.B, "blocks": fk.plan.nb, "per_K": {}}
+    out = {"sync": a.sync, "N": a.N, "t": a.t, "B": fk.plan.B, "blocks": fk.plan.nb, "per_K": {}}
     runners = {}
     for k in ks:
         r = NativeStepper(eng, use_graph=True, fused=fk, steps_per_launch=k, direct=True)
