@@ -45,10 +45,13 @@
 
 
 // STSP_FUSED_GINL=1: faces next to a panel-edge line evaluate their ghost
-// stencil neighbours themselves (index pair + weight from LDS); 0: a ghost pass
-// per stage writes them into the window's ghost area first (round 3)
+// stencil neighbours themselves (index pair + weight from LDS); 0 (default): a
+// ghost pass per stage writes them into the window's ghost area first.  At
+// C96 the inline form saved ~0.9k cycles in the corner blocks' stage-1 faces
+// but cost the edge blocks ~0.7k in stage 3 (twice the LDS reads in the near
+// waves): 13.88 against 13.66 us/step (profiles/r4_b8)
 #ifndef STSP_FUSED_GINL
-#define STSP_FUSED_GINL 1
+#define STSP_FUSED_GINL 0
 #endif
 
 namespace {
@@ -497,19 +500,35 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     p[4 * WW] = tsqrt(a.g * tmax(q[0], T(0)));
   };
   auto put = [&](const T (&q)[4]) { put_at(wi, q); };
-  // tail cells (outer ring beyond NT, see FD): load and put, every step
-  auto tail = [&](const T* Qin, int xe_, bool first) {
-    if constexpr (NT < W * W) {
-      for (int idx = NT + tid - NU; tid >= NU && idx < W * W; idx += NT - NU) {
-        int tu, tv, g_, I_, J_;
-        owner_cell<NS, B>(idx, tu, tv);
-        const int ts = cell_src(tu, tv, g_, I_, J_);
-        if (first && edge) s_code[tv * W + tu] = a.code[(long)bid * W * W + tv * W + tu];
-        T q[4];
-        load_state_of(ts, q, Qin, xe_);
-        put_at(tv * WS + tu, q);
-      }
+  // tail cells (outer ring beyond NT, see FD), loaded and put every step:
+  // their window index and source are static, so they are resolved once and a
+  // step issues the tail loads together with the ring loads (one memory round
+  // trip for the threads that own both, not two in a row)
+  constexpr int NTAIL = W * W > NT ? W * W - NT : 0;
+  constexpr int TPT = NTAIL ? (NTAIL + (NT - NU) - 1) / (NT - NU) : 1;
+  int tl_wi[TPT], tl_src[TPT];
+#pragma unroll
+  for (int k = 0; k < TPT; ++k) {
+    const int idx = NT + (tid - NU) + k * (NT - NU);
+    tl_wi[k] = -1;
+    tl_src[k] = -1;
+    if (NTAIL && tid >= NU && idx < W * W) {
+      int tu, tv, g_, I_, J_;
+      owner_cell<NS, B>(idx, tu, tv);
+      tl_src[k] = cell_src(tu, tv, g_, I_, J_);
+      tl_wi[k] = tv * WS + tu;
+      if (edge) s_code[tv * W + tu] = a.code[(long)bid * W * W + tv * W + tu];
     }
+  }
+  auto tail_load = [&](const T* Qin, int xe_, T (&tq)[TPT][4]) {
+#pragma unroll
+    for (int k = 0; k < TPT; ++k)
+      if (tl_wi[k] >= 0) load_state_of(tl_src[k], tq[k], Qin, xe_);
+  };
+  auto tail_put = [&](const T (&tq)[TPT][4]) {
+#pragma unroll
+    for (int k = 0; k < TPT; ++k)
+      if (tl_wi[k] >= 0) put_at(tl_wi[k], tq[k]);
   };
   // panel-edge lines in the window (block-uniform): x-lines X = 0 (W) / X = N
   // (E), y-lines Y = 0 (S) / Y = N (N); far away when absent
@@ -655,7 +674,9 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   if (wait) {
     if (tid < B * B) enter_cell();
   } else {
-    tail(buf[0], xe, true);
+    T tq[TPT][4];
+    tail_load(buf[0], xe, tq);
+    tail_put(tq);
     enter_cell();
   }
   __syncthreads();
@@ -681,12 +702,15 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   FSTAMP(1);
   __syncthreads();
   if (wait) {
-    // this step's ring (the own cells' new state is still in Q)
+    // this step's ring (the own cells' new state is still in Q), tail cells
+    // issued first
+    T tq[TPT][4];
+    tail_load(buf[it & 1], xe, tq);
     if (tid >= B * B) {
       load_state(buf[it & 1], xe);
       enter_cell();
     }
-    tail(buf[it & 1], xe, false);
+    tail_put(tq);
     __syncthreads();
   }
   FSTAMP(2);
