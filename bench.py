@@ -79,6 +79,9 @@ def parse(argv=None):
                          "after this many seconds (0 = no deadline)")
     ap.add_argument("--sync", default="spin", choices=["spin", "auto"],
                     help="host wait mode of the GPU: spin (hipDeviceScheduleSpin) or the runtime default")
+    ap.add_argument("--repeat", type=int, default=0,
+                    help="diagnostics: time R more regions of --steps steps after the measured one "
+                         "(reported as repeat_ms_per_step; the state then has advanced further)")
     ap.add_argument("--no-verify", action="store_true",
                     help="N > 1: skip the bitwise comparisons with a one-GPU run")
     return ap.parse_args(argv)
@@ -436,6 +439,15 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # diagnostics only (--repeat R): R more timed regions of the same K steps
+    # after the measured one, reported separately (the headline is the first)
+    repeats = []
+    for _ in range(a.repeat):
+        sync()
+        t1 = time.perf_counter()
+        step(a.steps)
+        sync()
+        repeats.append(1e3 * (time.perf_counter() - t1) / a.steps)
     if hasattr(runner, "check"):
         runner.check()
     graph_path = runtime in ("native", "fused") and getattr(runner, "use_graph", False) \
@@ -500,6 +512,8 @@ def main():
             "status": "ok",
             "mass": diag.get("mass"),
         }
+        if repeats:
+            out["repeat_ms_per_step"] = repeats
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -30,8 +30,8 @@ EOF
 done
 if [ "${BENCH:-1}" = "1" ]; then
   for i in 1 2; do
-    timeout -k 10 120 python -u bench.py --steps 20 --warmup 5 > $OUT/bench_20_5_$i.log 2>&1 || exit $?
-    tail -n 1 $OUT/bench_20_5_$i.log | cut -c1-330; echo
+    timeout -k 10 120 python -u bench.py --steps 20 --warmup 5 ${BENCH_ARGS} > $OUT/bench_20_5_$i.log 2>&1 || exit $?
+    tail -n 1 $OUT/bench_20_5_$i.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print({k: d.get(k) for k in ('value','ms_per_step','repeat_ms_per_step')}, d['config'].get('host_sync'))"
   done
 fi
 echo "== done"
