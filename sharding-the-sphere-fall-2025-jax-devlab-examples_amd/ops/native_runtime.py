@@ -442,18 +442,20 @@ class NativeStepper:
             e.step_count += full
         if nsteps - full:
             if self.fused is not None:
-                # remainder: an even part in one launch, an odd last step copied back to pool[0]
+                # remainder: an odd first step copied back to pool[0], then the even
+                # part in one launch (the multi-step kernel runs last, as in the
+                # next full period)
                 cur = torch.cuda.current_stream(e.device)
                 rem = nsteps - full
+                if rem % 2:
+                    self.fused.launch(0, int(cur.cuda_stream))
+                    e.pool[0].copy_(e.pool[1])
                 if rem >= 2 and self.spl > 1:
                     self.fused.launch(0, int(cur.cuda_stream), nsteps=rem - rem % 2)
                 elif rem >= 2:
                     for _ in range(rem // 2):
                         self.fused.launch(0, int(cur.cuda_stream))
                         self.fused.launch(1, int(cur.cuda_stream))
-                if rem % 2:
-                    self.fused.launch(0, int(cur.cuda_stream))
-                    e.pool[0].copy_(e.pool[1])
                 e.time += rem * e.dt
                 e.step_count += rem
             else:
