@@ -286,6 +286,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   const int xo = ow & 0xFFF, yo = (ow >> 12) & 0xFFF, flags = (ow >> 24) & 0x1F;   // face: bits 29..31
   const bool edge = (flags & 0x1E) != 0;                 // a side region is present (block-uniform)
   const int ngw = edge ? (a.G + 63) >> 6 : 0;            // ghost waves
+  int gbase = 0;                                         // first thread of the ghost waves (set below)
   int gtarget = 0;                                       // s_gdone once this stage's entries are written
   if (tid == 0) s_gdone = 0;
   const T* wf = &s_w[0];
@@ -337,6 +338,9 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       gtv = a.gw[(long)bid * a.G + tid];
     }
     ncor = a.ccnt[bid];
+    // ghost waves: the last ones before the corner wave (see the face loop)
+    gbase = NT - 64 * (ncor > 0 ? 1 : 0) - 64 * ngw;
+    if (gbase < 0) gbase = 0;
     if (tid < ncor) {
       const int* ct = a.ctab + ((long)bid * a.C + tid) * CT_INTS;
       const T* cg = a.cgf + ((long)bid * a.C + tid) * CG_VALS;
@@ -727,32 +731,37 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     // panel-edge line (or a cube-corner face) waits for the count before its
     // first ghost read; every other wave starts its faces at once.
     if (!GINL && edge) {
-      if (tid < a.G) {
-        const int i0 = s_gs[tid][0], i1 = s_gs[tid][1];
-        const T t = s_gt[tid];
+      const int ge = tid - gbase;                            // this thread's ghost entry
+      if (ge >= 0 && ge < a.G) {
+        const int i0 = s_gs[ge][0], i1 = s_gs[ge][1];
+        const T t = s_gt[ge];
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
           const T x0 = wf[f * WW + i0], x1 = wf[f * WW + i1];
-          s_w[f * WW + GB + tid] = x0 + t * (x1 - x0);
+          s_w[f * WW + GB + ge] = x0 + t * (x1 - x0);
         }
       }
-      if (tid < ngw * 64 && (tid & 63) == 0) {
+      if (ge >= 0 && ge < ngw * 64 && (tid & 63) == 0) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's entries are in LDS
         __hip_atomic_fetch_add(&s_gdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       gtarget += ngw;
     }
-    // cube-corner faces (corner blocks only) are wave 0's tasks, alone: the
-    // oldest wave wins the issue arbitration, so their long dependency chain
-    // (two reconstructions from the codes, one flux) runs beside the regular
-    // faces instead of after them (round 3 had them on the wave after the last
-    // regular face: 4k cycles, the slowest wave of the stage-3 face phase)
-    const int c0 = ncor ? 64 : 0;
+    // Work per wave, balanced: a stage has more regular faces than threads
+    // (C96 B = 16: 784 and 840 in stages 1 and 2), so a second round of them
+    // falls on waves 0, 1, ...; the cube-corner faces (corner blocks: a long
+    // chain of two reconstructions from the host table and one flux) run
+    // alone on the last wave, and the ghost entries on the waves before it
+    // (gbase), which have one regular round.  Round 3 had all three on wave 0:
+    // 6.2k cycles in the corner blocks' stage-1 faces against 3.3k for the
+    // slowest interior wave (profiles/r4_tail).
     const int nax = s == 0 ? NOX : nx;                       // stage 1: the outer faces only
-    const int ntask = c0 + 2 * nax;
-    for (int task = tid; task < ntask; task += NT) {
-      if (task >= c0) {
-        const int tf = task - c0;
+    const bool cwave = ncor && tid >= NT - 64;
+    const int nthr = ncor ? NT - 64 : NT;
+    // corner wave: one pass with task = j - 64 < 0 (corner face j); others: regular faces
+    for (int task = cwave ? tid - NT : tid; task < (cwave ? 0 : 2 * nax); task += cwave ? 64 : nthr) {
+      if (task >= 0) {
+        const int tf = task;
         const bool ax = tf >= nax;                           // false: x-face, true: y-face
         const int t2 = ax ? tf - nax : tf;
         int fu, fv, k, p;
@@ -766,12 +775,12 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         else { fu = p; fv = k; }                             // b = (fu, k), a = (fu, k - 1)
         if (edge) face(ax, fu, fv, k, std::true_type{});
         else face(ax, fu, fv, k, std::false_type{});
-      } else if (task < ncor) {
+      } else if (task + 64 < ncor) {
         // cube-corner face j: cell c's face on side_c meets cell d's face on
         // side_d; every stencil index comes from the host table (no codes, no
         // wait for the ghost pass: an interpolated neighbour is evaluated here
         // with the ghost pass's formula, x0 + t (x1 - x0), so bit for bit)
-        const int j = task;
+        const int j = task + 64;
         const int* ct = s_ct[j];
         const int fl_ = ct[CT_FLAGS];
         T fv2[2][4], cc[2][5];
