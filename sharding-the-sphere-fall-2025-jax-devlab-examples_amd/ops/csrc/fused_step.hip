@@ -54,6 +54,10 @@
 #define STSP_FUSED_GINL 0
 #endif
 
+#ifndef STSP_FUSED_CW0
+#define STSP_FUSED_CW0 1
+#endif
+
 namespace {
 
 constexpr bool GINL = STSP_FUSED_GINL != 0;
@@ -338,8 +342,9 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       gtv = a.gw[(long)bid * a.G + tid];
     }
     ncor = a.ccnt[bid];
-    // ghost waves: the last ones before the corner wave (see the face loop)
-    gbase = NT - 64 * (ncor > 0 ? 1 : 0) - 64 * ngw;
+    // ghost waves: right after the corner wave (the last ones before it with
+    // STSP_FUSED_CW0=0; see the face loop)
+    gbase = STSP_FUSED_CW0 ? 64 * (ncor > 0 ? 1 : 0) : NT - 64 * (ncor > 0 ? 1 : 0) - 64 * ngw;
     if (gbase < 0) gbase = 0;
     if (tid < ncor) {
       const int* ct = a.ctab + ((long)bid * a.C + tid) * CT_INTS;
@@ -748,18 +753,29 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       gtarget += ngw;
     }
     // Work per wave, balanced: a stage has more regular faces than threads
-    // (C96 B = 16: 784 and 840 in stages 1 and 2), so a second round of them
-    // falls on waves 0, 1, ...; the cube-corner faces (corner blocks: a long
-    // chain of two reconstructions from the host table and one flux) run
-    // alone on the last wave, and the ghost entries on the waves before it
-    // (gbase), which have one regular round.  Round 3 had all three on wave 0:
-    // 6.2k cycles in the corner blocks' stage-1 faces against 3.3k for the
-    // slowest interior wave (profiles/r4_tail).
+    // (C96 B = 16: 784 and 840 in stages 1 and 2), so some waves take a second
+    // round of them.  The cube-corner faces (corner blocks: a long chain of two
+    // reconstructions from the host table and one flux) run alone on wave 0,
+    // the oldest (it wins the issue arbitration: on the last wave the same
+    // chain took 4.8k cycles, profiles/r4_wb), the ghost entries on the waves
+    // after it, and the second round of regular faces on the waves after
+    // those.  Round 3 had all three on wave 0: 6.2k cycles in the corner
+    // blocks' stage-1 faces against 3.3k for the slowest interior wave
+    // (profiles/r4_tail).  STSP_FUSED_CW0=0: corner faces on the last wave.
     const int nax = s == 0 ? NOX : nx;                       // stage 1: the outer faces only
+#if STSP_FUSED_CW0
+    const int cw = ncor ? 1 : 0;
+    const int nreg = NT - 64 * cw, r2 = 64 * (cw + (GINL ? 0 : ngw)), nr2 = NT - r2;
+    const bool cwave = cw && tid < 64;
+    const int tend = cwave ? 0 : 2 * nax;
+    // corner wave: one pass with task = j - 64 < 0 (corner face j); others: regular faces
+    for (int task = cwave ? tid - 64 : tid - 64 * cw, first = 1; task < tend;
+         task = first ? (tid >= r2 ? nreg + tid - r2 : tend) : task + nr2, first = 0) {
+#else
     const bool cwave = ncor && tid >= NT - 64;
     const int nthr = ncor ? NT - 64 : NT;
-    // corner wave: one pass with task = j - 64 < 0 (corner face j); others: regular faces
     for (int task = cwave ? tid - NT : tid; task < (cwave ? 0 : 2 * nax); task += cwave ? 64 : nthr) {
+#endif
       if (task >= 0) {
         const int tf = task;
         const bool ax = tf >= nax;                           // false: x-face, true: y-face
