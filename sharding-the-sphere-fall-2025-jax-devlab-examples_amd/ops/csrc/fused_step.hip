@@ -765,12 +765,12 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     const int nax = s == 0 ? NOX : nx;                       // stage 1: the outer faces only
 #if STSP_FUSED_CW0
     const int cw = ncor ? 1 : 0;
-    const int nreg = NT - 64 * cw, r2 = 64 * (cw + (GINL ? 0 : ngw)), nr2 = NT - r2;
+    const int nreg = NT - 64 * cw, t2r = 64 * (cw + (GINL ? 0 : ngw)), nr2 = NT - t2r;   // round 2 from thread t2r
     const bool cwave = cw && tid < 64;
     const int tend = cwave ? 0 : 2 * nax;
     // corner wave: one pass with task = j - 64 < 0 (corner face j); others: regular faces
     for (int task = cwave ? tid - 64 : tid - 64 * cw, first = 1; task < tend;
-         task = first ? (tid >= r2 ? nreg + tid - r2 : tend) : task + nr2, first = 0) {
+         task = first ? (tid >= t2r ? nreg + tid - t2r : tend) : task + nr2, first = 0) {
 #else
     const bool cwave = ncor && tid >= NT - 64;
     const int nthr = ncor ? NT - 64 : NT;
