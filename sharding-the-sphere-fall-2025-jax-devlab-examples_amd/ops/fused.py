@@ -943,6 +943,7 @@ class FusedKernel:
         self.e = e
         self.group = group
         self.lib = native.require_native()
+        self._launch_fn = self.lib.stsp_fused_launch
         world = e.layout.num_ranks
         self.world = world
         X = None
@@ -1030,6 +1031,7 @@ class FusedKernel:
             self._setup_exchange(X, timeout_s)
         self.descs = [self._desc(0, 1), self._desc(1, 0)]
         self._multi = {}          # nsteps -> descriptor (pool[0] -> ... -> pool[nsteps % 2])
+        self._multi_ptrs = {}     # nsteps -> (Q, out) the descriptor holds
         if X is not None:
             self.prime()
 
@@ -1111,9 +1113,13 @@ class FusedKernel:
         d = self._multi.get(nsteps)
         if d is None:
             d = self._multi[nsteps] = self._desc(0, 1, nsteps)
-        # follow the engine's current buffer order (step() swaps the pool)
-        from . import native
-        d.Q, d.out = native.ptr(self.e.pool[0]), native.ptr(self.e.pool[1])
+            self._multi_ptrs[nsteps] = (d.Q, d.out)
+        # follow the engine's current buffer order (step() swaps the pool);
+        # the ctypes fields are only written when it changed (launch path)
+        pp = (self.e.pool[0].data_ptr(), self.e.pool[1].data_ptr())
+        if pp != self._multi_ptrs[nsteps]:
+            d.Q, d.out = pp
+            self._multi_ptrs[nsteps] = pp
         return d
 
     # ---- several ranks: delivery of the current state, error check ----------
@@ -1165,10 +1171,12 @@ class FusedKernel:
         """One fused step from pool[parity] into pool[1 - parity] (the
         engine's pool list is not touched); nsteps > 1 (even, parity 0): that
         many steps in one launch, the state back in pool[0]."""
-        from . import native
         d = self.descs[parity] if nsteps == 1 else self.multi_desc(nsteps)
-        rc = self.lib.stsp_fused_launch(self.dcode, d, native.current_stream_handle() if stream is None else stream)
-        native.check(rc, "fused step")
+        if stream is None:
+            stream = int(torch.cuda.current_stream().cuda_stream)
+        rc = self._launch_fn(self.dcode, d, stream)
+        if rc:
+            raise RuntimeError(f"fused step failed with code {rc}")
 
     def step(self, nsteps: int = 1) -> None:
         """Eager fused steps on the engine (state in pool[0] afterwards)."""
