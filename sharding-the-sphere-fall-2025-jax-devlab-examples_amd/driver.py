@@ -57,6 +57,69 @@ def make_physics(pc) -> Any:
     raise ValueError(f"unknown physics model {pc.model!r}")
 
 
+class _HostQueue:
+    """Host work of the run loop, in submission order: ``append((event,
+    work))`` runs ``work()`` once ``event`` (a CUDA event, or None) has
+    completed; threaded, on one background thread, else inline at ``drain``."""
+
+    def __init__(self, threaded: bool):
+        self._items: List[Any] = []
+        self._ex = None
+        if threaded:
+            from concurrent.futures import ThreadPoolExecutor
+            self._ex = ThreadPoolExecutor(max_workers=1, thread_name_prefix="stsp-io")
+
+    def append(self, item) -> None:
+        ev, work = item
+        if self._ex is None:
+            self._items.append(item)
+            return
+
+        def job():
+            if ev is not None:
+                ev.synchronize()
+            work()
+        self._items.append(self._ex.submit(job))
+
+    def __len__(self) -> int:
+        return len(self._items)
+
+    def drain(self, block: bool = False) -> None:
+        """Finish the completed items (all of them when ``block``); a failed
+        background item raises here."""
+        while self._items:
+            it = self._items[0]
+            if self._ex is not None:
+                if not block and not it.done():
+                    return
+                self._items.pop(0).result()
+                continue
+            ev, work = it
+            if not block and ev is not None and not ev.query():
+                return
+            self._items.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            work()
+
+    def close(self) -> None:
+        self.drain(block=True)
+        if self._ex is not None:
+            self._ex.shutdown(wait=True)
+            self._ex = None
+
+    def clear(self) -> None:
+        """Drop what has not run yet (recovery); a running item completes."""
+        for it in self._items:
+            if self._ex is not None:
+                it.cancel()
+        if self._ex is not None:
+            for it in self._items:
+                if not it.cancelled():
+                    it.exception()
+        self._items = []
+
+
 class Solver:
     def __init__(self, config=None, verbose: bool = True):
         self.cfg: Config = load_config(config)
@@ -443,14 +506,14 @@ class Solver:
         cells = 6 * self.layout.N ** 2
         gpu = self.device.type == "cuda"
         deferred = gpu and self.mode != "spmd"
-        pending: List[Any] = []               # (event, host work) done while the next chunk runs
+        # (event, host work) done while the next chunks run: on a GPU by one
+        # background thread (zarr / JSONL / checkpoint writes release the GIL),
+        # so the loop keeps the launch queue full (a history frame's ~100 tile
+        # files took ~10 ms of GPU idle per frame when written in the loop)
+        pending = _HostQueue(threaded=deferred)
 
         def drain(block: bool = False) -> None:
-            while pending and (block or pending[0][0] is None or pending[0][0].query()):
-                ev, work = pending.pop(0)
-                if ev is not None:
-                    ev.synchronize()
-                work()
+            pending.drain(block)
 
         def chunk_at(p: int, step_ticks: int) -> int:
             nxt = min([(p // v + 1) * v for v in iv.values()] + [end])
@@ -512,6 +575,7 @@ class Solver:
                     drain(block=True)
                     ok = self._watchdog(pending, False)
             if not ok:
+                drain(block=True)                   # checkpoints still being written
                 saved = [s for s in ckpt.list_checkpoints(self.checkpoint_root())]
                 if recoveries < 3 and saved:
                     recoveries += 1
@@ -535,14 +599,17 @@ class Solver:
                     self._snapshot_history(hist, p // iv["history"], pending, async_copy=deferred)
             if "checkpoint" in due and p % iv["checkpoint"] == 0:
                 with ph("checkpoint"):
-                    drain(block=True)
-                    self.save_checkpoint()
+                    if deferred:
+                        self._checkpoint_async(pending)
+                    else:
+                        drain(block=True)
+                        self.save_checkpoint()
             if "metrics" in due:                 # every interval and the end of the run
                 with ph("metrics"):
                     self._snapshot_metrics(metrics, pending, deferred, cells, done, wall0, p)
         with ph("drain"):
             self._sync()
-            drain(block=True)
+            pending.close()
         wall = time.perf_counter() - wall0
         summary = {"steps": nsteps, "steps_run": done, "wall_s": wall, "setup_s": ph.times.get("setup", 0.0),
                    "sim_days": self.time / DAY,
@@ -674,6 +741,40 @@ class Solver:
             hist.write_tiles(k, e.plan.tiles, self.layout.tile_origin, e.tiles_view().detach().cpu().double().numpy())
         if self.rank == 0:
             hist.write_time(k, self.time, self.step_count)
+
+    def _checkpoint_async(self, pending: "_HostQueue") -> None:
+        """Checkpoint of the current state without stopping the GPU (single
+        process): the interior values are copied to pinned host memory on the
+        stepping stream and the background writer commits the step directory
+        once the copy is done (in order with the history frames before it)."""
+        root = self.checkpoint_root()
+        step, t, dt = self.step_count, self.time, self.dt
+        snaps = []
+        for e in self.engines:
+            v = e.tiles_view().detach()
+            h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+            h.copy_(v, non_blocking=True)
+            snaps.append((e.plan.tiles, h))
+        ev = torch.cuda.Event()
+        ev.record()
+
+        def work():
+            self._write_checkpoint(root, step, t, dt, [(tiles, h.double().numpy()) for tiles, h in snaps])
+        pending.append((ev, work))
+
+    def _write_checkpoint(self, root: str, step: int, t: float, dt: float, parts) -> str:
+        d = ckpt.step_dir(root, step)
+        meta = {"step": step, "time": t, "dt": dt, "N": self.layout.N,
+                "tiles_per_edge": self.layout.t, "num_ranks": self.layout.num_ranks,
+                "owner": self.layout.owner, "fields": self.fields, "dtype": self.cfg.grid.dtype,
+                "integrator": self.cfg.time.integrator, "physics": self.physics.name,
+                "config": self.config, "format": "stsphere-ckpt-v1"}
+        ckpt.begin(root, step, meta, self.fields, self.layout.N, self.layout.n, np.float64)
+        for tiles, arr in parts:
+            ckpt.write_tiles(d, self.fields, tiles, self.layout.tile_origin, arr, self.layout.n)
+        ckpt.commit(d)
+        ckpt.prune(root, self.cfg.io.keep_checkpoints)
+        return d
 
     # ---- checkpoint / restart ------------------------------------------------------
     def checkpoint_root(self) -> str:

@@ -213,3 +213,33 @@ def test_plot_cli_products(tmp_path):
     assert main(["plot", str(tmp_path / "history.zarr"), "h", str(out)]) == 0
     names = {p.name for p in out.rglob("*.png")}
     assert {"h_band_initial.png", "h_band_final.png", "h_six_panel.png", "h_0000.png"} <= names
+
+
+def test_host_queue_threaded_keeps_order_and_raises():
+    """Solver.run's background writer (_HostQueue): items run in submission
+    order, drain(block=True) waits for all, a failing item raises at the next
+    drain, clear() drops what has not started."""
+    import threading
+    import time
+    from stsphere.driver import _HostQueue
+    q = _HostQueue(threaded=True)
+    out = []
+    gate = threading.Event()
+    q.append((None, lambda: (gate.wait(5), out.append(1))))
+    for k in range(2, 6):
+        q.append((None, lambda k=k: out.append(k)))
+    q.drain()                 # nothing done yet: returns at once
+    assert out == []
+    gate.set()
+    q.drain(block=True)
+    assert out == [1, 2, 3, 4, 5] and len(q) == 0
+    q.append((None, lambda: 1 / 0))
+    time.sleep(0.05)
+    with pytest.raises(ZeroDivisionError):
+        q.drain(block=True)
+    q.close()
+    inline = _HostQueue(threaded=False)
+    inline.append((None, lambda: out.append(6)))
+    assert out[-1] == 5
+    inline.drain()
+    assert out[-1] == 6
