@@ -498,7 +498,7 @@ class Solver:
             if self.rank == 0:
                 os.makedirs(out, exist_ok=True)
                 HistoryWriter(hpath, self.fields, self.layout.N, self.layout.n, n_out,
-                              attrs={"config": self.config})
+                              attrs={"config": self.config}, frame_chunks=self.mode != "spmd")
             self._barrier()
             hist = HistoryWriter(hpath, self.fields, self.layout.N, self.layout.n, n_out, create=False)
         metrics = MetricsLogger(os.path.join(out, "metrics.jsonl") if "metrics" in iv else None,
@@ -651,8 +651,11 @@ class Solver:
             ev.record()
 
         def work():
-            for tiles, h in snaps:
-                hist.write_tiles(k, tiles, self.layout.tile_origin, h.double().numpy())
+            parts = [(list(tiles), h.double().numpy()) for tiles, h in snaps]
+            if hist.frame_chunks and len(parts) > 1:      # every engine of this process in one frame
+                parts = [(sum((p_[0] for p_ in parts), []), np.concatenate([p_[1] for p_ in parts], 1))]
+            for tiles, arr in parts:
+                hist.write_tiles(k, tiles, self.layout.tile_origin, arr)
             if self.rank == 0:
                 hist.write_time(k, t, sc)
         pending.append((ev, work))
@@ -737,8 +740,11 @@ class Solver:
             dist.barrier()
 
     def _write_history(self, hist: HistoryWriter, k: int) -> None:
-        for e in self.engines:
-            hist.write_tiles(k, e.plan.tiles, self.layout.tile_origin, e.tiles_view().detach().cpu().double().numpy())
+        parts = [(list(e.plan.tiles), e.tiles_view().detach().cpu().double().numpy()) for e in self.engines]
+        if hist.frame_chunks and len(parts) > 1:
+            parts = [(sum((p_[0] for p_ in parts), []), np.concatenate([p_[1] for p_ in parts], 1))]
+        for tiles, arr in parts:
+            hist.write_tiles(k, tiles, self.layout.tile_origin, arr)
         if self.rank == 0:
             hist.write_time(k, self.time, self.step_count)
 

@@ -94,14 +94,20 @@ def _chunk_key(idx: Sequence[int]) -> str:
     return ".".join(str(int(i)) for i in idx) if len(idx) else "0"
 
 
-def write_chunk(group: str, name: str, chunk_idx: Sequence[int], data: np.ndarray) -> None:
-    meta = array_meta(group, name)
+def write_chunk(group: str, name: str, chunk_idx: Sequence[int], data: np.ndarray,
+                meta: Optional[Dict[str, Any]] = None) -> None:
+    """Write one chunk (atomic rename).  ``meta``: the array's metadata when the
+    caller holds it (a writer of many chunks skips re-reading .zarray)."""
+    meta = meta or array_meta(group, name)
     chunks = tuple(meta["chunks"])
     dt = np.dtype(meta["dtype"])
-    buf = np.zeros(chunks, dtype=dt)
     data = np.asarray(data)
-    sl = tuple(slice(0, s) for s in data.shape)
-    buf[sl] = data
+    if data.shape == chunks and data.dtype == dt:
+        buf = data
+    else:
+        buf = np.zeros(chunks, dtype=dt)
+        sl = tuple(slice(0, s) for s in data.shape)
+        buf[sl] = data
     p = os.path.join(group, name, _chunk_key(chunk_idx))
     tmp = p + ".tmp"
     with open(tmp, "wb") as f:
