@@ -18,9 +18,12 @@ run_case() {  # name, kprobe args
       python3 $ROOT/tools/kprobe.py --reps 10 "$@" > $OUT/${name}_pmc$i.log 2>&1 || { echo "$name pmc $i failed"; tail -3 $OUT/${name}_pmc$i.log; return 3; }
     i=$((i+1))
   done
-  python3 $ROOT/tools/pmc_summary.py stage_kernel $OUT/$name > $OUT/${name}_summary.txt
+  python3 $ROOT/tools/pmc_summary.py ${KERNEL:-stage_kernel} $OUT/$name > $OUT/${name}_summary.txt
   echo "== $name"; cat $OUT/${name}_summary.txt
 }
-run_case c720_fp64_8x8 --N 720 --dtype fp64 --blocks 8x8 && \
-run_case c720_fp32_16x8 --N 720 --dtype fp32 --blocks 16x8 && \
-run_case c96_fp64_16x16 --N 96 --dtype fp64 --blocks 16x16
+# CASES="name:kprobe args;..." (default: the block kernel at C720 fp64 / fp32 and C96);
+# KERNEL: the kernel-name substring pmc_summary.py aggregates (march_kernel for 64xR)
+IFS=';' read -ra cases <<< "${CASES:-c720_fp64_8x8:--N 720 --dtype fp64 --blocks 8x8;c720_fp32_16x8:--N 720 --dtype fp32 --blocks 16x8;c96_fp64_16x16:--N 96 --dtype fp64 --blocks 16x16}"
+for c in "${cases[@]}"; do
+  run_case ${c%%:*} ${c#*:} || exit $?
+done
