@@ -249,14 +249,14 @@ def main():
     if runtime == "auto":
         runtime = "native" if (device.type == "cuda" and backend == "hip") else "eager"
         if runtime == "native" and (world == 1 or a.comm in ("auto", "xgmi")):
-            from stsphere.ops.fused import fused_block, fused_supported_config
+            from stsphere.ops.fused import fused_block, fused_supported_config, rank_cus
             # the fused step recomputes a ring of 2 x 3 cells per block: it wins
             # where launches and hand-offs dominate (every block resident, so
             # several steps run per launch); larger grids keep the stage path.
             # One GPU up to two passes over the CUs: one fused launch per step still
             # beats three stage launches (C180, 3 tiles per edge, 486 blocks: 38.6 vs
             # 44.5 us/step, profiles/r3_march/c180_fused_b20.log)
-            cus = torch.cuda.get_device_properties(device).multi_processor_count if device.type == "cuda" else 256
+            cus = rank_cus(device) if device.type == "cuda" else 256
             ntl = len(layout.rank_tiles[rank])
             B = fused_block(layout.n, ntl, cus)
             nb = ntl * (layout.n // B) ** 2 if B else None
@@ -312,7 +312,7 @@ def main():
             spl = a.steps_per_launch
             if spl == 0:
                 # several steps per launch (in-kernel producer waits) need every block resident
-                cus = torch.cuda.get_device_properties(device).multi_processor_count
+                cus = rank_cus(device)
                 spl = max([k for k in range(2, 65, 2) if a.steps % k == 0], default=1) if fk.plan.nb <= cus else 1
             info["steps_per_launch"] = spl
             runner = NativeStepper(eng, use_graph=True, steps_per_graph=spg, fused=fk, steps_per_launch=spl,

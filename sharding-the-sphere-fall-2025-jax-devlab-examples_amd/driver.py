@@ -370,7 +370,7 @@ class Solver:
         solver (PDF s.6 pipeline).  auto: shallow water + SSP-RK3 + PLR, one GPU
         or SPMD ranks with the direct xGMI exchange, and at most two passes of
         blocks over the CUs (one step per launch beyond one pass)."""
-        from .ops.fused import fused_block, fused_supported
+        from .ops.fused import fused_block, fused_supported, rank_cus
         c = self.cfg.runtime
         e = self.engines[0]
         if c.fused == "off" or e.device.type != "cuda":
@@ -386,7 +386,7 @@ class Solver:
             if c.fused == "on":
                 raise ValueError(why)
             return False, 1
-        cus = torch.cuda.get_device_properties(e.device).multi_processor_count
+        cus = rank_cus(e.device)
         B = fused_block(e.plan.n, len(e.plan.tiles), cus)
         nb = len(e.plan.tiles) * (e.plan.n // B) ** 2
         if c.fused == "auto" and nb > (2 * cus if self.mode == "single" else cus):
@@ -409,8 +409,8 @@ class Solver:
         use_fused, spl = self._fused_plan(chunk)
         self.fused = None
         if use_fused:
-            from .ops.fused import FusedKernel, fused_block
-            cus = torch.cuda.get_device_properties(e.device).multi_processor_count
+            from .ops.fused import FusedKernel, fused_block, rank_cus
+            cus = rank_cus(e.device)
             fk = FusedKernel(e, B=fused_block(e.plan.n, len(e.plan.tiles), cus))   # collective with several ranks
             self.fused = fk
             self.xgmi = fk if self.mode == "spmd" else None

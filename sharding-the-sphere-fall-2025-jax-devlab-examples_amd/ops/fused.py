@@ -871,6 +871,18 @@ class FusedTorch:
 FUSED_BLOCKS = (8, 12, 16, 18, 20)  # block sizes the kernel is instantiated for
 
 
+def rank_cus(device) -> int:
+    """Compute units one rank can count on: the device's, or its share when
+    STSP_SHARE_GPU=1 puts every rank of the job on one GPU (rehearsals: all
+    ranks' multi-step blocks must be resident together, since a block waits
+    for producers of other ranks)."""
+    import os
+    cus = torch.cuda.get_device_properties(device).multi_processor_count
+    if os.environ.get("STSP_SHARE_GPU") == "1":
+        cus = max(1, cus // max(1, int(os.environ.get("WORLD_SIZE", "1"))))
+    return cus
+
+
 def fused_block(n: int, tiles: Optional[int] = None, cus: Optional[int] = None) -> Optional[int]:
     """Block size of the fused kernel for ``tiles`` tiles of n x n cells
     (None: none divides n).  With the tile count and the GPU's CU count: the
@@ -937,7 +949,7 @@ class FusedKernel:
         if B is None:
             cus = None
             if engine.device.type == "cuda":
-                cus = torch.cuda.get_device_properties(engine.device).multi_processor_count
+                cus = rank_cus(engine.device)
             B = fused_block(engine.plan.n, len(engine.plan.tiles), cus)
         e = engine
         self.e = e
