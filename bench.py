@@ -305,14 +305,14 @@ def main():
         if runtime == "fused":
             # one launch per SSP-RK3 step (temporal blocking, ops/fused.py), hipGraph replay;
             # between GPUs the remote window cells travel through the kernel's own xGMI ring
-            from stsphere.ops.fused import FusedKernel
+            from stsphere.ops.fused import FusedKernel, rank_cus as _rank_cus
             from stsphere.ops.native_runtime import NativeStepper
             fk = FusedKernel(eng, timeout_s=2.0)      # collective with several ranks
             xg = fk if world > 1 else None
             spl = a.steps_per_launch
             if spl == 0:
                 # several steps per launch (in-kernel producer waits) need every block resident
-                cus = rank_cus(device)
+                cus = _rank_cus(device)
                 spl = max([k for k in range(2, 65, 2) if a.steps % k == 0], default=1) if fk.plan.nb <= cus else 1
             info["steps_per_launch"] = spl
             runner = NativeStepper(eng, use_graph=True, steps_per_graph=spg, fused=fk, steps_per_launch=spl,
