@@ -318,7 +318,7 @@ class LowRankDiffusion:
 
     def __init__(self, N: int, L: float = 1.0, kappa: float = 1.0, bc: str = "dirichlet",
                  eps: float = 1e-10, max_rank: Optional[int] = None, dtype=torch.float64, device="cpu",
-                 backend: str = "torch", substeps: int = 1, qr: str = "cholqr3n"):
+                 backend: str = "torch", substeps: int = 1, qr: str = "cholqr3n", core: str = "device"):
         self.h = L / (N + 1) if bc == "dirichlet" else L / N
         # hip recompression: "cholqr3n" (default: device CholeskyQR3,
         # machine-precision factors, the whole step in one native call,
@@ -328,7 +328,13 @@ class LowRankDiffusion:
         # ~sqrt(eps) accuracy; kept for comparison)
         if qr not in ("cholqr3", "cholqr3n", "gram"):
             raise ValueError(f"unknown qr {qr!r}")
+        if core not in ("device", "host"):
+            raise ValueError(f"unknown core {core!r}")
         self.qr = qr
+        # "cholqr3n": the k x k core (R products, Jacobi SVD, truncation) on the
+        # device for k <= 32 (tt_core_kernel; one 4-byte read-back per step)
+        # or on the host (six R factors down, the core maps up)
+        self.core = core
         self.bc = bc
         self.kappa = kappa
         self.eps = eps
@@ -397,6 +403,7 @@ class LowRankDiffusion:
             self._wkey3 = key
         rmax = k if self.max_rank is None else min(k, self.max_rank)
         out = torch.empty((2, N, rmax), dtype=dt_, device=dev)
+        L.stsp_tt_set_core(1 if self.core == "device" else 0)
         rn = L.stsp_tt_lr_step3(native.dtype_code(dt_), native.ptr(A), A.stride(0), native.ptr(B), B.stride(0), N, r,
                                 ns, dt * self.kappa, 1.0 / (self.h * self.h), int(self.bc == "periodic"), self.eps,
                                 self.max_rank or 0, native.ptr(self._ws3), native.ptr(self._hbuf3),

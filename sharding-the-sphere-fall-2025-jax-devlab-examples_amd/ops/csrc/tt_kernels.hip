@@ -538,6 +538,165 @@ __global__ __launch_bounds__(64) void chol_inv_kernel(const T* __restrict__ G, i
   if (t == 0) info[b] = bad;
 }
 
+
+// The k x k core of the CholeskyQR3 recompression on the device (k <= 32, one
+// workgroup, fp64 arithmetic for either element type): Rt = R3 R2 R1 per
+// factor, C = Rt_A Rt_B^T, one-sided (Hestenes) Jacobi SVD of C with the
+// round-robin pair order (16 lanes per column pair, one barrier per round),
+// singular values sorted, the eps / max_rank truncation, and the core maps
+// X = [U S | W] (k x 2k, row stride 2k, rn columns each) of the final
+// products; out[0] = rn (<= 0: failure code).  Replaces the host round trip
+// of stsp_tt_lr_step3 (six R factors down, jacobi_svd on the host, X up).
+constexpr int CORE_K = 32;
+
+template <typename T>
+__global__ __launch_bounds__(256) void tt_core_kernel(const T* __restrict__ Rs, const int* __restrict__ dinfo, int k,
+                                                      double eps, int max_rank, T* __restrict__ X,
+                                                      int* __restrict__ out) {
+  constexpr int K = CORE_K, KS = CORE_K + 1;
+  __shared__ double sR[2][3][K * K];        // R factors [side][pass]
+  __shared__ double sP[2][K * K];           // R2 R1
+  __shared__ double sC[K * KS], sW[K * KS];
+  __shared__ double sig[K];
+  __shared__ int s_ord[K];
+  __shared__ int s_flag, s_rot, s_rn;
+  __shared__ double s_tot;
+  const int tid = threadIdx.x;
+  const int kk = k * k;
+  if (tid == 0) {
+    int bad = 0;
+    for (int i = 0; i < 6; ++i) bad |= dinfo[i] != 0;
+    s_flag = bad;
+  }
+  for (int e = tid; e < 6 * kk; e += blockDim.x) {
+    const int sp = e / kk, r = e - sp * kk;
+    sR[sp / 3][sp % 3][r] = (double)Rs[(size_t)(sp * 2) * kk + r];     // [side][pass][R, Ri]: the R block
+  }
+  __syncthreads();
+  if (s_flag) {
+    if (tid == 0) out[0] = -24;
+    return;
+  }
+  // P = R2 R1, then R3 P (into sR[side][0]); upper-triangular left factors
+  for (int e = tid; e < 2 * kk; e += blockDim.x) {
+    const int sd = e / kk, r = e - sd * kk, i = r / k, j = r - i * k;
+    double acc = 0;
+    for (int l = i; l < k; ++l) acc += sR[sd][1][i * k + l] * sR[sd][0][l * k + j];
+    sP[sd][r] = acc;
+  }
+  __syncthreads();
+  for (int e = tid; e < 2 * kk; e += blockDim.x) {
+    const int sd = e / kk, r = e - sd * kk, i = r / k, j = r - i * k;
+    double acc = 0;
+    for (int l = i; l < k; ++l) acc += sR[sd][2][i * k + l] * sP[sd][l * k + j];
+    sR[sd][0][r] = acc;
+  }
+  __syncthreads();
+  // C = Rt_A Rt_B^T, W = I
+  for (int e = tid; e < kk; e += blockDim.x) {
+    const int i = e / k, j = e - i * k;
+    double acc = 0;
+    for (int l = 0; l < k; ++l) acc += sR[0][0][i * k + l] * sR[1][0][j * k + l];
+    sC[i * KS + j] = acc;
+    sW[i * KS + j] = i == j ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0;
+    for (int i = 0; i < k; ++i)
+      for (int j = 0; j < k; ++j) t += sC[i * KS + j] * sC[i * KS + j];
+    s_tot = t;
+  }
+  __syncthreads();
+  const double tiny = 1e-30 * s_tot;
+  // round-robin: m = k rounded up to even, position 0 fixed, the rest rotate;
+  // pair p joins positions p and m - 1 - p (index k: the dummy of odd k)
+  const int m = (k + 1) & ~1;
+  const int pr = tid >> 4, ln = tid & 15;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    if (tid == 0) s_rot = 0;
+    __syncthreads();
+    for (int rd = 0; rd < m - 1; ++rd) {
+      if (pr < m / 2) {
+        const int qa = pr, qb = m - 1 - pr;
+        int p = qa == 0 ? 0 : 1 + (qa - 1 + rd) % (m - 1);
+        int q = qb == 0 ? 0 : 1 + (qb - 1 + rd) % (m - 1);
+        if (p > q) { const int x = p; p = q; q = x; }
+        if (q < k) {
+          double al = 0, be = 0, ga = 0;
+          for (int r = ln; r < k; r += 16) {
+            const double x = sC[r * KS + p], y = sC[r * KS + q];
+            al += x * x;
+            be += y * y;
+            ga += x * y;
+          }
+#pragma unroll
+          for (int o = 8; o >= 1; o >>= 1) {
+            al += __shfl_xor(al, o, 16);
+            be += __shfl_xor(be, o, 16);
+            ga += __shfl_xor(ga, o, 16);
+          }
+          if (!(al <= tiny || be <= tiny || fabs(ga) <= 1e-15 * sqrt(al * be))) {
+            const double ze = (be - al) / (2.0 * ga);
+            const double t = (ze >= 0 ? 1.0 : -1.0) / (fabs(ze) + sqrt(1.0 + ze * ze));
+            const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+            for (int r = ln; r < k; r += 16) {
+              const double x = sC[r * KS + p], y = sC[r * KS + q];
+              sC[r * KS + p] = c * x - s * y;
+              sC[r * KS + q] = s * x + c * y;
+              const double u = sW[r * KS + p], w = sW[r * KS + q];
+              sW[r * KS + p] = c * u - s * w;
+              sW[r * KS + q] = s * u + c * w;
+            }
+            if (ln == 0) s_rot = 1;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    const int rot = s_rot;
+    __syncthreads();
+    if (!rot) break;
+  }
+  if (tid < k) {
+    double s2 = 0;
+    for (int r = 0; r < k; ++r) s2 += sC[r * KS + tid] * sC[r * KS + tid];
+    sig[tid] = sqrt(s2);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int j = 0; j < k; ++j) s_ord[j] = j;
+    for (int a = 1; a < k; ++a) {              // insertion sort, descending
+      const int v = s_ord[a];
+      int b = a - 1;
+      while (b >= 0 && sig[s_ord[b]] < sig[v]) { s_ord[b + 1] = s_ord[b]; --b; }
+      s_ord[b + 1] = v;
+    }
+    double tot = 0;
+    for (int j = 0; j < k; ++j) tot += sig[j] * sig[j];
+    int rn = k;
+    double tail = 0;
+    for (int jj = k - 1; jj >= 1; --jj) {
+      tail += sig[s_ord[jj]] * sig[s_ord[jj]];
+      if (tail <= eps * eps * tot) rn = jj;
+      else break;
+    }
+    if (max_rank > 0 && rn > max_rank) rn = max_rank;
+    if (rn < 1) rn = 1;
+    s_rn = tot > 0 ? rn : -22;
+  }
+  __syncthreads();
+  const int rn = s_rn;
+  if (rn > 0) {
+    for (int e = tid; e < k * rn; e += blockDim.x) {
+      const int i = e / rn, jj = e - i * rn, j = s_ord[jj];
+      X[(size_t)i * 2 * k + jj] = (T)sC[i * KS + j];
+      X[(size_t)i * 2 * k + rn + jj] = (T)sW[i * KS + j];
+    }
+  }
+  if (tid == 0) out[0] = rn;
+}
+
 }  // namespace
 
 extern "C" {
@@ -705,6 +864,15 @@ size_t stsp_tt_step_workspace3(int N, int r, int nsub) {
          (size_t)12 * k * k + 16;
 }
 
+// 1 (default): stsp_tt_lr_step3 forms the k x k core on the device when k <= 32
+// (tt_core_kernel); 0: on the host (jacobi_svd), for comparison
+static int tt_core_mode = 1;
+int stsp_tt_set_core(int mode) {
+  const int old = tt_core_mode;
+  tt_core_mode = mode;
+  return old;
+}
+
 int stsp_tt_lr_step3(int dtype, const void* A, int lda, const void* B, int ldb, int N, int r, int nsub, double c,
                      double ih2, int periodic, double eps, int max_rank, void* ws, double* hbuf, void* Aout,
                      void* Bout, int ldo, hipStream_t st) {
@@ -760,6 +928,24 @@ int stsp_tt_lr_step3(int dtype, const void* A, int lda, const void* B, int ldb, 
   double* hR = hbuf;                 // [side][pass] k x k
   int* hinfo = (int*)(hbuf + 6 * k * k);
   double* hX = hbuf + 6 * k * k + 8;
+  if (k <= CORE_K && tt_core_mode != 0) {
+    // the core on the device: one 4-byte read-back (the rank sizes the final products)
+    int* drn = dinfo + 8;
+    if (dtype == 1)
+      hipLaunchKernelGGL(tt_core_kernel<double>, dim3(1), dim3(256), 0, st, (const double*)Rs, dinfo, k, eps,
+                         max_rank, (double*)dX, drn);
+    else
+      hipLaunchKernelGGL(tt_core_kernel<float>, dim3(1), dim3(256), 0, st, (const float*)Rs, dinfo, k, eps,
+                         max_rank, (float*)dX, drn);
+    if (hipGetLastError() != hipSuccess) return -25;
+    if (hipMemcpyAsync(hinfo, drn, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess) return -20;
+    if (hipStreamSynchronize(st) != hipSuccess) return -21;
+    const int rn = hinfo[0];
+    if (rn <= 0) return rn;
+    if ((rc = stsp_tt_mm(dtype, Q[0], k, dX, 2 * k, Aout, ldo, N, k, rn, 1.0, 0.0, st))) return rc;
+    if ((rc = stsp_tt_mm(dtype, Q[1], k, (char*)dX + es * rn, 2 * k, Bout, ldo, N, k, rn, 1.0, 0.0, st))) return rc;
+    return rn;
+  }
   for (int side = 0; side < 2; ++side)
     for (int pass = 0; pass < 3; ++pass)
       if (hipMemcpyAsync((char*)hR + es * (size_t)(side * 3 + pass) * k * k, Rp(side, pass, 0), es * (size_t)k * k,

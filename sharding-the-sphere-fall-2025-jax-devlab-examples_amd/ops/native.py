@@ -171,6 +171,8 @@ def _declare_tt(L):
     L.stsp_tt_step_workspace2.restype = ctypes.c_size_t
     L.stsp_tt_lr_step2.argtypes = [ci, vp, ci, vp, ci, ci, ci, ci, cd, cd, ci, cd, ci, vp, vp, vp, vp, ci, vp]
     L.stsp_tt_lr_step2.restype = ci
+    L.stsp_tt_set_core.argtypes = [ci]
+    L.stsp_tt_set_core.restype = ci
     L.stsp_tt_lr_step3.argtypes = [ci, vp, ci, vp, ci, ci, ci, ci, cd, cd, ci, cd, ci, vp, vp, vp, vp, ci, vp]
     L.stsp_tt_lr_step3.restype = ci
     L.stsp_tt_step_workspace3.argtypes = [ci, ci, ci]

@@ -308,3 +308,30 @@ def test_lowrank_shallow_water_hip_matches_dense():
     R = sw.to_dense(F)
     assert float((R - D).norm() / D.norm()) < 1e-10
     assert max(f.rank for f in F) <= 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-12), (torch.float32, 1e-5)])
+@pytest.mark.parametrize("ns,max_rank", [(1, None), (2, None), (2, 6)])
+def test_device_core_matches_host_core(dtype, tol, ns, max_rank):
+    """the k x k core of the CholeskyQR3 step (R products,
+    one-sided Jacobi SVD, truncation) on the device (tt_core_kernel, k <= 32)
+    gives the host core's factored field to rounding, with and without a rank
+    cap, and the same rank."""
+    N = 320
+    U = _panel(N)
+    kw = dict(kappa=1.0, eps=1e-12 if dtype == torch.float64 else 1e-6, max_rank=max_rank, backend="hip",
+              substeps=ns, qr="cholqr3n", dtype=dtype)
+    dev = tt.LowRankDiffusion(N, core="device", **kw)
+    host = tt.LowRankDiffusion(N, core="host", **kw)
+    lr = tt.LowRankField.from_dense(U.cuda().to(dtype), eps=1e-14 if dtype == torch.float64 else 1e-7,
+                                    max_rank=16 >> ns)
+    dt = 0.5 * dev.dt_max
+    a, b = lr, lr
+    for _ in range(4):
+        a = dev.step(a, dt)
+        b = host.step(b, dt)
+        torch.cuda.synchronize()
+        assert a.rank == b.rank
+        da, db = a.dense().double(), b.dense().double()
+        assert float((da - db).norm() / db.norm()) < tol

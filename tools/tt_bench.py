@@ -56,8 +56,10 @@ def main():
     ap.add_argument("--eps", type=float, default=1e-8)
     ap.add_argument("--max-rank", type=int, default=16)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--qr", default="cholqr3", choices=["cholqr3", "cholqr3n", "gram"],
+    ap.add_argument("--qr", default="cholqr3n", choices=["cholqr3", "cholqr3n", "gram"],
                     help="hip recompression: device CholeskyQR3 (default) or the native Gram/eigen step")
+    ap.add_argument("--core", default="device", choices=["device", "host"],
+                    help="cholqr3n: the k x k core (Jacobi SVD) on the device (k <= 32) or on the host")
     ap.add_argument("--substeps", default="1,2,3",
                     help="explicit steps per recompression (tt us is per simulated step)")
     a = ap.parse_args()
@@ -95,7 +97,7 @@ def main():
         t_dense = time_loop(dense_step, a.steps, sync)
         for ns in subs:
             s = tt.LowRankDiffusion(N, kappa=1.0, eps=a.eps, max_rank=min(a.max_rank, 64 >> ns), backend="hip", device=dev,
-                                    substeps=ns, qr=a.qr)
+                                    substeps=ns, qr=a.qr, core=a.core)
             st = {"lr": tt.LowRankField(A.clone(), B.clone())}
 
             def tt_step():
