@@ -320,6 +320,8 @@ def test_device_core_matches_host_core(dtype, tol, ns, max_rank):
     cap, and the same rank."""
     N = 320
     U = _panel(N)
+    if max_rank is None and dtype == torch.float32:
+        max_rank = 64 >> ns          # fp32 rounding noise grows the rank past the 64-column kernels
     kw = dict(kappa=1.0, eps=1e-12 if dtype == torch.float64 else 1e-6, max_rank=max_rank, backend="hip",
               substeps=ns, qr="cholqr3n", dtype=dtype)
     dev = tt.LowRankDiffusion(N, core="device", **kw)
