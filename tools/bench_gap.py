@@ -68,6 +68,17 @@ def main():
             torch.cuda.synchronize()
             host.append((time.perf_counter() - t0) * 1e6)
             ev.append(e0.elapsed_time(e1) * 1e3)
+        # host cost of issuing run(k) (no sync) and of a synchronize on an idle GPU
+        enq, idle = [], []
+        for _ in range(a.reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r.run(k)
+            enq.append((time.perf_counter() - t0) * 1e6)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            torch.cuda.synchronize()
+            idle.append((time.perf_counter() - t0) * 1e6)
         # back to back: 10 regions, one sync
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -77,7 +88,8 @@ def main():
         b2b = (time.perf_counter() - t0) * 1e6 / 10
         out["per_K"][k] = {"host_us_min": min(host), "host_us_med": float(np.median(host)),
                            "event_us_min": min(ev), "event_us_med": float(np.median(ev)),
-                           "b2b_host_us": b2b}
+                           "b2b_host_us": b2b, "enqueue_us_med": float(np.median(enq)),
+                           "idle_sync_us_med": float(np.median(idle))}
         print(k, out["per_K"][k], file=sys.stderr, flush=True)
     K = np.array(ks, dtype=float)
     for key in ("host_us_min", "event_us_min", "b2b_host_us"):
