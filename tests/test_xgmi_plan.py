@@ -43,16 +43,36 @@ def test_every_remote_ghost_delivered(N, t, R, loop):
         for p, s, gval in zip(peer, slot, gid):
             assert rings[p][s] in (-1, gval), "two different cells pushed into one ring slot"
             rings[p][s] = gval
-        # prime entries = the distinct (source cell, destination) pairs of the push map
+        want = set(zip(L.local_flat(gid).tolist(), code.tolist()))
+        # carried corner ghosts (panel-edge strip ends): their own push table
+        crem = x.cpush < -1
+        ccode = (-2 - x.cpush[crem]).astype(np.int64)
+        cpeer, cslot = ccode >> SLOT_BITS, ccode & ((1 << SLOT_BITS) - 1)
+        cli, cq, ca, cb = np.nonzero(crem)
+        ci = np.where(cq & 1, n - 1 - cb, cb)
+        cj = np.where(cq & 2, n - 1 - ca, ca)
+        for k in range(len(cli)):
+            f, I0, J0 = L.tile_origin(int(x.plan.tiles[cli[k]]))
+            gval = L.global_flat(f, I0 + ci[k], J0 + cj[k])
+            assert rings[cpeer[k]][cslot[k]] in (-1, gval), "two different cells pushed into one ring slot"
+            rings[cpeer[k]][cslot[k]] = gval
+            want.add((int(L.local_flat(np.array([gval]))[0]), int(ccode[k])))
+        # prime entries = the distinct (source cell, destination) pairs of both push tables
         assert len(x.prime_src) == len(np.unique(np.stack([x.prime_src, x.prime_code], 1), axis=0))
         pairs = set(zip(x.prime_src.tolist(), x.prime_code.tolist()))
-        want = set(zip(L.local_flat(gid).tolist(), code.tolist()))
         assert pairs == want
+    ncorner = 0
     for p in range(R):
-        gm = L.plan(p).ghost_map
+        pl = L.plan(p)
+        gm = pl.ghost_map
         gs = L.ghost_sources(p)
         m = gm < 0
         assert (rings[p][-1 - gm[m]] == gs[m]).all()
+        rc = pl.remote_corners()
+        ncorner += int(rc.sum())
+        assert (rings[p][-1 - pl.corner_map[rc]] == L.corner_sources(p)[rc]).all()
+    if t > 1 and R > 1 and not loop:
+        assert ncorner > 0 or R <= 2
 
 
 @pytest.mark.parametrize("N,t,R,loop", CASES)
