@@ -57,10 +57,16 @@
 #ifndef STSP_FUSED_CW0
 #define STSP_FUSED_CW0 1
 #endif
+// STSP_FUSED_PAIR=1: stages 2 and 3 compute two faces of a line pair per task
+// (the shared cell's slope once); 0: one face per task
+#ifndef STSP_FUSED_PAIR
+#define STSP_FUSED_PAIR 1
+#endif
 
 namespace {
 
 constexpr bool GINL = STSP_FUSED_GINL != 0;
+constexpr bool PAIR = STSP_FUSED_PAIR != 0 && !GINL;
 
 // cube-corner face table widths (ops/fused.py::corner_tables)
 constexpr int CT_INTS = 16, CT_FLAGS = 12, CG_VALS = 8;
@@ -638,6 +644,103 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
 #pragma unroll
     for (int f = 0; f < 4; ++f) s_fl[f][fslot] = fl[f];
   };
+  // Two faces in a row along one line direction, lines k and k + 1 (stages
+  // 2 and 3, PAIR): they share cell k, whose slope (the right state of face k,
+  // the left state of face k + 1) is computed once from the same operands the
+  // single-face body uses for it (its own codes), so the pair is bitwise the
+  // two single faces; 3 slopes and 5 cells instead of 4 and 8.  two = false:
+  // face k alone (the last line of an odd count).
+  auto face2 = [&](bool ax, int fu, int fv, int k, bool two, auto edge_c) {
+    constexpr bool EDGE = decltype(edge_c)::value;
+    const int st = ax ? WS : 1;
+    const int ib = fv * WS + fu, ia = ib - st, ic = ib + st;
+    // stencil neighbours: cell a (k - 1), b (k), c (k + 1), minus / plus side
+    int iam = ia - st, iap = ib, ibm = ia, ibp = ic, icm = ib, icp = ic + st;
+    int ra = 0, rb = 0;
+    bool wnear = false, skip0 = false, skip1 = !two;
+    if constexpr (EDGE) {
+      const int e0 = ax ? ky0 : kx0, e1 = ax ? ky1 : kx1;
+      // line k or k + 1 within one line of a panel-edge line (wider is harmless: a
+      // plain neighbour's code is -1)
+      const bool near = (unsigned)(k - e0 + 2) <= 3u || (unsigned)(k - e1 + 2) <= 3u;
+      wnear = __builtin_amdgcn_ballot_w64(near) != 0;
+      if (wnear) gwait();
+      if (near) {
+        const int sm = ax ? 2 : 0;
+        const int ci = fv * W + fu, cs = ax ? W : 1;           // window (code) index of cell b
+        const unsigned long long ca = s_code[ci - cs], cb = s_code[ci], cc = two ? s_code[ci + cs] : 0ull;
+        const int eam = ncode(ca, sm), eap = ncode(ca, sm + 1);
+        const int ebm = ncode(cb, sm), ebp = ncode(cb, sm + 1);
+        const int ecm = two ? ncode(cc, sm) : -1, ecp = two ? ncode(cc, sm + 1) : -1;
+        skip0 = eam == -3 || ebm == -3;                        // a cell is missing: corner faces
+        skip1 = skip1 || ebm == -3 || ecm == -3;
+        if (eam >= 0) iam = GB + eam;
+        if (eap >= 0) iap = GB + eap;
+        if (ebm >= 0) ibm = GB + ebm;
+        if (ebp >= 0) ibp = GB + ebp;
+        if (ecm >= 0) icm = GB + ecm;
+        if (ecp >= 0) icp = GB + ecp;
+      }
+      ra = fregion(X0 + fu - (ax ? 0 : 1), Y0 + fv - (ax ? 1 : 0), N);
+      ra = ra < 0 ? 0 : ra;
+      rb = fregion(X0 + fu, Y0 + fv, N);
+      rb = rb < 0 ? 0 : rb;
+    }
+    if (skip0 && skip1) return;
+    // face k first (cells a, b), keeping only b's primitives and slope for face
+    // k + 1: fewer live registers than both faces' states at once
+    T ca_[5], cb_[5], hb[4];
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+      ca_[f] = wf[f * WW + ia];
+      cb_[f] = wf[f * WW + ib];
+    }
+    {
+      T wl0[4], wr0[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const T am = wf[f * WW + iam], bp = wf[f * WW + ibp];
+        T ap = cb_[f], bm = ca_[f];
+        if constexpr (EDGE) {
+          if (wnear) {
+            ap = wf[f * WW + iap];
+            bm = wf[f * WW + ibm];
+          }
+        }
+        wl0[f] = ca_[f] + half_slope<LIM>(ca_[f] - am, ap - ca_[f]);
+        hb[f] = half_slope<LIM>(cb_[f] - bm, bp - cb_[f]);
+        wr0[f] = cb_[f] - hb[f];
+      }
+      if (!skip0) {
+        const int fs = ax ? NFX + (k - L1) * H1 + (fu - L1) : (fv - L1) * (H1 + 1) + (k - L1);
+        const T* m = &s_nrm[ax ? 1 : 0][ra][0][k];
+        T fl[4];
+        swe_flux<T>(wl0, wr0, ca_, cb_, m[0], m[W + 1], m[2 * (W + 1)], s_len[fs], a.g, fl);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) s_fl[f][fs] = fl[f];
+      }
+    }
+    if (skip1) return;
+    T cc_[5], wl1[4], wr1[4];
+#pragma unroll
+    for (int f = 0; f < 5; ++f) cc_[f] = wf[f * WW + ic];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const T cp = wf[f * WW + icp];
+      T cm = cb_[f];
+      if constexpr (EDGE) {
+        if (wnear) cm = wf[f * WW + icm];
+      }
+      wl1[f] = cb_[f] + hb[f];
+      wr1[f] = cc_[f] - half_slope<LIM>(cc_[f] - cm, cp - cc_[f]);
+    }
+    const int fs = ax ? NFX + (k + 1 - L1) * H1 + (fu - L1) : (fv - L1) * (H1 + 1) + (k + 1 - L1);
+    const T* m = &s_nrm[ax ? 1 : 0][rb][0][k + 1];
+    T fl[4];
+    swe_flux<T>(wl1, wr1, cb_, cc_, m[0], m[W + 1], m[2 * (W + 1)], s_len[fs], a.g, fl);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) s_fl[f][fs] = fl[f];
+  };
   // Stage-1 faces whose whole stencil lies in the block's own cells ("inner":
   // lines k in [R+2, R+B-2] x the block's B rows, both axes): a multi-step
   // launch computes them while it waits for its producers (the own cells'
@@ -762,7 +865,8 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     // those.  Round 3 had all three on wave 0: 6.2k cycles in the corner
     // blocks' stage-1 faces against 3.3k for the slowest interior wave
     // (profiles/r4_tail).  STSP_FUSED_CW0=0: corner faces on the last wave.
-    const int nax = s == 0 ? NOX : nx;                       // stage 1: the outer faces only
+    // stage 1: the outer faces only; stages 2, 3 (PAIR): two faces per task
+    const int nax = s == 0 ? NOX : (PAIR ? ((nl + 1) >> 1) * nr : nx);
 #if STSP_FUSED_CW0
     const int cw = ncor ? 1 : 0;
     const int nreg = NT - 64 * cw, t2r = 64 * (cw + (GINL ? 0 : ngw)), nr2 = NT - t2r;   // round 2 from thread t2r
@@ -781,6 +885,15 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         const bool ax = tf >= nax;                           // false: x-face, true: y-face
         const int t2 = ax ? tf - nax : tf;
         int fu, fv, k, p;
+        if (PAIR && s > 0) {                                 // lines k, k + 1 of row p
+          const int c = t2 / nr, r = t2 - c * nr;
+          k = lo + 2 * c; p = lo + r;
+          const bool two = k + 1 <= hi;
+          if (!ax) { fv = p; fu = k; } else { fu = p; fv = k; }
+          if (edge) face2(ax, fu, fv, k, two, std::true_type{});
+          else face2(ax, fu, fv, k, two, std::false_type{});
+          continue;
+        }
         if (s == 0) {
           outer_face(t2, k, p);
         } else {                                             // line-major: the faces near an
