@@ -57,10 +57,12 @@
 #ifndef STSP_FUSED_CW0
 #define STSP_FUSED_CW0 1
 #endif
-// STSP_FUSED_PAIR=1: stages 2 and 3 compute two faces of a line pair per task
-// (the shared cell's slope once); 0: one face per task
+// STSP_FUSED_PAIR=1 (pair1 variant): stages 2 and 3 compute two faces of a
+// line pair per task (the shared cell's slope once); 0 (default): one face per
+// task.  The pair form raises the multi-step kernel's VGPR spills at B = 16
+// from 5 to 54 (fp64, 168 VGPRs)
 #ifndef STSP_FUSED_PAIR
-#define STSP_FUSED_PAIR 1
+#define STSP_FUSED_PAIR 0
 #endif
 
 namespace {
