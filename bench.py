@@ -177,9 +177,12 @@ def launch_ranks(a) -> int:
         shutil.rmtree(pdir, ignore_errors=True)
 
 
-def single_rank_reference(a, phys_factory, grid, dtype, device, dt, ng, nsteps, runtime, backend):
+def single_rank_reference(a, phys_factory, grid, dtype, device, dt, ng, nsteps, runtime, backend, fused_B=None):
     """[F, 6, N, N] state of one rank stepping ``nsteps`` from the initial
-    condition on this device (the bitwise reference of a multi-rank run)."""
+    condition on this device (the bitwise reference of a multi-rank run).
+    ``fused_B``: the ranks' fused block size (the panel-edge normals and lengths
+    of a face come from in-kernel tangents inside one panel and from host
+    tables in edge blocks, so the block size moves results by roundoff)."""
     import numpy as np
     from stsphere.engine import Engine
     from stsphere.parallel.layout import TileLayout
@@ -191,7 +194,7 @@ def single_rank_reference(a, phys_factory, grid, dtype, device, dt, ng, nsteps, 
         fk = None
         if runtime == "fused":
             from stsphere.ops.fused import FusedKernel
-            fk = FusedKernel(ref)
+            fk = FusedKernel(ref, B=fused_B)
         r = NativeStepper(ref, use_graph=True, steps_per_graph=max(nsteps, 1), fused=fk)
         r.run(nsteps)
         r.close()
@@ -315,6 +318,7 @@ def main():
                 cus = _rank_cus(device)
                 spl = max([k for k in range(2, 65, 2) if a.steps % k == 0], default=1) if fk.plan.nb <= cus else 1
             info["steps_per_launch"] = spl
+            info["fused_B"] = fk.plan.B
             runner = NativeStepper(eng, use_graph=True, steps_per_graph=spg, fused=fk, steps_per_launch=spl,
                                    direct=a.launch == "direct" or (a.launch == "auto" and world == 1))
         elif runtime == "native":
@@ -369,7 +373,8 @@ def main():
         got = gathered(eng)
         d = torch.zeros(1, dtype=torch.float64, device=cdev)
         if rank == 0:
-            want = single_rank_reference(a, phys_factory, grid, dtype, device, eng.dt, ng, nsteps, runtime, backend)
+            want = single_rank_reference(a, phys_factory, grid, dtype, device, eng.dt, ng, nsteps, runtime, backend,
+                                         fused_B=info.get("fused_B") if runtime == "fused" else None)
             d[0] = float(np.abs(got - want).max())
         dist.broadcast(d, src=0)
         return float(d.item())
@@ -497,6 +502,7 @@ def main():
                 "comm": comm,
                 "block": list((eng.compute.bx, eng.compute.by)) if hasattr(eng.compute, "bx") else None,
                 "steps_per_launch": info["steps_per_launch"],
+                "fused_block": info.get("fused_B"),
                 "graph_replayed_steps": timed.get("graph_steps"),
                 "direct_launch_steps": timed.get("direct_steps"),
                 "kernel_launches": timed.get("launches") if timed.get("direct_steps") else None,
