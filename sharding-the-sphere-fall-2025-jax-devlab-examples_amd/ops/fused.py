@@ -1185,7 +1185,8 @@ class FusedKernel:
         many steps in one launch, the state back in pool[0]."""
         d = self.descs[parity] if nsteps == 1 else self.multi_desc(nsteps)
         if stream is None:
-            stream = int(torch.cuda.current_stream().cuda_stream)
+            from . import native
+            stream = native.current_stream_handle()
         rc = self._launch_fn(self.dcode, d, stream)
         if rc:
             raise RuntimeError(f"fused step failed with code {rc}")
