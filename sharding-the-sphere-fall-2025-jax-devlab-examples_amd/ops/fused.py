@@ -1185,8 +1185,7 @@ class FusedKernel:
         many steps in one launch, the state back in pool[0]."""
         d = self.descs[parity] if nsteps == 1 else self.multi_desc(nsteps)
         if stream is None:
-            from . import native
-            stream = native.current_stream_handle()
+            stream = int(torch.cuda.current_stream().cuda_stream)
         rc = self._launch_fn(self.dcode, d, stream)
         if rc:
             raise RuntimeError(f"fused step failed with code {rc}")

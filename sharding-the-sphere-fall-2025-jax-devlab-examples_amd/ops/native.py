@@ -12,7 +12,6 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
-from typing import Optional
 
 import torch  # noqa: F401  (must precede the library load)
 
@@ -209,15 +208,8 @@ def ptr(t) -> int:
     return 0 if t is None else int(t.data_ptr())
 
 
-_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
-
-
-def current_stream_handle(device_index: Optional[int] = None) -> int:
-    """The current HIP stream of a device as an int (torch's raw accessor when
-    present: the launch path of a timed region calls this once per launch)."""
-    if _RAW_STREAM is not None:
-        return int(_RAW_STREAM(torch.cuda.current_device() if device_index is None else device_index))
-    return int(torch.cuda.current_stream(device_index).cuda_stream)
+def current_stream_handle() -> int:
+    return int(torch.cuda.current_stream().cuda_stream)
 
 
 def check(rc: int, what: str) -> None:

@@ -357,7 +357,7 @@ class NativeStepper:
 
     def _run_direct(self, nsteps: int) -> None:
         """nsteps (a multiple of the period) as direct fused launches."""
-        st = native.current_stream_handle(self.e.device.index)
+        st = int(torch.cuda.current_stream(self.e.device).cuda_stream)
         for _ in range(nsteps // self.period):
             if self.spl > 1:
                 self.fused.launch(0, st, nsteps=self.spl)
