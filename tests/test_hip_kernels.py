@@ -25,10 +25,16 @@ PHYS = {
 
 
 def _relerr(ref, hip):
-    """max over fields of max|a-b| / max|a| on the interior cells."""
+    """max over fields of max|a-b| / max|a| on the interior cells; a NaN
+    raises with where it sits (engine, field, tile, row, column)."""
     F = ref.physics.F
     a = ref.tiles_view().reshape(F, -1)
     b = hip.tiles_view().reshape(F, -1).double()
+    for nm, e in (("reference", ref), ("hip", hip)):
+        bad = torch.isnan(e.tiles_view())
+        if bool(bad.any()):
+            raise AssertionError(f"NaN in the {nm} state: {int(bad.sum())} values, first (f, tile, j, i) "
+                                 f"{torch.nonzero(bad)[:6].tolist()}")
     return ((a - b).abs().amax(dim=1) / a.abs().amax(dim=1).clamp_min(1e-30)).max().item()
 
 
