@@ -29,7 +29,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 // ---- RCCL, resolved at run time (rccl_abi.h) -------------------------------------
@@ -429,15 +431,43 @@ extern "C" int stsp_nccl_selftest(void* comm, void* stream) {
 // over xGMI.  Uncached (MTYPE UC) so neither the owner's nor a peer's L2 keeps
 // a line of it; every kernel access is additionally system scope.
 
+// Ring memory stays with the process once allocated: a freed ring goes on a
+// free list and the next ring that fits reuses it (zeroed).  Handing uncached
+// memory back with hipFree was followed by corrupted values in ordinary
+// allocations made afterwards (a test after the loopback test read NaN and
+// garbage from fresh torch buffers in 5 of 6 runs; never with the ring kept,
+// profiles/r4_ring/README.md), and a ring peers have mapped should not
+// return to the driver under them anyway.
+namespace {
+std::mutex g_ring_mu;
+std::unordered_map<void*, size_t> g_ring_bytes;   // every ring ever allocated
+std::vector<void*> g_ring_free;                   // of those, the free ones
+}  // namespace
+
 extern "C" int stsp_xg_alloc(size_t bytes, void** out) {
   *out = nullptr;
   void* p = nullptr;
-  if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) return -1;
-  if (hipMemset(p, 0, bytes) != hipSuccess) {
-    hipFree(p);
+  size_t have = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    size_t best = 0;
+    for (size_t k = 0; k < g_ring_free.size(); ++k) {   // smallest free ring that fits
+      const size_t b = g_ring_bytes[g_ring_free[k]];
+      if (b >= bytes && (!p || b < have)) { p = g_ring_free[k]; have = b; best = k; }
+    }
+    if (p) g_ring_free.erase(g_ring_free.begin() + best);
+  }
+  if (!p) {
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) return -1;
+    have = bytes;
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    g_ring_bytes[p] = bytes;
+  }
+  if (hipMemset(p, 0, have) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    g_ring_free.push_back(p);
     return -2;
   }
-  if (hipDeviceSynchronize() != hipSuccess) return -3;
   *out = p;
   return 0;
 }
@@ -457,7 +487,28 @@ extern "C" int stsp_alloc_flags(size_t bytes, unsigned flags, void** out) {
   return 0;
 }
 
-extern "C" int stsp_xg_free(void* p) { return p && hipFree(p) != hipSuccess ? -1 : 0; }
+extern "C" int stsp_xg_free(void* p) {
+  if (!p) return 0;
+  std::lock_guard<std::mutex> lk(g_ring_mu);
+  if (!g_ring_bytes.count(p)) return -1;   // not a ring of this process
+  for (void* q : g_ring_free)
+    if (q == p) return -1;                 // freed twice
+  g_ring_free.push_back(p);
+  return 0;
+}
+
+// Rings held by the process (allocated, free) and their bytes.
+extern "C" int stsp_xg_pool(long long* out4) {
+  std::lock_guard<std::mutex> lk(g_ring_mu);
+  long long tot = 0, fb = 0;
+  for (auto& kv : g_ring_bytes) tot += (long long)kv.second;
+  for (void* q : g_ring_free) fb += (long long)g_ring_bytes[q];
+  out4[0] = (long long)g_ring_bytes.size();
+  out4[1] = (long long)g_ring_free.size();
+  out4[2] = tot;
+  out4[3] = fb;
+  return 0;
+}
 
 extern "C" int stsp_ipc_handle_bytes(void) { return HIP_IPC_HANDLE_SIZE; }
 

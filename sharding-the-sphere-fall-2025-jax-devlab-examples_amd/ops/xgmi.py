@@ -437,7 +437,7 @@ class IpcRing:
         self.opened = []
         if self.base:
             torch.cuda.synchronize(self.device)
-            L.stsp_xg_free(ctypes.c_void_p(self.base))
+            L.stsp_xg_free(ctypes.c_void_p(self.base))     # back to the process's ring pool
             self.base = None
 
 
@@ -447,6 +447,8 @@ def _declare(L):
     L.stsp_xg_alloc.restype = ci
     L.stsp_xg_free.argtypes = [vp]
     L.stsp_xg_free.restype = ci
+    L.stsp_xg_pool.argtypes = [ctypes.POINTER(ctypes.c_longlong)]
+    L.stsp_xg_pool.restype = ci
     L.stsp_ipc_handle_bytes.argtypes = []
     L.stsp_ipc_handle_bytes.restype = ci
     L.stsp_ipc_get.argtypes = [vp, vp]

@@ -27,3 +27,30 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _heap_canary(request):
+    """STSP_HEAP_CANARY=1 (GPU runs): after every GPU test, collect garbage
+    (so destructors run here, not inside a later test) and check that fresh
+    device allocations do not overlap (each filled with its own value and
+    read back) and that a session-long canary buffer is unchanged."""
+    yield
+    if os.environ.get("STSP_HEAP_CANARY") != "1" or "gpu" not in request.keywords:
+        return
+    import gc
+    import torch
+    if not torch.cuda.is_available():
+        return
+    gc.collect()
+    torch.cuda.synchronize()
+    if not hasattr(_heap_canary, "keep"):
+        _heap_canary.keep = torch.full((1 << 23,), 7.0, dtype=torch.float64, device="cuda")
+    bad_keep = int((_heap_canary.keep != 7.0).sum())
+    xs = [torch.full(((1 << (8 + k % 14)) + 8 * k,), float(k), dtype=torch.float64, device="cuda")
+          for k in range(96)]
+    bad = [k for k, x in enumerate(xs) if not bool((x == float(k)).all())]
+    print(f"\n[heap-canary] after {request.node.nodeid}: keep bad {bad_keep}, overlapping {bad[:8]}",
+          flush=True)
+    del xs
+

@@ -38,6 +38,22 @@ def _relerr(ref, hip):
     return ((a - b).abs().amax(dim=1) / a.abs().amax(dim=1).clamp_min(1e-30)).max().item()
 
 
+def _finite(e, what, trail):
+    torch.cuda.synchronize()
+    bad = ~torch.isfinite(e.tiles_view())
+    trail.append(what)
+    if not hasattr(e, "_snap"):
+        e._snap = {k: v.clone() for k, v in list(e.tens.items()) + [("gmap", e.gmap), ("cmap", e.cmap)]
+                   if torch.is_tensor(v)}
+    if bool(bad.any()):
+        now = dict(e.tens, gmap=e.gmap, cmap=e.cmap)
+        changed = [k for k, v in e._snap.items() if not torch.equal(v, now[k])]
+        pool = [int((~torch.isfinite(b)).sum()) for b in e.pool]
+        raise AssertionError(f"non-finite values {int(bad.sum())} first (f, tile, j, i) "
+                             f"{torch.nonzero(bad)[:4].tolist()} at: " + " | ".join(trail)
+                             + f"; tables changed since construction: {changed}; non-finite per pool buffer {pool}")
+
+
 def _pair(name, N, t, dtype, integ="ssprk3", ranks=1, block=(16, 16)):
     grid = CubedSphereGrid(N)
     L = TileLayout(N, t, ranks, ng=PHYS[name]().halo)
@@ -51,8 +67,15 @@ def _pair(name, N, t, dtype, integ="ssprk3", ranks=1, block=(16, 16)):
 @pytest.mark.parametrize("t", [1, 2])
 def test_stage_fp64_matches_reference(name, t):
     ref, hip = _pair(name, 24, t, torch.float64)
-    ref.step(4)
-    hip.step(4)
+    # a non-finite value says at which point it appeared (construction of
+    # either engine, or which step of which engine), and with what dt
+    trail = []
+    for nm, e in (("reference", ref), ("hip", hip)):
+        _finite(e, f"{nm} after construction", trail)
+    for nm, e in (("reference", ref), ("hip", hip)):
+        for k in range(4):
+            e.step(1)
+            _finite(e, f"{nm} after step {k + 1} (dt {e.dt!r})", trail)
     torch.cuda.synchronize()
     assert _relerr(ref, hip) < 1e-11
 

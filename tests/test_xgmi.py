@@ -171,3 +171,27 @@ def test_xgmi_multiprocess_one_gpu_march():
     for f in range(4):
         glob = assemble_global(L, {r: np.load(os.path.join(out, f"r{r}.npy"))[f] for r in range(world)})
         assert np.array_equal(glob, single.global_field(f)), f
+
+
+def test_ring_memory_is_pooled_and_zeroed():
+    """Uncached ring memory stays with the process: a freed ring is reused by
+    the next ring that fits (the allocation zeroes it; handing it back with hipFree was
+    followed by corrupted fresh allocations, profiles/r4_ring)."""
+    import ctypes
+    from stsphere.ops import native
+    from stsphere.ops.xgmi import _declare
+    L = _declare(native.require_native())
+    nb = 3 << 20
+    a = ctypes.c_void_p()
+    assert L.stsp_xg_alloc(ctypes.c_size_t(nb), ctypes.byref(a)) == 0
+    ta = torch.cuda.ByteTensor(1)   # keep torch's allocator busy in between
+    L.stsp_xg_free(a)
+    assert L.stsp_xg_free(a) == -1                 # a second free is refused
+    b = ctypes.c_void_p()
+    assert L.stsp_xg_alloc(ctypes.c_size_t(nb // 2), ctypes.byref(b)) == 0
+    assert b.value == a.value                      # the free ring is reused
+    st = (ctypes.c_longlong * 4)()
+    L.stsp_xg_pool(st)
+    assert st[0] >= 1 and st[2] >= nb
+    L.stsp_xg_free(b)
+    del ta
