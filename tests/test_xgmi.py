@@ -184,7 +184,7 @@ def test_ring_memory_is_pooled_and_zeroed():
     nb = 3 << 20
     a = ctypes.c_void_p()
     assert L.stsp_xg_alloc(ctypes.c_size_t(nb), ctypes.byref(a)) == 0
-    ta = torch.cuda.ByteTensor(1)   # keep torch's allocator busy in between
+    ta = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")   # an ordinary allocation in between
     L.stsp_xg_free(a)
     assert L.stsp_xg_free(a) == -1                 # a second free is refused
     b = ctypes.c_void_p()
