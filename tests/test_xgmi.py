@@ -117,7 +117,8 @@ def test_xgmi_loopback_march_matches_single(N, t, dtype):
     xg.close()
 
 
-def _worker(rank, world, port, N, t, steps, outdir, block=None):
+def _worker(rank, world, port, N, t, steps, outdir, block=None, rounds=1):
+    import ctypes
     import torch.distributed as dist
     from stsphere.ops.native_runtime import NativeStepper
     from stsphere.ops.xgmi import XgmiHalo
@@ -127,17 +128,26 @@ def _worker(rank, world, port, N, t, steps, outdir, block=None):
     try:
         L = TileLayout(N, t, world, ng=2)
         dev = torch.device("cuda:0")
-        e = Engine(ShallowWater("tc5"), L, rank, device=dev, backend="hip", dt=200.0, block=block,
-                   transport=NativeBuffers(L.plan(rank), 4, torch.float64, dev))
-        xg = XgmiHalo(e, timeout_s=5.0)
-        ns = NativeStepper(e, use_graph=True, steps_per_graph=5, xgmi=xg)
-        ns.run(steps)
-        torch.cuda.synchronize()
-        ns.check()
-        np.save(os.path.join(outdir, f"r{rank}.npy"), e.tiles_view().cpu().numpy())
-        dist.barrier()
-        ns.close()
-        xg.close()
+        held = []
+        for _ in range(rounds):
+            # rounds > 1: the next exchange reuses this process's pooled ring
+            # and the peers open its IPC handle again
+            e = Engine(ShallowWater("tc5"), L, rank, device=dev, backend="hip", dt=200.0, block=block,
+                       transport=NativeBuffers(L.plan(rank), 4, torch.float64, dev))
+            xg = XgmiHalo(e, timeout_s=5.0)
+            ns = NativeStepper(e, use_graph=True, steps_per_graph=5, xgmi=xg)
+            ns.run(steps)
+            torch.cuda.synchronize()
+            ns.check()
+            np.save(os.path.join(outdir, f"r{rank}.npy"), e.tiles_view().cpu().numpy())
+            dist.barrier()
+            ns.close()
+            xg.close()
+            st = (ctypes.c_longlong * 4)()
+            xg._lib.stsp_xg_pool(st)
+            held.append(int(st[0]))
+            dist.barrier()
+        assert len(set(held)) == 1, held          # no new ring after the first round
     finally:
         dist.destroy_process_group()
 
@@ -147,6 +157,22 @@ def test_xgmi_multiprocess_one_gpu(world, t):
     N, steps = 24, 10
     out = tempfile.mkdtemp()
     mp.spawn(_worker, args=(world, _free_port(), N, t, steps, out), nprocs=world, join=True)
+    g = CubedSphereGrid(N)
+    single = Engine(ShallowWater("tc5"), TileLayout(N, t, 1, ng=2), grid=g, device="cuda", backend="hip", dt=200.0)
+    single.step(steps)
+    L = TileLayout(N, t, world, ng=2)
+    for f in range(4):
+        glob = assemble_global(L, {r: np.load(os.path.join(out, f"r{r}.npy"))[f] for r in range(world)})
+        assert np.array_equal(glob, single.global_field(f)), f
+
+
+def test_xgmi_multiprocess_rings_reused():
+    """Two exchanges one after the other in the same two processes: the second
+    runs on the pooled rings (peers reopen the same IPC handles) and still
+    equals the one-rank run bit for bit."""
+    N, t, world, steps = 24, 2, 2, 6
+    out = tempfile.mkdtemp()
+    mp.spawn(_worker, args=(world, _free_port(), N, t, steps, out, None, 2), nprocs=world, join=True)
     g = CubedSphereGrid(N)
     single = Engine(ShallowWater("tc5"), TileLayout(N, t, 1, ng=2), grid=g, device="cuda", backend="hip", dt=200.0)
     single.step(steps)
