@@ -314,9 +314,12 @@ def main():
             xg = fk if world > 1 else None
             spl = a.steps_per_launch
             if spl == 0:
-                # several steps per launch (in-kernel producer waits) need every block resident
+                # several steps per launch (in-kernel producer waits) need every block resident;
+                # the longest even launch that divides the timed steps (each launch boundary
+                # costs ~18 us of ramp: 300 steps in one launch 12.05 us/step against 12.09-12.18
+                # in 60-step launches, profiles/r4_spl/)
                 cus = _rank_cus(device)
-                spl = max([k for k in range(2, 65, 2) if a.steps % k == 0], default=1) if fk.plan.nb <= cus else 1
+                spl = max([k for k in range(2, 513, 2) if a.steps % k == 0], default=1) if fk.plan.nb <= cus else 1
             info["steps_per_launch"] = spl
             info["fused_B"] = fk.plan.B
             runner = NativeStepper(eng, use_graph=True, steps_per_graph=spg, fused=fk, steps_per_launch=spl,
