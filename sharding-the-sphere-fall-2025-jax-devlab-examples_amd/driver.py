@@ -396,8 +396,10 @@ class Solver:
         spl = c.steps_per_launch
         if spl <= 0:
             k = max(1, chunk)
-            divs = [s for s in range(2, 41, 2) if k % s == 0]
-            spl = max(divs) if divs else (min(40, k - k % 2) if k >= 2 else 1)
+            # the longest even launch dividing the chunk (each launch boundary
+            # costs ~18 us of ramp, profiles/r4_spl/)
+            divs = [s for s in range(2, 513, 2) if k % s == 0]
+            spl = max(divs) if divs else (min(512, k - k % 2) if k >= 2 else 1)
         if spl > 1 and spl % 2:
             raise ValueError("runtime.steps_per_launch must be even")
         return True, spl
