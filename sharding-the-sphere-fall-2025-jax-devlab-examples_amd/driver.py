@@ -362,7 +362,7 @@ class Solver:
             return c.graph
         return self.mode == "spmd" and self.comm in ("xgmi", "rccl")
 
-    def _fused_plan(self, chunk: int):
+    def _fused_plan(self, chunks):
         """(use the fused step, steps per launch) for this run.  The fused
         SSP-RK3 step (ops/fused.py) is the flagship path: one launch advances
         a rank by several steps (every block resident, in-launch hand-offs), the
@@ -375,8 +375,10 @@ class Solver:
         e = self.engines[0]
         if c.fused == "off" or e.device.type != "cuda":
             return False, 1
-        # auto: one GPU; several ranks (the xGMI ring inside the fused kernel) on request
-        if not (self.mode == "single" or (self.mode == "spmd" and self.comm == "xgmi" and c.fused == "on")):
+        # one GPU, or SPMD ranks with the direct xGMI exchange (the ring inside
+        # the fused kernel); auto takes the multi-rank fused step when every
+        # block of the rank's share is resident (checked below)
+        if not (self.mode == "single" or (self.mode == "spmd" and self.comm == "xgmi")):
             if c.fused == "on":
                 raise ValueError(f"runtime.fused = on needs one GPU or the xgmi exchange (mode {self.mode}, "
                                  f"comm {self.comm})")
@@ -395,20 +397,27 @@ class Solver:
             return True, 1                     # one step per launch (blocks not all resident)
         spl = c.steps_per_launch
         if spl <= 0:
-            k = max(1, chunk)
-            # the longest even launch dividing the chunk (each launch boundary
-            # costs ~18 us of ramp, profiles/r4_spl/)
-            divs = [s for s in range(2, 513, 2) if k % s == 0]
-            spl = max(divs) if divs else (min(512, k - k % 2) if k >= 2 else 1)
+            # the longest even launch dividing EVERY chunk length of the run
+            # (each launch boundary costs ~18 us of ramp, profiles/r4_spl/); a
+            # run whose chunks share no even divisor launches its longest even
+            # part per chunk, the rest through the remainder path (its
+            # descriptors are built and primed by prepare())
+            lens = [max(1, int(k)) for k in (chunks if isinstance(chunks, (list, tuple)) else [chunks])]
+            g = 0
+            for k in lens:
+                g = math.gcd(g, k)
+            divs = [s for s in range(2, 513, 2) if g % s == 0]
+            k0 = min(lens)
+            spl = max(divs) if divs else (min(512, k0 - k0 % 2) if k0 >= 2 else 1)
         if spl > 1 and spl % 2:
             raise ValueError("runtime.steps_per_launch must be even")
         return True, spl
 
-    def _make_runner(self, chunk: int = 20):
+    def _make_runner(self, chunks=(20,)):
         from .ops.native_runtime import NativeStepper, create_nccl_comm
         e = self.engines[0]
         c = self.cfg.runtime
-        use_fused, spl = self._fused_plan(chunk)
+        use_fused, spl = self._fused_plan(list(chunks))
         self.fused = None
         if use_fused:
             from .ops.fused import FusedKernel, fused_block, rank_cus
@@ -538,12 +547,11 @@ class Solver:
                     p += k * SUB
                     it += 1
                 if self.runner is None:
-                    self.runner = self._make_runner(chunk=lens[0])
+                    self.runner = self._make_runner(chunks=lens)
                 per = self.runner.period
                 self.runner.graph_periods = max(1, min(max(lens), 512) // per)
                 for k in lens[:8]:
-                    if k >= per:
-                        self.runner.prepare(k)
+                    self.runner.prepare(k)      # chunks shorter than a period: their remainder launch
             if deferred and ("watchdog" in iv or "metrics" in iv):
                 self._warm_checks()
             self._sync()
@@ -612,6 +620,11 @@ class Solver:
         with ph("drain"):
             self._sync()
             pending.close()
+            if self.runner is not None:
+                # a producer wait or xGMI poll that timed out sets the kernel's
+                # error word and the kernel carries on with stale cells: never
+                # report such a run
+                self.runner.check()
         wall = time.perf_counter() - wall0
         summary = {"steps": nsteps, "steps_run": done, "wall_s": wall, "setup_s": ph.times.get("setup", 0.0),
                    "sim_days": self.time / DAY,
@@ -714,20 +727,33 @@ class Solver:
             self._wd_pending = None
             ok = self.all_finite()
             if prev is not None:
-                prev[0].synchronize()
-                ok = ok and bool(prev[1].item())
+                ok = self._wd_result(prev) and ok
             return ok
-        flag = torch.stack([torch.isfinite(e.tiles_view()).all() for e in self.engines]).all()
-        h = torch.empty((), dtype=torch.bool, pin_memory=True)
-        h.copy_(flag, non_blocking=True)
+        # [finite, no kernel error word set]: the error words of the fused step's
+        # producer waits and the xGMI polls travel in the same pinned copy, so a
+        # timed-out wait (the kernel then computes on stale cells) is seen one
+        # interval late like a non-finite state, and raises
+        finite = torch.stack([torch.isfinite(e.tiles_view()).all() for e in self.engines]).all()
+        errs = self.runner.err_words() if self.runner is not None else []
+        clean = torch.stack([(w[0] == 0) for w in errs]).all() if errs else torch.ones_like(finite)
+        h = torch.empty(2, dtype=torch.bool, pin_memory=True)
+        h.copy_(torch.stack([finite, clean]), non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         prev = getattr(self, "_wd_pending", None)
         self._wd_pending = (ev, h)
         if prev is None:
             return True
+        return self._wd_result(prev)
+
+    def _wd_result(self, prev) -> bool:
+        """Finite flag of a deferred watchdog copy; raises if a kernel error
+        word was set (not a numerical failure: no rollback)."""
         prev[0].synchronize()
-        return bool(prev[1].item())
+        if not bool(prev[1][1].item()):
+            self.runner.check()
+            raise RuntimeError("kernel error word set during the run")
+        return bool(prev[1][0].item())
 
     def set_dt(self, dt: float) -> None:
         self.dt = dt

@@ -30,7 +30,7 @@ VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgc": ["-DSTSP_XG_TAG=0"],
                  "pnotab": ["-DSTSP_PROBE_NOTAB=1"], "pnoslot": ["-DSTSP_PROBE_NOSLOT=1"],
                  "ownw0": ["-DSTSP_OWN_SKIP0=0"], "w9": ["-DSTSP_W10=0"], "swsqrt": ["-DSTSP_HW_SQRT=0"],
                  "selslope": ["-DSTSP_SIGN_SLOPE=0"], "wpe6": ["-DSTSP_WPE=6"], "wpe7": ["-DSTSP_WPE=7"],
-                 "ginl": ["-DSTSP_FUSED_GINL=1"], "cwlast": ["-DSTSP_FUSED_CW0=0"], "pair1": ["-DSTSP_FUSED_PAIR=1"],
+                 "fp_alledge": ["-DSTSP_FPROBE_ALLEDGE=1"], "fp_nogwait": ["-DSTSP_FPROBE_NOGWAIT=1"],
                  "mprobe": ["-DSTSP_MARCH_PROBE_NOWE=1", "-DSTSP_MARCH_WPE64=3", "-DSTSP_MARCH_WPE32=5"]}
 
 

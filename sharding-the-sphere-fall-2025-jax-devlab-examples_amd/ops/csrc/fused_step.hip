@@ -44,31 +44,17 @@
 #include <type_traits>
 
 
-// STSP_FUSED_GINL=1: faces next to a panel-edge line evaluate their ghost
-// stencil neighbours themselves (index pair + weight from LDS); 0 (default): a
-// ghost pass per stage writes them into the window's ghost area first.  At
-// C96 the inline form saved ~0.9k cycles in the corner blocks' stage-1 faces
-// but cost the edge blocks ~0.7k in stage 3 (twice the LDS reads in the near
-// waves): 13.88 against 13.66 us/step (profiles/r4_b8)
-#ifndef STSP_FUSED_GINL
-#define STSP_FUSED_GINL 0
+// Timing-only probe builds (ops/build.py variants fp_alledge / fp_nogwait):
+// every block runs the panel-edge face body (numerics unchanged), or near
+// faces skip the wait for the ghost pass (numerics wrong: timing only)
+#ifndef STSP_FPROBE_ALLEDGE
+#define STSP_FPROBE_ALLEDGE 0
 #endif
-
-#ifndef STSP_FUSED_CW0
-#define STSP_FUSED_CW0 1
-#endif
-// STSP_FUSED_PAIR=1 (pair1 variant): stages 2 and 3 compute two faces of a
-// line pair per task (the shared cell's slope once); 0 (default): one face per
-// task.  The pair form raises the multi-step kernel's VGPR spills at B = 16
-// from 5 to 54 (fp64, 168 VGPRs)
-#ifndef STSP_FUSED_PAIR
-#define STSP_FUSED_PAIR 0
+#ifndef STSP_FPROBE_NOGWAIT
+#define STSP_FPROBE_NOGWAIT 0
 #endif
 
 namespace {
-
-constexpr bool GINL = STSP_FUSED_GINL != 0;
-constexpr bool PAIR = STSP_FUSED_PAIR != 0 && !GINL;
 
 // cube-corner face table widths (ops/fused.py::corner_tables)
 constexpr int CT_INTS = 16, CT_FLAGS = 12, CG_VALS = 8;
@@ -96,6 +82,8 @@ struct FD {
   static constexpr int NT = NU <= 768 ? 768 : 1024;
   static_assert(NU <= NT && W * W <= 2 * NT, "owner threads for every updated cell");
   static_assert(GMAX <= NT, "one fix-up thread per ghost entry");
+  static_assert(2 * (B + 4 * (NS - 2)) * (B + 4 * (NS - 2) + 1) <= 32 * 64 && 2 * H1 * (H1 + 1) <= 32 * 64 + 64 * 64,
+                "face passes per stage fit the 32-entry pass table");
   static constexpr int CMAX = 32;
 };
 
@@ -193,15 +181,21 @@ struct FArgs {
   int nsteps;
   const int* prod;        // [nb][PM] producer blocks, -1 padded
   int PM;
+  const unsigned* sched;  // [nb][3 stages][17]: per wave (16) bit p = the wave runs face pass p (faces 64 p ..
+                          // 64 p + 63); word 16 bit p = pass p holds a face next to a panel-edge line
+  const T* nrmf;          // [nb][3][NFL] per-face normals of panel-edge blocks (PFN builds)
 };
 
-// phase stamp (profiling): lane 0 of every wave, when a.stamps is set
+// phase stamp (profiling): lane 0 of every wave, when a.stamps is set;
+// stamps[block][wave < 16][FST_W]: slots 0-15 clocks, 16 HW_ID (SIMD, CU, SE
+// of the wave), 17 XCC_ID (the XCD), 18 the dispatch-order blockIdx.x
+constexpr int FST_W = 32;
 #define FSTAMP(k)                                                                                \
   do {                                                                                           \
     if (a.stamps) {                                                                              \
       __builtin_amdgcn_sched_barrier(0);                                                         \
       if ((threadIdx.x & 63) == 0)                                                               \
-        a.stamps[((long)bid * 16 + (threadIdx.x >> 6)) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+        a.stamps[((long)bid * 16 + (threadIdx.x >> 6)) * FST_W + (k)] = __builtin_amdgcn_s_memtime(); \
       __builtin_amdgcn_sched_barrier(0);                                                         \
     }                                                                                            \
   } while (0)
@@ -210,7 +204,7 @@ struct FArgs {
 #define FSTAMP_RT(k)                                                                             \
   do {                                                                                           \
     if (a.stamps && (threadIdx.x & 63) == 0)                                                     \
-      a.stamps[((long)bid * 16 + (threadIdx.x >> 6)) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+      a.stamps[((long)bid * 16 + (threadIdx.x >> 6)) * FST_W + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 // Panel cell (g, I, J) at extended-panel coordinates (X, Y) of face f; false
@@ -267,13 +261,21 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   using D = FD<NS, B>;
   constexpr int W = D::W, WS = D::WS, WW = D::WW, GB = D::GB, R = D::R, L1 = D::L1, H1 = D::H1;
   constexpr int NFX = D::NFX, NFL = D::NFL, NT = D::NT, NU = D::NU;
-  constexpr int NN = 2 * 5 * 3 * (W + 1);
+  // PFN: panel-edge blocks take each face's normal from a per-face table
+  // (FArgs::nrmf, host-built from the region tables) and learn from the host
+  // which face passes hold a face next to a panel-edge line; the other passes
+  // run the interior body (no region test, no neighbour codes).  Where the
+  // per-face table does not fit the LDS (fp64, B >= 18) the region tables stay.
+  constexpr bool PFN = sizeof(T) == 4 || B <= 16;
+  constexpr int NRG = PFN ? 1 : 5;                // regions in the line-normal table
+  constexpr int NN = 2 * NRG * 3 * (W + 1);
   // primitives h, vx, vy, vz and sound speed of the window cells, then (fields
   // 0-3) the values of the block's ghost entries, refreshed before each stage's faces
   __shared__ T s_w[5 * WW];
   __shared__ T s_fl[4][NFL];               // face fluxes (stage-1 face set, compact)
   __shared__ T s_len[NFL];                 // face lengths
-  __shared__ T s_nrm[2][5][3][W + 1];      // line normals per region, component-major
+  __shared__ T s_nrm[2][NRG][3][W + 1];    // line normals per region, component-major
+  __shared__ T s_nrmf[PFN ? 3 * NFL : 1];  // PFN: per-face normals of edge blocks, component-major
   __shared__ unsigned long long s_code[W * W];   // neighbour codes (edge blocks)
   __shared__ short s_gs[D::GMAX][2];       // ghost entry: interpolation pair (LDS window index)
   __shared__ T s_gt[D::GMAX];              //              and weight
@@ -304,6 +306,12 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   const T* wf = &s_w[0];
   FSTAMP(0);
   FSTAMP_RT(14);
+  if (a.stamps && (tid & 63) == 0) {
+    unsigned long long* sp = a.stamps + ((long)bid * 16 + (tid >> 6)) * FST_W;
+    sp[16] = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
+    sp[17] = __builtin_amdgcn_s_getreg((31 << 11) | 20);    // HW_REG_XCC_ID
+    sp[18] = blockIdx.x;
+  }
 
   // ---- 0. prologue: every global load first, then the LDS writes --------------
   // Per block only the state is unique data: the geometry comes from
@@ -350,10 +358,9 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       gtv = a.gw[(long)bid * a.G + tid];
     }
     ncor = a.ccnt[bid];
-    // ghost waves: right after the corner wave (the last ones before it with
-    // STSP_FUSED_CW0=0; see the face loop)
-    gbase = STSP_FUSED_CW0 ? 64 * (ncor > 0 ? 1 : 0) : NT - 64 * (ncor > 0 ? 1 : 0) - 64 * ngw;
-    if (gbase < 0) gbase = 0;
+    // ghost waves: right after the corner wave (wave 0 when the block has
+    // cube-corner faces); ops/fused.py::pass_schedule knows this layout
+    gbase = 64 * (ncor > 0 ? 1 : 0);
     if (tid < ncor) {
       const int* ct = a.ctab + ((long)bid * a.C + tid) * CT_INTS;
       const T* cg = a.cgf + ((long)bid * a.C + tid) * CG_VALS;
@@ -362,6 +369,14 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
 #pragma unroll
       for (int k = 0; k < CG_VALS; ++k) cgv[k] = cg[k];
     }
+  }
+  // this wave's face passes per stage (bit p: faces 64 p .. 64 p + 63), in SGPRs
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  unsigned pmask[3], nmask[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    pmask[s] = __builtin_amdgcn_readfirstlane(a.sched[((long)bid * 3 + s) * 17 + wv]);
+    nmask[s] = __builtin_amdgcn_readfirstlane(a.sched[((long)bid * 3 + s) * 17 + 16]);
   }
   // face lengths of the stage-1 face set: region of the face's lower cell (else
   // upper), its panel-local edge through the region map, the shared length table
@@ -387,14 +402,24 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   // line normals: one panel -> the panel's own lines from the tangents (thread
   // (axis, line) < 2 (W + 1)), else the block's table (thread per value)
   T nrv = T(0);
-  const bool nr_ld = flags == 1 ? tid < 2 * (W + 1) : tid < NN;
+  const bool nr_ld = flags == 1 ? tid < 2 * (W + 1) : (!PFN && tid < NN);
   T nrv2 = T(0);                                         // a second table value (NN > NT)
   if (nr_ld) {
     if (flags == 1) nrv = a.tane[(tid < W + 1 ? X0 + tid : Y0 + tid - (W + 1))];
     else nrv = a.nrm[(long)bid * NN + tid];
   }
   static_assert(NN <= 2 * NT, "line-normal table: two values per thread at most");
-  if (NN > NT && flags != 1 && tid + NT < NN) nrv2 = a.nrm[(long)bid * NN + tid + NT];
+  if (!PFN && NN > NT && flags != 1 && tid + NT < NN) nrv2 = a.nrm[(long)bid * NN + tid + NT];
+  // PFN, panel-edge block: the per-face normals (component-major, stage-1 face slots)
+  constexpr int NPF = PFN ? (3 * NFL + NT - 1) / NT : 1;
+  T nfv[NPF];
+  if (PFN && flags != 1) {
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int j = tid + k * NT;
+      nfv[k] = j < 3 * NFL ? a.nrmf[(long)bid * 3 * NFL + j] : T(0);
+    }
+  }
   // own window cell: state (+ geometry for the cells stage 1 updates)
   T Q[4];
   T iA = T(0), r0 = T(0), r1 = T(0), r2 = T(0), gb0 = T(0), gb1 = T(0), gb2 = T(0), S0 = T(0), S1 = T(0),
@@ -496,7 +521,14 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       (&s_nrm[0][0][0][0])[tid] = nrv;
     }
   }
-  if (NN > NT && flags != 1 && tid + NT < NN) (&s_nrm[0][0][0][0])[tid + NT] = nrv2;
+  if (!PFN && NN > NT && flags != 1 && tid + NT < NN) (&s_nrm[0][0][0][0])[tid + NT] = nrv2;
+  if (PFN && flags != 1) {
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int j = tid + k * NT;
+      if (j < 3 * NFL) s_nrmf[j] = nfv[k];
+    }
+  }
   if (edge) {
     if (owner) s_code[v * W + u] = cdv;
     if (tid < a.G) { s_gs[tid][0] = (short)gs0; s_gs[tid][1] = (short)gs1; s_gt[tid] = gtv; }
@@ -557,23 +589,33 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       __builtin_amdgcn_s_sleep(0);
   };
   // ---- faces ---------------------------------------------------------------
-  // EDGE (blocks with a side region): the face's normal is that of the lower
-  // cell's region; only faces within one line of a panel edge line (a few
-  // lanes) take their stencil neighbours from the codes (window cell or ghost
-  // entry) -- a short divergent branch instead of a second face body.
-  auto face = [&](bool ax, int fu, int fv, int k, auto edge_c) {
-    constexpr bool EDGE = decltype(edge_c)::value;
+  // MODE 0: interior body (line normals).  Blocks with a side region: the
+  // face's normal is that of the lower cell's region, and only faces within
+  // one line of a panel edge line (a few lanes) take their stencil neighbours
+  // from the codes (window cell or ghost entry).  PFN builds split that work
+  // by face pass (host flag): MODE 1 = no face of the pass is near an edge
+  // line (the interior body with per-face normals: no codes, no conditional
+  // loads), MODE 2 = the pass holds near faces (codes, ghost wait).  Without
+  // PFN every face of an edge block runs MODE 2 with the region tables.
+  auto face = [&](bool ax, int fu, int fv, int k, auto mode_c) {
+    constexpr int MODE = decltype(mode_c)::value;
+    constexpr bool EDGE = MODE == 2;
     const int st = ax ? WS : 1;
     const int fslot = ax ? NFX + (k - L1) * H1 + (fu - L1) : (fv - L1) * (H1 + 1) + (k - L1);
     const int ib = fv * WS + fu, ia = ib - st;
     int iam = ia - st, iap = ib, ibm = ia, ibp = ib + st, ra = 0;
     bool wnear = false;                                    // some lane of this wave is near an edge line
-    int gq[4] = {-1, -1, -1, -1};                          // ghost entries at am, ap, bm, bp (GINL)
     if constexpr (EDGE) {
       const int e0 = ax ? ky0 : kx0, e1 = ax ? ky1 : kx1;
-      const bool near = (unsigned)(k - e0 + 1) <= 2u || (unsigned)(k - e1 + 1) <= 2u;
-      wnear = __builtin_amdgcn_ballot_w64(near) != 0;
-      if (!GINL && wnear) gwait();                         // this wave reads ghost entries
+      bool near = false;
+      if constexpr (PFN) {
+        wnear = true;                                      // the host flagged this face pass
+        near = (unsigned)(k - e0 + 1) <= 2u || (unsigned)(k - e1 + 1) <= 2u;
+      } else {
+        near = (unsigned)(k - e0 + 1) <= 2u || (unsigned)(k - e1 + 1) <= 2u;
+        wnear = __builtin_amdgcn_ballot_w64(near) != 0;
+      }
+      if (wnear && !STSP_FPROBE_NOGWAIT) gwait();          // this wave reads ghost entries
       if (near) {
         const int sm = ax ? 2 : 0;                         // side index of -axis; +axis = sm + 1
         const int ci = fv * W + fu, cj = ci - (ax ? W : 1);  // window indices of b and a
@@ -581,167 +623,43 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         const int eam = ncode(ca, sm), eap = ncode(ca, sm + 1);
         const int ebm = ncode(cb, sm), ebp = ncode(cb, sm + 1);
         if (eam == -3 || ebm == -3) return;                // a cell is missing: a corner face
-        if constexpr (GINL) {
-          gq[0] = eam; gq[1] = eap; gq[2] = ebm; gq[3] = ebp;
-        } else {
-          if (eam >= 0) iam = GB + eam;
-          if (eap >= 0) iap = GB + eap;
-          if (ebm >= 0) ibm = GB + ebm;
-          if (ebp >= 0) ibp = GB + ebp;
-        }
-      }
-      ra = fregion(X0 + fu - (ax ? 0 : 1), Y0 + fv - (ax ? 1 : 0), N);
-      ra = ra < 0 ? 0 : ra;                                // a missing: junk face, never read
-    }
-    T wl[4], wr[4], cl[5], cr[5];
-#pragma unroll
-    for (int f = 0; f < 5; ++f) { cl[f] = wf[f * WW + ia]; cr[f] = wf[f * WW + ib]; }
-    if constexpr (EDGE && GINL) {
-      if (wnear) {
-        // the waves with a face next to a panel-edge line evaluate their ghost
-        // stencil neighbours here, with the ghost pass's formula x0 + t (x1 - x0)
-        // (a plain neighbour is the pair (i, i) with t = 0): no ghost pass, no
-        // wait on it, one LDS round trip for the pair instead
-        const int ix[4] = {iam, iap, ibm, ibp};
-        int j0[4], j1[4];
-        T tw[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int e = gq[q];
-          j0[q] = e >= 0 ? (int)s_gs[e][0] : ix[q];
-          j1[q] = e >= 0 ? (int)s_gs[e][1] : ix[q];
-          tw[q] = e >= 0 ? s_gt[e] : T(0);
-        }
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          T x[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const T x0 = wf[f * WW + j0[q]];
-            x[q] = x0 + tw[q] * (wf[f * WW + j1[q]] - x0);
-          }
-          wl[f] = cl[f] + half_slope<LIM>(cl[f] - x[0], x[1] - cl[f]);
-          wr[f] = cr[f] - half_slope<LIM>(cr[f] - x[2], x[3] - cr[f]);
-        }
-      }
-    }
-    if (!(EDGE && GINL) || !wnear) {
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        const T am = wf[f * WW + iam], bp = wf[f * WW + ibp];
-        T ap = cr[f], bm = cl[f];
-        if constexpr (EDGE && !GINL) {
-          if (wnear) {                                     // wave-uniform: most waves skip these loads
-            ap = wf[f * WW + iap];
-            bm = wf[f * WW + ibm];
-          }
-        }
-        wl[f] = cl[f] + half_slope<LIM>(cl[f] - am, ap - cl[f]);
-        wr[f] = cr[f] - half_slope<LIM>(cr[f] - bm, bp - cr[f]);
-      }
-    }
-    const T* m = &s_nrm[ax ? 1 : 0][ra][0][k];
-    T fl[4];
-    swe_flux<T>(wl, wr, cl, cr, m[0], m[W + 1], m[2 * (W + 1)], s_len[fslot], a.g, fl);
-#pragma unroll
-    for (int f = 0; f < 4; ++f) s_fl[f][fslot] = fl[f];
-  };
-  // Two faces in a row along one line direction, lines k and k + 1 (stages
-  // 2 and 3, PAIR): they share cell k, whose slope (the right state of face k,
-  // the left state of face k + 1) is computed once from the same operands the
-  // single-face body uses for it (its own codes), so the pair is bitwise the
-  // two single faces; 3 slopes and 5 cells instead of 4 and 8.  two = false:
-  // face k alone (the last line of an odd count).
-  auto face2 = [&](bool ax, int fu, int fv, int k, bool two, auto edge_c) {
-    constexpr bool EDGE = decltype(edge_c)::value;
-    const int st = ax ? WS : 1;
-    const int ib = fv * WS + fu, ia = ib - st, ic = ib + st;
-    // stencil neighbours: cell a (k - 1), b (k), c (k + 1), minus / plus side
-    int iam = ia - st, iap = ib, ibm = ia, ibp = ic, icm = ib, icp = ic + st;
-    int ra = 0, rb = 0;
-    bool wnear = false, skip0 = false, skip1 = !two;
-    if constexpr (EDGE) {
-      const int e0 = ax ? ky0 : kx0, e1 = ax ? ky1 : kx1;
-      // line k or k + 1 within one line of a panel-edge line (wider is harmless: a
-      // plain neighbour's code is -1)
-      const bool near = (unsigned)(k - e0 + 2) <= 3u || (unsigned)(k - e1 + 2) <= 3u;
-      wnear = __builtin_amdgcn_ballot_w64(near) != 0;
-      if (wnear) gwait();
-      if (near) {
-        const int sm = ax ? 2 : 0;
-        const int ci = fv * W + fu, cs = ax ? W : 1;           // window (code) index of cell b
-        const unsigned long long ca = s_code[ci - cs], cb = s_code[ci], cc = two ? s_code[ci + cs] : 0ull;
-        const int eam = ncode(ca, sm), eap = ncode(ca, sm + 1);
-        const int ebm = ncode(cb, sm), ebp = ncode(cb, sm + 1);
-        const int ecm = two ? ncode(cc, sm) : -1, ecp = two ? ncode(cc, sm + 1) : -1;
-        skip0 = eam == -3 || ebm == -3;                        // a cell is missing: corner faces
-        skip1 = skip1 || ebm == -3 || ecm == -3;
         if (eam >= 0) iam = GB + eam;
         if (eap >= 0) iap = GB + eap;
         if (ebm >= 0) ibm = GB + ebm;
         if (ebp >= 0) ibp = GB + ebp;
-        if (ecm >= 0) icm = GB + ecm;
-        if (ecp >= 0) icp = GB + ecp;
       }
-      ra = fregion(X0 + fu - (ax ? 0 : 1), Y0 + fv - (ax ? 1 : 0), N);
-      ra = ra < 0 ? 0 : ra;
-      rb = fregion(X0 + fu, Y0 + fv, N);
-      rb = rb < 0 ? 0 : rb;
-    }
-    if (skip0 && skip1) return;
-    // face k first (cells a, b), keeping only b's primitives and slope for face
-    // k + 1: fewer live registers than both faces' states at once
-    T ca_[5], cb_[5], hb[4];
-#pragma unroll
-    for (int f = 0; f < 5; ++f) {
-      ca_[f] = wf[f * WW + ia];
-      cb_[f] = wf[f * WW + ib];
-    }
-    {
-      T wl0[4], wr0[4];
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        const T am = wf[f * WW + iam], bp = wf[f * WW + ibp];
-        T ap = cb_[f], bm = ca_[f];
-        if constexpr (EDGE) {
-          if (wnear) {
-            ap = wf[f * WW + iap];
-            bm = wf[f * WW + ibm];
-          }
-        }
-        wl0[f] = ca_[f] + half_slope<LIM>(ca_[f] - am, ap - ca_[f]);
-        hb[f] = half_slope<LIM>(cb_[f] - bm, bp - cb_[f]);
-        wr0[f] = cb_[f] - hb[f];
-      }
-      if (!skip0) {
-        const int fs = ax ? NFX + (k - L1) * H1 + (fu - L1) : (fv - L1) * (H1 + 1) + (k - L1);
-        const T* m = &s_nrm[ax ? 1 : 0][ra][0][k];
-        T fl[4];
-        swe_flux<T>(wl0, wr0, ca_, cb_, m[0], m[W + 1], m[2 * (W + 1)], s_len[fs], a.g, fl);
-#pragma unroll
-        for (int f = 0; f < 4; ++f) s_fl[f][fs] = fl[f];
+      if constexpr (!PFN) {
+        ra = fregion(X0 + fu - (ax ? 0 : 1), Y0 + fv - (ax ? 1 : 0), N);
+        ra = ra < 0 ? 0 : ra;                              // a missing: junk face, never read
       }
     }
-    if (skip1) return;
-    T cc_[5], wl1[4], wr1[4];
+    T wl[4], wr[4], cl[5], cr[5];
 #pragma unroll
-    for (int f = 0; f < 5; ++f) cc_[f] = wf[f * WW + ic];
+    for (int f = 0; f < 5; ++f) { cl[f] = wf[f * WW + ia]; cr[f] = wf[f * WW + ib]; }
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-      const T cp = wf[f * WW + icp];
-      T cm = cb_[f];
+      const T am = wf[f * WW + iam], bp = wf[f * WW + ibp];
+      T ap = cr[f], bm = cl[f];
       if constexpr (EDGE) {
-        if (wnear) cm = wf[f * WW + icm];
+        if (wnear) {                                       // wave-uniform: most waves skip these loads
+          ap = wf[f * WW + iap];
+          bm = wf[f * WW + ibm];
+        }
       }
-      wl1[f] = cb_[f] + hb[f];
-      wr1[f] = cc_[f] - half_slope<LIM>(cc_[f] - cm, cp - cc_[f]);
+      wl[f] = cl[f] + half_slope<LIM>(cl[f] - am, ap - cl[f]);
+      wr[f] = cr[f] - half_slope<LIM>(cr[f] - bm, bp - cr[f]);
     }
-    const int fs = ax ? NFX + (k + 1 - L1) * H1 + (fu - L1) : (fv - L1) * (H1 + 1) + (k + 1 - L1);
-    const T* m = &s_nrm[ax ? 1 : 0][rb][0][k + 1];
+    T m0, m1, m2;
+    if constexpr (MODE != 0 && PFN) {                      // per-face normal (edge block)
+      m0 = s_nrmf[fslot]; m1 = s_nrmf[NFL + fslot]; m2 = s_nrmf[2 * NFL + fslot];
+    } else {                                               // line normal of the face's region
+      const T* m = &s_nrm[ax ? 1 : 0][ra][0][k];
+      m0 = m[0]; m1 = m[W + 1]; m2 = m[2 * (W + 1)];
+    }
     T fl[4];
-    swe_flux<T>(wl1, wr1, cb_, cc_, m[0], m[W + 1], m[2 * (W + 1)], s_len[fs], a.g, fl);
+    swe_flux<T>(wl, wr, cl, cr, m0, m1, m2, s_len[fslot], a.g, fl);
 #pragma unroll
-    for (int f = 0; f < 4; ++f) s_fl[f][fs] = fl[f];
+    for (int f = 0; f < 4; ++f) s_fl[f][fslot] = fl[f];
   };
   // Stage-1 faces whose whole stencil lies in the block's own cells ("inner":
   // lines k in [R+2, R+B-2] x the block's B rows, both axes): a multi-step
@@ -758,8 +676,15 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     const bool ax = t >= NIL * B;
     const int t2 = ax ? t - NIL * B : t;
     const int k = R + 2 + t2 / B, p = R + t2 % B;
-    if (ax) face(true, p, k, k, std::false_type{});
-    else face(false, k, p, k, std::false_type{});
+    // (PFN edge blocks hold no line normals: their inner faces read the
+    // per-face table through the edge body, never near a panel-edge line)
+    if (PFN && edge) {
+      if (ax) face(true, p, k, k, std::integral_constant<int, 1>{});
+      else face(false, k, p, k, std::integral_constant<int, 1>{});
+    } else {
+      if (ax) face(true, p, k, k, std::integral_constant<int, 0>{});
+      else face(false, k, p, k, std::integral_constant<int, 0>{});
+    }
   };
   // outer face t of one axis -> (line k, position along it)
   auto outer_face = [&](int t, int& k, int& p) {
@@ -840,7 +765,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     // count themselves done in s_gdone, and only a wave with a face next to a
     // panel-edge line (or a cube-corner face) waits for the count before its
     // first ghost read; every other wave starts its faces at once.
-    if (!GINL && edge) {
+    if (edge) {
       const int ge = tid - gbase;                            // this thread's ghost entry
       if (ge >= 0 && ge < a.G) {
         const int i0 = s_gs[ge][0], i1 = s_gs[ge][1];
@@ -857,45 +782,39 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       }
       gtarget += ngw;
     }
-    // Work per wave, balanced: a stage has more regular faces than threads
-    // (C96 B = 16: 784 and 840 in stages 1 and 2), so some waves take a second
-    // round of them.  The cube-corner faces (corner blocks: a long chain of two
-    // reconstructions from the host table and one flux) run alone on wave 0,
-    // the oldest (it wins the issue arbitration: on the last wave the same
-    // chain took 4.8k cycles, profiles/r4_wb), the ghost entries on the waves
-    // after it, and the second round of regular faces on the waves after
-    // those.  Round 3 had all three on wave 0: 6.2k cycles in the corner
-    // blocks' stage-1 faces against 3.3k for the slowest interior wave
-    // (profiles/r4_tail).  STSP_FUSED_CW0=0: corner faces on the last wave.
-    // stage 1: the outer faces only; stages 2, 3 (PAIR): two faces per task
-    const int nax = s == 0 ? NOX : (PAIR ? ((nl + 1) >> 1) * nr : nx);
-#if STSP_FUSED_CW0
-    const int cw = ncor ? 1 : 0;
-    const int nreg = NT - 64 * cw, t2r = 64 * (cw + (GINL ? 0 : ngw)), nr2 = NT - t2r;   // round 2 from thread t2r
-    const bool cwave = cw && tid < 64;
-    const int tend = cwave ? 0 : 2 * nax;
-    // corner wave: one pass with task = j - 64 < 0 (corner face j); others: regular faces
-    for (int task = cwave ? tid - 64 : tid - 64 * cw, first = 1; task < tend;
-         task = first ? (tid >= t2r ? nreg + tid - t2r : tend) : task + nr2, first = 0) {
-#else
-    const bool cwave = ncor && tid >= NT - 64;
-    const int nthr = ncor ? NT - 64 : NT;
-    for (int task = cwave ? tid - NT : tid; task < (cwave ? 0 : 2 * nax); task += cwave ? 64 : nthr) {
-#endif
+    // Work per wave, balanced over the CU's four SIMDs.  A stage has more
+    // regular faces than one per thread (C96 B = 16: 784, 840 and 544 in stages
+    // 1-3 for 768 threads), the cube-corner faces (corner blocks: a long chain of
+    // two reconstructions from the host table and one flux) run on wave 0, the
+    // ghost entries on the waves after it.  The regular faces go in passes of
+    // 64 (faces 64 p .. 64 p + 63, line-major, so the few faces next to a
+    // panel-edge line fill few passes); the host's pass table (pass_schedule)
+    // gives each pass to a wave so that the SIMD groups {w, w + 4, w + 8} carry
+    // equal issue work: the corner wave and the ghost entries count too.
+    // Round 4 put the second round on the waves right after the ghost waves,
+    // i.e. on wave 4 beside the corner wave: 5 passes' work on one SIMD against
+    // 4 in interior blocks.  Stage 1: the outer faces only.
+    const int nax = s == 0 ? NOX : nx;
+    const int ntask = 2 * nax;
+    unsigned m = pmask[s];
+    for (int first = (ncor && wv == 0) ? 1 : 0; first || m;) {
+      int task;
+      bool nearp = false;
+      if (first) {                                          // the corner wave's cube-corner faces
+        task = (tid & 63) - 64;
+        first = 0;
+      } else {
+        const int pp = __builtin_ctz(m);
+        task = pp * 64 + (tid & 63);
+        nearp = (nmask[s] >> pp) & 1u;
+        m &= m - 1u;
+      }
+      if (task >= ntask) continue;
       if (task >= 0) {
         const int tf = task;
         const bool ax = tf >= nax;                           // false: x-face, true: y-face
         const int t2 = ax ? tf - nax : tf;
         int fu, fv, k, p;
-        if (PAIR && s > 0) {                                 // lines k, k + 1 of row p
-          const int c = t2 / nr, r = t2 - c * nr;
-          k = lo + 2 * c; p = lo + r;
-          const bool two = k + 1 <= hi;
-          if (!ax) { fv = p; fu = k; } else { fu = p; fv = k; }
-          if (edge) face2(ax, fu, fv, k, two, std::true_type{});
-          else face2(ax, fu, fv, k, two, std::false_type{});
-          continue;
-        }
         if (s == 0) {
           outer_face(t2, k, p);
         } else {                                             // line-major: the faces near an
@@ -904,8 +823,12 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         }
         if (!ax) { fv = p; fu = k; }                         // b = (k, fv), a = (k - 1, fv)
         else { fu = p; fv = k; }                             // b = (fu, k), a = (fu, k - 1)
-        if (edge) face(ax, fu, fv, k, std::true_type{});
-        else face(ax, fu, fv, k, std::false_type{});
+        if (edge || STSP_FPROBE_ALLEDGE) {
+          if (PFN && !nearp) face(ax, fu, fv, k, std::integral_constant<int, 1>{});
+          else face(ax, fu, fv, k, std::integral_constant<int, 2>{});
+        } else {
+          face(ax, fu, fv, k, std::integral_constant<int, 0>{});
+        }
       } else if (task + 64 < ncor) {
         // cube-corner face j: cell c's face on side_c meets cell d's face on
         // side_d; every stencil index comes from the host table (no codes, no
@@ -1090,6 +1013,9 @@ int launch_fused(const FusedDesc* d, hipStream_t s) {
   a.nsteps = d->nsteps < 1 ? 1 : d->nsteps;
   a.prod = d->prod;
   a.PM = d->PM;
+  a.sched = (const unsigned*)d->sched;
+  a.nrmf = (const T*)d->nrmf;
+  if (!a.sched || !a.nrmf) return -4;
   if (a.nsteps > 1 && (!a.prod || a.PM <= 0 || a.PM > 64 || !d->epoch || !d->err)) return -7;
   a.mdiv_n = magic_div((unsigned)d->n, (unsigned long long)d->N + 1);
   if (d->xg && (!STSP_XG_TAG || !d->recv || !d->peer_ring || !d->xpush || !d->epoch || !d->err || d->ring <= 0 ||

@@ -144,6 +144,12 @@ typedef struct FusedDesc {
   const int* prod;
   int PM;
   const int* cpush;     // [T][4][mg][mg] carried corner ghost pushes (StageDesc::cpush), nullable
+  // face-pass schedule (ops/fused.py::pass_schedule): [nb][3 stages][17] u32:
+  // per wave (16) bit p set = the wave runs pass p (faces 64 p .. 64 p + 63) of
+  // the stage, balanced over the CU's four SIMDs (waves w and w + 4 share one);
+  // word 16 bit p = pass p holds a face next to a panel-edge line
+  const unsigned* sched;
+  const void* nrmf;     // [nb][3][2 H1 (H1+1)] per-face normals of panel-edge blocks (component-major)
 } FusedDesc;
 int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stream);
 int stsp_fused_limits(int* gmax, int* cmax);

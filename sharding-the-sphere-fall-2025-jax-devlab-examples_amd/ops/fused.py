@@ -901,6 +901,197 @@ def fused_block(n: int, tiles: Optional[int] = None, cus: Optional[int] = None) 
 
 
 
+def fused_threads(B: int, ns: int = 3) -> int:
+    """Threads per workgroup of the fused kernel (fused_step.hip FD::NT)."""
+    h1 = B + 4 * (ns - 1)
+    return 768 if h1 * h1 <= 768 else 1024
+
+
+def stage_face_counts(B: int, ns: int = 3) -> List[int]:
+    """Regular face tasks per stage after the producer wait: stage 1 only its
+    outer faces (the inner ones run during the wait), then the full face sets
+    of the shrinking squares (fused_step.hip: NOX, nx)."""
+    h1 = B + 4 * (ns - 1)
+    nil = B - 3
+    out = [2 * (h1 * (h1 + 1) - nil * B)]
+    for s in range(1, ns):
+        nr = B + 4 * (ns - 1 - s)
+        out.append(2 * nr * (nr + 1))
+    return out
+
+
+PASS_SLOTS = 32    # face passes per stage in the kernel's table
+
+
+def pass_schedule(B: int, ncorner: np.ndarray, edge: np.ndarray, G: int, ns: int = 3,
+                  weights: Optional[str] = None) -> np.ndarray:
+    """[nb, ns, PASS_SLOTS] uint8: the wave that runs face pass p (faces 64 p
+    .. 64 p + 63) of stage s, per block (``pass_masks`` turns it into the
+    kernel's per-wave bit masks).
+
+    The waves of a workgroup share the CU's four SIMDs as the groups
+    {w, w + 4, w + 8, ...} (cyclic dispatch; tools/fused_probe.py records the
+    SIMD of every wave), and a wave64 fp64 VALU instruction holds its SIMD for
+    4 cycles, so a face phase lasts as long as its busiest SIMD group issues.
+    Greedy balance: every pass goes to the least-loaded group, inside it to the
+    least-loaded wave.  Loads in quarter passes: a regular pass 4, the cube-
+    corner wave (wave 0 of a corner block) ``corner``, each ghost-entry wave
+    (the waves after it in a panel-edge block) ``ghost``.  ``weights`` (or
+    STSP_FUSED_SCHED) = "corner:ghost" (default "8:1"), or "legacy": round 4's
+    placement (one pass per wave in wave order, then the second round from the
+    wave after the ghost waves), kept for A/B runs."""
+    import os
+    weights = weights or os.environ.get("STSP_FUSED_SCHED", "8:1")
+    nt = fused_threads(B, ns)
+    nw = nt // 64
+    counts = stage_face_counts(B, ns)
+    nb = len(ncorner)
+    out = np.zeros((nb, ns, PASS_SLOTS), dtype=np.uint8)
+    ngw = -(-G // 64) if G > 0 else 0
+    cache = {}
+    for b in range(nb):
+        cw = 1 if ncorner[b] > 0 else 0
+        gw = ngw if edge[b] else 0
+        key = (cw, gw)
+        if key not in cache:
+            tab = np.zeros((ns, PASS_SLOTS), dtype=np.uint8)
+            for s, nt_s in enumerate(counts):
+                npass = -(-nt_s // 64)
+                assert npass <= PASS_SLOTS
+                if weights == "legacy":
+                    first = nw - cw
+                    for p in range(npass):
+                        tab[s, p] = p + cw if p < first else cw + gw + (p - first) % (nw - cw - gw)
+                    continue
+                wc, wg = (int(x) for x in weights.split(":"))
+                wl = [0] * nw
+                if cw:
+                    wl[0] += wc
+                for w in range(cw, cw + gw):
+                    wl[w] += wg
+                for p in range(npass):
+                    gl = [sum(wl[w] for w in range(g, nw, 4)) for g in range(4)]
+                    g = min(range(4), key=lambda g_: (gl[g_], g_))
+                    w = min(range(g, nw, 4), key=lambda w_: (wl[w_], w_))
+                    tab[s, p] = w
+                    wl[w] += 4
+            cache[key] = tab
+        out[b] = cache[key]
+    return out
+
+
+def pass_masks(B: int, sched: np.ndarray, ns: int = 3, near: Optional[np.ndarray] = None) -> np.ndarray:
+    """[nb, ns, 17] uint32 from ``pass_schedule``: bit p of wave w's word is
+    set when w runs pass p of the stage; word 16 is the near-pass mask
+    (``near_pass_masks``; fused_step.hip FArgs::sched)."""
+    counts = stage_face_counts(B, ns)
+    nb = sched.shape[0]
+    m = np.zeros((nb, ns, 17), dtype=np.uint32)
+    for s_, cnt in enumerate(counts):
+        for p in range(-(-cnt // 64)):
+            w = sched[:, s_, p].astype(np.int64)
+            m[np.arange(nb), s_, w] |= np.uint32(1 << p)
+    if near is not None:
+        m[:, :, 16] = near
+    return m
+
+
+def stage_face_coords(B: int, ns: int = 3) -> List[Tuple[np.ndarray, np.ndarray, np.ndarray]]:
+    """Per stage, for every regular face task t of the kernel's pass loop: the
+    axis (0: x-face, 1: y-face), the grid line k and the position p along it
+    (window coordinates), exactly as fused_step.hip's outer_face (stage 1) and
+    line-major order (stages 2, 3) map tasks."""
+    d = FusedDims.make(B, ns)
+    R, W, L1, H1 = d.R, d.W, d.L1, d.H1
+    nil = B - 3
+    ol0 = R + 2 - L1
+    ol1 = (W - L1) - (R + B - 1) + 1
+    nr1, nor = H1, H1 - B
+    noa = (ol0 + ol1) * nr1
+    nox = noa + nil * nor
+    out = []
+    for s_ in range(ns):
+        if s_ == 0:
+            nax = nox
+            t = np.arange(nax)
+            k = np.empty(nax, np.int64)
+            p = np.empty(nax, np.int64)
+            a = t < noa
+            li, r = np.divmod(t[a], nr1)
+            k[a] = np.where(li < ol0, L1 + li, R + B - 1 + (li - ol0))
+            p[a] = L1 + r
+            t2 = t[~a] - noa
+            li, r = np.divmod(t2, nor)
+            k[~a] = R + 2 + li
+            p[~a] = np.where(r < R - L1, L1 + r, R + B + (r - (R - L1)))
+        else:
+            lo = R - 2 * (ns - 1 - s_)
+            nr = W - 2 * lo
+            nax = nr * (nr + 1)
+            c, r = np.divmod(np.arange(nax), nr)
+            k, p = lo + c, lo + r
+        out.append((np.concatenate([np.zeros(nax, np.int64), np.ones(nax, np.int64)]),
+                    np.concatenate([k, k]), np.concatenate([p, p])))
+    return out
+
+
+def near_pass_masks(B: int, org: np.ndarray, flags: np.ndarray, N: int, ns: int = 3) -> np.ndarray:
+    """[nb, ns] uint32: bit p set when face pass p of the stage holds a face
+    within one line of a panel-edge line of the block's window (the faces that
+    read neighbour codes and ghost entries; fused_step.hip ``near``)."""
+    nb = org.shape[0]
+    out = np.zeros((nb, ns), dtype=np.uint32)
+    coords = stage_face_coords(B, ns)
+    far = -1000
+    X0, Y0 = org[:, 0].astype(np.int64), org[:, 1].astype(np.int64)
+    kx0 = np.where(flags & 2, -X0, far)
+    kx1 = np.where(flags & 4, N - X0, far)
+    ky0 = np.where(flags & 8, -Y0, far)
+    ky1 = np.where(flags & 16, N - Y0, far)
+    for s_, (ax, k, _) in enumerate(coords):
+        e0 = np.where(ax[None, :] == 1, ky0[:, None], kx0[:, None])
+        e1 = np.where(ax[None, :] == 1, ky1[:, None], kx1[:, None])
+        kk = k[None, :]
+        near = ((kk - e0 + 1 >= 0) & (kk - e0 + 1 <= 2)) | ((kk - e1 + 1 >= 0) & (kk - e1 + 1 <= 2))
+        npass = -(-near.shape[1] // 64)
+        for p in range(npass):
+            hit = near[:, 64 * p:64 * (p + 1)].any(1)
+            out[hit, s_] |= np.uint32(1 << p)
+    return out
+
+
+def face_normals(P: "FusedPlan", flags: np.ndarray) -> np.ndarray:
+    """[nb, 3, NFL] normal of every stage-1 face slot (component-major), from
+    the region line-normal tables: the region of the face's lower cell, as
+    the kernel's region-table path (PFN builds read this for panel-edge
+    blocks; interior blocks keep their line normals, rows left 0)."""
+    d = P.d
+    H1, L1 = d.H1, d.L1
+    nfx = d.nfx
+    nfl = 2 * nfx
+    j = np.arange(nfl)
+    yf = j >= nfx
+    jj = np.where(yf, j - nfx, j)
+    r = np.where(yf, jj // H1, jj // (H1 + 1))
+    c = np.where(yf, jj - r * H1, jj - r * (H1 + 1))
+    # x-face slot: row fv = L1 + r, line k = fu = L1 + c; y-face: line k = fv = L1 + r, fu = L1 + c
+    fu = L1 + c
+    fv = L1 + r
+    k = np.where(yf, fv, fu)
+    lu = fu - np.where(yf, 0, 1)          # lower cell of the face
+    lv = fv - np.where(yf, 1, 0)
+    ax = yf.astype(np.int64)
+    out = np.zeros((P.nb, 3, nfl))
+    for b in range(P.nb):
+        if flags[b] == 1:
+            continue
+        X0, Y0 = int(P.org[b, 0]), int(P.org[b, 1])
+        ra = region(X0 + lu, Y0 + lv, P.N)
+        ra = np.where(ra < 0, 0, ra)
+        out[b] = P.nrm[b, ax, ra, k, :].T
+    return out
+
+
 def fused_supported(engine, B: Optional[int] = None) -> Optional[str]:
     """None if ``engine`` can take the fused step, else the reason it cannot."""
     e = engine
@@ -1038,6 +1229,15 @@ class FusedKernel:
         self.tens["epoch"] = torch.zeros(nb, dtype=torch.int32, device=dev)
         self.tens["err"] = torch.zeros(4, dtype=torch.int32, device=dev)
         self.tens["prod"] = torch.as_tensor(producer_table(P), dtype=torch.int32, device=dev).contiguous()
+        # face passes per wave, balanced over the SIMDs (pass_schedule)
+        edge_b = np.array([any(int(x) > 0 for x in np.unique(P.reg[b])) for b in range(nb)])
+        sched = pass_schedule(B, np.asarray(P.ccnt), edge_b, G)
+        assert int(sched.max()) < fused_threads(B) // 64
+        flg = (org[:, 3].view(np.uint32) >> 24) & 0x1F
+        near = near_pass_masks(B, P.org, flg.astype(np.int64), e.layout.N)
+        self.tens["sched"] = torch.as_tensor(pass_masks(B, sched, near=near).view(np.int32), device=dev).contiguous()
+        # per-face normals of the panel-edge blocks (the kernel's PFN builds)
+        self.tens["nrmf"] = t(face_normals(P, flg.astype(np.int64)))
         self.timeout_ticks = int(timeout_s * 1e8)
         if X is not None:
             self._setup_exchange(X, timeout_s)
@@ -1108,6 +1308,8 @@ class FusedKernel:
         d.nsteps = nsteps
         d.prod = p(tn["prod"])
         d.PM = int(tn["prod"].shape[1])
+        d.sched = p(tn["sched"])
+        d.nrmf = p(tn["nrmf"])
         if self.mem is not None:
             d.xg = 1
             d.ring = self.ring

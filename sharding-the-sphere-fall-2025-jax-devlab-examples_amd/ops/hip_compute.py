@@ -282,6 +282,11 @@ class HipCompute:
             return False
         self._shape(*MARCH_AUTO)
         self._tables()
+        # the interior / boundary block lists describe the old block grid: a
+        # march job id is not a block id, so the split launch path is closed for
+        # this engine (its stages run inside the xGMI stage ops)
+        self.blk_interior = self.blk_boundary = None
+        self._xg_march = True
         return True
 
     def desc(self, st: Stage, dt: float, blocks: Optional[torch.Tensor], nblocks: int,
@@ -338,6 +343,9 @@ class HipCompute:
         native.check(rc, "stage kernel")
 
     def stage(self, st: Stage, dt: float, recv, part: str = "all") -> None:
+        if getattr(self, "_xg_march", False):
+            raise RuntimeError("this engine marches with the direct xGMI exchange: its stages run through "
+                               "XgmiHalo (the interior / boundary split has no march form)")
         if not self.remote:
             if part in ("all", "interior"):
                 self.launch(self.desc(st, dt, None, self.nblocks))

@@ -291,6 +291,16 @@ class NativeStepper:
         if self.fused is not None:
             self.fused.check()
 
+    def err_words(self) -> List[torch.Tensor]:
+        """Device error words the kernels set on a timed-out wait (non-zero:
+        the state is not to be trusted); ``check()`` raises on them."""
+        out = []
+        if self.xgmi is not None:
+            out.append(self.xgmi.err)
+        if self.fused is not None:
+            out.append(self.fused.tens["err"])
+        return out
+
     def _run_native(self, nsteps: int) -> None:
         """Eager op list on self.stream, ordered after and before torch's
         current stream."""
@@ -375,10 +385,19 @@ class NativeStepper:
         time and step count are unchanged.  With the direct xGMI exchange this
         is collective (the restore re-primes the rings)."""
         if self.direct:
-            # one untimed pass of the same launches on a scratch copy (first-use costs)
-            if prime and nsteps // self.period:
+            # one untimed pass of the same launches on a scratch copy (first-use
+            # costs), the remainder launch of a chunk that is not a whole number
+            # of periods included (its descriptor is built here, not in the run)
+            rem = nsteps % self.period
+            if rem >= 2 and self.spl > 1:
+                self.fused.multi_desc(rem - rem % 2)
+            if prime and nsteps:
                 saved = self._save()
-                self._run_direct((nsteps // self.period) * self.period)
+                if nsteps // self.period:
+                    self._run_direct((nsteps // self.period) * self.period)
+                if rem >= 2 and self.spl > 1:
+                    self.fused.launch(0, int(torch.cuda.current_stream(self.e.device).cuda_stream),
+                                      nsteps=rem - rem % 2)
                 torch.cuda.synchronize(self.e.device)
                 self._restore(saved)
                 self.stats["direct_steps"] = 0

@@ -431,12 +431,26 @@ class IpcRing:
             raise err if err is not None else RuntimeError("xGMI setup failed on another rank")
 
     def close(self) -> None:
+        """Collective when distributed (every rank closes its ring together,
+        as every call site does).  Order: this rank's kernels are done (no more
+        stores into peers' rings), its peer mappings are closed, then a group
+        barrier, and only then does the ring go back to the process's pool,
+        where the next ``stsp_xg_alloc`` zeroes and reuses it: without the
+        barrier a peer still inside its last launch could store tagged granules
+        into a ring this rank had already handed to a new exchange."""
+        import torch.distributed as dist
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
         L = self._lib
+        if self.base or self.opened:
+            torch.cuda.synchronize(self.device)
         for p in self.opened:
             L.stsp_ipc_close(ctypes.c_void_p(p))
         self.opened = []
+        if self.distributed and dist.is_initialized():
+            dist.barrier(group=self.group)       # every rank, with or without a ring
         if self.base:
-            torch.cuda.synchronize(self.device)
             L.stsp_xg_free(ctypes.c_void_p(self.base))     # back to the process's ring pool
             self.base = None
 

@@ -101,15 +101,33 @@ def main():
         out["stage_graph_us_per_step"] = s0.elapsed_time(s1) * 1e3 / (2 * a.reps)
     if a.stamps:
         nb = fk.plan.nb
-        st = torch.zeros((nb, 16, 16), dtype=torch.int64, device="cuda")
+        FW = 32                              # stamp row width (fused_step.hip FST_W)
+        st = torch.zeros((nb, 16, FW), dtype=torch.int64, device="cuda")
         for d in fk.descs:
             d.stamps = st.data_ptr()
         for _ in range(3):
             fk.launch(0)
         torch.cuda.synchronize()
-        v = st.cpu().numpy().astype(np.float64)
+        raw = st.cpu().numpy()
+        v = raw[:, :, :16].astype(np.float64)
         for d in fk.descs:
             d.stamps = 0
+        # placement: HW_ID (SIMD bits 5:4, CU 11:8, SH 12, SE 15:13) and XCC_ID per wave
+        hw, xcc, disp = raw[:, :, 16], raw[:, :, 17], raw[:, :, 18]
+        live = v[:, :, 0] != 0
+        simd = (hw >> 4) & 3
+        blk_xcc = np.array([int(xcc[b][live[b]][0]) & 15 for b in range(nb)])
+        blk_disp = np.array([int(disp[b][live[b]][0]) for b in range(nb)])
+        # waves of one block sharing a SIMD: is it always w mod 4?
+        grp_ok = all(len(set(int(simd[b, w]) for w in range(16) if live[b, w] and w % 4 == r)) == 1
+                     for b in range(nb) for r in range(4))
+        out["placement"] = {
+            "simd_of_wave_mod4_consistent": bool(grp_ok),
+            "simd_order_block0": [int(simd[0, w]) for w in range(16) if live[0, w]],
+            "xcc_of_dispatch_mod8": {str(r): sorted(set(int(x) for x in blk_xcc[blk_disp % 8 == r])) for r in range(8)},
+            "blocks_per_xcc": {str(x): int((blk_xcc == x).sum()) for x in sorted(set(blk_xcc.tolist()))},
+            "xcc_by_logical_block": blk_xcc.tolist(),
+        }
         # stamps [block][wave][phase]: phase time of a block = its last wave's stamp;
         # waves that do not exist (768-thread blocks: 12 waves) or phases a wave
         # never stamped stay 0 -> NaN
@@ -154,7 +172,7 @@ def main():
         torch.cuda.synchronize()
         md.stamps = 0
         fk.check()
-        v2 = st.cpu().numpy().astype(np.float64).reshape(nb, nw, 16)
+        v2 = st.cpu().numpy()[:, :, :16].astype(np.float64).reshape(nb, nw, 16)
         v2 = np.where(v2 == 0, np.nan, v2)
         top = np.nanmin(v2[:, :, 13], 1)
         rel2 = np.nanmax(v2 - top[:, None, None], 1)
@@ -166,8 +184,9 @@ def main():
         pw = {}
         for s_ in (1, 2, 3):
             dtw = v2[:, :, 9 + s_] - np.nanmax(v2[:, :, starts[s_]], 1)[:, None]
-            pw[f"s{s_}"] = {"int": [None if np.isnan(x) else int(x) for x in np.nanmean(dtw[~edge], 0)],
-                            "corner": [None if np.isnan(x) else int(x) for x in np.nanmean(dtw[corner], 0)]}
+            with np.errstate(all="ignore"):
+                pw[f"s{s_}"] = {c_: [None if np.isnan(x) else int(x) for x in np.nanmean(dtw[m_], 0)]
+                                for c_, m_ in (("int", ~edge), ("edge", side), ("corner", corner))}
         out["multi_wave_face_cycles"] = pw
         out["multi_last_step_cycles"] = {n_: {"int": mean2(rel2, ~edge, k), "edge": mean2(rel2, side, k),
                                               "corner": mean2(rel2, corner, k), "max": float(rel2[:, k].max())}
