@@ -818,6 +818,209 @@ class CubedSphereLowRankAdvection:
         return torch.stack([f.dense() for f in F])
 
 
+class CubedSphereLowRankShallowWater:
+    """Linearised rotating shallow water on the six panels of the cubed
+    sphere, carried entirely in factored form U_p = A_p B_p^T: the six-panel
+    counterpart of ``LowRankShallowWater`` (the Cartesian 2-D SWEs of the TT
+    speed-up the slides cite, PDF s.3) on the reference's own grid (PDF s.4,
+    s.19).
+
+    State per panel: the height perturbation h and the velocity as Cartesian
+    components (vx, vy, vz), exchanged across panel edges as three scalars, as
+    the reference exchanges winds ("Cartesian Velocity Exchange", PDF s.18).
+    About a resting layer of depth H:
+
+        h_t = -H div v,    v_t = -g P grad h - f r x v,    f = 2 Omega z,
+
+    finite volumes with the true sphere metric (models/swe.py's geometry):
+    central face values, edge lengths L and unit normals m (per grid line),
+    exact cell areas A, the Gauss gradient minus its curvature sum
+    S = sum L m (so a constant h has no gradient), P = I - r r^T the tangent
+    projection at the cell centre r, SSP-RK3.  The operator is linear, so
+    every product stays factored: the metric coefficients (L m_c per face,
+    S_c, 1/A, r_c, f r_c) are factored once (``coef_eps``), a coefficient
+    times a field is a Khatri-Rao product of factors, face averages and
+    differences act on the factors' rows, and the cube coupling is the ghost
+    strips gathered from the neighbour panels' factors (O(N r) per side;
+    ``CubedSphereLowRankDiffusion.ghosts``), added as rank-1 terms.  Ranks are
+    truncated to ``eps`` after every product.  A face between two panels sees
+    the same two cells from both sides, so the total mass sum(A h) is
+    conserved to round-off and truncation.  ``dense_step`` is the N x N
+    six-panel reference of the same discrete operator
+    (tests/test_tt_and_models.py: factored vs dense to 1e-10)."""
+
+    FIELDS = ("h", "vx", "vy", "vz")
+
+    def __init__(self, N: int, H: float = 1000.0, g: float = 9.80616, omega: float = 7.292e-5,
+                 eps: float = 1e-13, max_rank: Optional[int] = None, coef_eps: float = 1e-15,
+                 dtype=torch.float64, device="cpu"):
+        from .geometry import CubedSphereGrid
+        self.N, self.H, self.g, self.omega = N, H, g, omega
+        self.eps, self.max_rank = eps, max_rank
+        self.dtype, self.device = dtype, torch.device(device)
+        grid = CubedSphereGrid(N)
+        self.grid = grid
+        lx, ly = grid.x_edge_lengths(), grid.y_edge_lengths()          # [6, N, N+1], [6, N+1, N]
+        mx, my = grid.x_edge_normals(), grid.y_edge_normals()          # [6, N+1, 3] per grid line
+        area = grid.areas()
+        r = grid.centers()                                               # [6, N, N, 3]
+        cx = lx[..., None] * mx[:, None, :, :]                           # [6, N, N+1, 3]
+        cy = ly[..., None] * my[:, :, None, :]                           # [6, N+1, N, 3]
+        S = (cx[:, :, 1:] - cx[:, :, :-1]) + (cy[:, 1:] - cy[:, :-1])   # [6, N, N, 3] curvature sum
+        f = 2.0 * omega * r[..., 2]
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=self.device)
+        # dense copies (reference operator)
+        self.Cx, self.Cy, self.S = t(cx), t(cy), t(S)
+        self.invA, self.r, self.fr = t(1.0 / area), t(r), t(f[..., None] * r)
+        fac = lambda M: lowrank_coefficients(M, coef_eps)
+        self.kcx = [[fac(self.Cx[p, ..., c]) for c in range(3)] for p in range(6)]
+        self.kcy = [[fac(self.Cy[p, ..., c]) for c in range(3)] for p in range(6)]
+        self.kS = [[fac(self.S[p, ..., c]) for c in range(3)] for p in range(6)]
+        self.kA = [fac(self.invA[p]) for p in range(6)]
+        self.kr = [[fac(self.r[p, ..., c]) for c in range(3)] for p in range(6)]
+        self.kfr = [[fac(self.fr[p, ..., c]) for c in range(3)] for p in range(6)]
+        self.halo = CubedSphereLowRankDiffusion(N, dtype=dtype, device=device)
+        e = torch.zeros((N + 1, 2), dtype=dtype, device=self.device)
+        e[0, 0] = 1.0
+        e[N, 1] = 1.0
+        self._e = e
+        c = math.sqrt(g * H)
+        self.dt_max = 0.5 * grid.min_spacing() / (c + 1e-300)
+        self.stats = {"recompressions": 0, "max_k": 0}
+
+    def coefficient_ranks(self) -> dict:
+        rk = lambda L: max(int(C.shape[1]) for C, _ in L)
+        return {"L m": max(rk(self.kcx[p]) for p in range(6)), "S": max(rk(self.kS[p]) for p in range(6)),
+                "1/A": max(int(C.shape[1]) for C, _ in self.kA), "r": max(rk(self.kr[p]) for p in range(6)),
+                "f r": max(rk(self.kfr[p]) for p in range(6))}
+
+    # ---- factored operator ----------------------------------------------------
+    def _trunc(self, A, B) -> LowRankField:
+        self.stats["recompressions"] += 1
+        self.stats["max_k"] = max(self.stats["max_k"], int(A.shape[1]))
+        return recompress(A, B, self.eps, self.max_rank)
+
+    def _avg_x(self, X: LowRankField, g: torch.Tensor):
+        """Face values of x-faces [N, N+1] with the W / E ghost strips."""
+        return (torch.cat([X.A, 0.5 * g[0:2].T], 1), torch.cat([_face_avg(X.B), self._e], 1))
+
+    def _avg_y(self, X: LowRankField, g: torch.Tensor):
+        return (torch.cat([_face_avg(X.A), self._e], 1), torch.cat([X.B, 0.5 * g[2:4].T], 1))
+
+    def _div(self, kx, ky, ax, ay) -> LowRankField:
+        """sum_c  diff_x (Cx_c avg_x(X_c)) + diff_y (Cy_c avg_y(X_c)) over the
+        given (coefficient, face-value) pairs, then times 1/A."""
+        As, Bs = [], []
+        for (Cc, Dc), (A, B) in zip(kx, ax):
+            fx = self._trunc(*hadamard(Cc, Dc, A, B))
+            As.append(fx.A)
+            Bs.append(_face_diff(fx.B))
+        for (Cc, Dc), (A, B) in zip(ky, ay):
+            fy = self._trunc(*hadamard(Cc, Dc, A, B))
+            As.append(_face_diff(fy.A))
+            Bs.append(fy.B)
+        return self._trunc(torch.cat(As, 1), torch.cat(Bs, 1))
+
+    def _times(self, k, X: LowRankField) -> LowRankField:
+        return self._trunc(*hadamard(k[0], k[1], X.A, X.B))
+
+    def rhs(self, F: Sequence[Sequence[LowRankField]]) -> List[List[LowRankField]]:
+        """F[q][p]: field q (h, vx, vy, vz) of panel p -> the same for d/dt."""
+        out = [[None] * 6 for _ in range(4)]
+        for p in range(6):
+            gh = [self.halo.ghosts(F[q], p) for q in range(4)]           # [4, N] strips per field
+            # h_t = -H (1/A) div v
+            div = self._div(self.kcx[p], self.kcy[p], [self._avg_x(F[1 + c][p], gh[1 + c]) for c in range(3)],
+                            [self._avg_y(F[1 + c][p], gh[1 + c]) for c in range(3)])
+            dh = self._times(self.kA[p], div)
+            out[0][p] = LowRankField(-self.H * dh.A, dh.B)
+            # Gauss gradient G_c = (1/A) (sum_faces h L m_c - S_c h)
+            hx, hy = self._avg_x(F[0][p], gh[0]), self._avg_y(F[0][p], gh[0])
+            G = []
+            for c in range(3):
+                d = self._div([self.kcx[p][c]], [self.kcy[p][c]], [hx], [hy])
+                sh = self._times(self.kS[p][c], F[0][p])
+                G.append(self._times(self.kA[p], self._trunc(torch.cat([d.A, -sh.A], 1), torch.cat([d.B, sh.B], 1))))
+            rG = [self._times(self.kr[p][c], G[c]) for c in range(3)]
+            rGs = self._trunc(torch.cat([x.A for x in rG], 1), torch.cat([x.B for x in rG], 1))
+            v = [F[1 + c][p] for c in range(3)]
+            for c in range(3):
+                # -g (G_c - r_c (r . G)) - (f r x v)_c
+                a_, b_ = (c + 1) % 3, (c + 2) % 3
+                rc = self._times(self.kr[p][c], rGs)
+                t1 = self._times(self.kfr[p][a_], v[b_])
+                t2 = self._times(self.kfr[p][b_], v[a_])
+                out[1 + c][p] = self._trunc(torch.cat([-self.g * G[c].A, self.g * rc.A, -t1.A, t2.A], 1),
+                                            torch.cat([G[c].B, rc.B, t1.B, t2.B], 1))
+        return out
+
+    def _axpy(self, a: float, X, b: float, Y):
+        return [[self._trunc(torch.cat([a * x.A, b * y.A], 1), torch.cat([x.B, y.B], 1)) for x, y in zip(Xq, Yq)]
+                for Xq, Yq in zip(X, Y)]
+
+    def step(self, F, dt: float):
+        """One SSP-RK3 step of the four factored fields."""
+        U1 = self._axpy(1.0, F, dt, self.rhs(F))
+        U2 = self._axpy(0.75, F, 0.25, self._axpy(1.0, U1, dt, self.rhs(U1)))
+        return self._axpy(1.0 / 3.0, F, 2.0 / 3.0, self._axpy(1.0, U2, dt, self.rhs(U2)))
+
+    # ---- dense reference of the same operator --------------------------------
+    def _pad(self, U6: torch.Tensor) -> torch.Tensor:
+        N = self.N
+        P = torch.zeros((6, N + 2, N + 2), dtype=U6.dtype, device=U6.device)
+        P[:, 1:-1, 1:-1] = U6
+        flat = P.reshape(-1)
+        flat[self.halo._ddst] = flat[self.halo._dsrc]
+        return P
+
+    def dense_rhs(self, W: torch.Tensor) -> torch.Tensor:
+        """W [4, 6, N, N] = (h, vx, vy, vz)."""
+        Ps = [self._pad(W[q]) for q in range(4)]
+        avx = lambda P: 0.5 * (P[:, 1:-1, :-1] + P[:, 1:-1, 1:])         # [6, N, N+1]
+        avy = lambda P: 0.5 * (P[:, :-1, 1:-1] + P[:, 1:, 1:-1])         # [6, N+1, N]
+        dvg = lambda fx, fy: (fx[:, :, 1:] - fx[:, :, :-1]) + (fy[:, 1:] - fy[:, :-1])
+        div = sum(dvg(self.Cx[..., c] * avx(Ps[1 + c]), self.Cy[..., c] * avy(Ps[1 + c])) for c in range(3))
+        dh = -self.H * self.invA * div
+        h = W[0]
+        G = torch.stack([self.invA * (dvg(self.Cx[..., c] * avx(Ps[0]), self.Cy[..., c] * avy(Ps[0]))
+                                      - self.S[..., c] * h) for c in range(3)])
+        rG = sum(self.r[..., c] * G[c] for c in range(3))
+        out = [dh]
+        for c in range(3):
+            a_, b_ = (c + 1) % 3, (c + 2) % 3
+            cor = self.fr[..., a_] * W[1 + b_] - self.fr[..., b_] * W[1 + a_]
+            out.append(-self.g * (G[c] - self.r[..., c] * rG) - cor)
+        return torch.stack(out)
+
+    def dense_step(self, W: torch.Tensor, dt: float) -> torch.Tensor:
+        W1 = W + dt * self.dense_rhs(W)
+        W2 = 0.75 * W + 0.25 * (W1 + dt * self.dense_rhs(W1))
+        return W / 3.0 + (2.0 / 3.0) * (W2 + dt * self.dense_rhs(W2))
+
+    # ---- conversions / diagnostics --------------------------------------------
+    def to_factored(self, W: torch.Tensor):
+        return [[LowRankField.from_dense(W[q, p].to(device=self.device, dtype=self.dtype), min(self.eps, 1e-14),
+                                         self.max_rank) for p in range(6)] for q in range(4)]
+
+    @staticmethod
+    def to_dense(F) -> torch.Tensor:
+        return torch.stack([torch.stack([f.dense() for f in Fq]) for Fq in F])
+
+    def mass(self, W: torch.Tensor) -> float:
+        return float((W[0] / self.invA).sum())
+
+    def gaussian_hill(self, lon0: float = 0.3, lat0: float = 0.4, width: float = 0.25, amp: float = 10.0):
+        """A resting layer with a Gaussian hill of height perturbation: the
+        gravity waves it sheds cross every panel edge within a few hours."""
+        c = self.grid.centers()
+        p0 = np.array([math.cos(lat0) * math.cos(lon0), math.cos(lat0) * math.sin(lon0), math.sin(lat0)])
+        d = np.arccos(np.clip(c @ p0, -1.0, 1.0))
+        h = amp * np.exp(-(d / width) ** 2)
+        W = np.zeros((4, 6, self.N, self.N))
+        W[0] = h
+        return torch.as_tensor(W, dtype=self.dtype, device=self.device)
+
+
 def _cdiff(X: torch.Tensor, h: float) -> torch.Tensor:
     """Periodic central difference of a factor's rows, (X[i+1] - X[i-1]) / 2h."""
     return (torch.roll(X, -1, 0) - torch.roll(X, 1, 0)) * (0.5 / h)

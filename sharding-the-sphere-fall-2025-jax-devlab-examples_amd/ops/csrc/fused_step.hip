@@ -246,6 +246,20 @@ __device__ __forceinline__ void to_global(int fr, T xi, T xj, T xn, T& o0, T& o1
   o2 = ai == 2 ? xi : (aj == 2 ? xj : xn);
 }
 
+// swap a value between the lanes of a pair (2 j, 2 j + 1): DPP quad_perm
+// [1, 0, 3, 2], one v_mov_dpp per 32 bits, every lane of the wave active
+template <typename T>
+__device__ __forceinline__ T pair_swap(T v) {
+  if constexpr (sizeof(T) == 8) {
+    int2 p = __builtin_bit_cast(int2, v);
+    p.x = __builtin_amdgcn_update_dpp(0, p.x, 0xB1, 0xF, 0xF, false);
+    p.y = __builtin_amdgcn_update_dpp(0, p.y, 0xB1, 0xF, 0xF, false);
+    return __builtin_bit_cast(T, p);
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  }
+}
+
 __device__ __forceinline__ int sel5(int r, int v0, int v1, int v2, int v3, int v4) {
   return r == 0 ? v0 : r == 1 ? v1 : r == 2 ? v2 : r == 3 ? v3 : v4;
 }
@@ -829,40 +843,56 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         } else {
           face(ax, fu, fv, k, std::integral_constant<int, 0>{});
         }
-      } else if (task + 64 < ncor) {
+      } else {
         // cube-corner face j: cell c's face on side_c meets cell d's face on
         // side_d; every stencil index comes from the host table (no codes, no
         // wait for the ghost pass: an interpolated neighbour is evaluated here
-        // with the ghost pass's formula, x0 + t (x1 - x0), so bit for bit)
-        const int j = task + 64;
-        const int* ct = s_ct[j];
-        const int fl_ = ct[CT_FLAGS];
-        T fv2[2][4], cc[2][5];
+        // with the ghost pass's formula, x0 + t (x1 - x0), so bit for bit).
+        // A lane pair per face: lane 2 j + q reconstructs side q, the pair
+        // swaps its results (DPP quad_perm [1,0,3,2]) and the even lane takes
+        // the flux: the corner wave's chain is one reconstruction long, not two
+        // (alone on its wave it set the corner blocks' stage-3 face phase)
+        const int lane = tid & 63, j = lane >> 1, q = lane & 1;
+        const bool live = j < ncor;
+        T fvq[4], ccq[5];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int f = 0; f < 4; ++f) fvq[f] = T(0);
+#pragma unroll
+        for (int f = 0; f < 5; ++f) ccq[f] = T(0);
+        int fl_ = 0;
+        if (live) {
+          const int* ct = s_ct[j];
+          fl_ = ct[CT_FLAGS];
           const int ic = ct[5 * q], a0 = ct[5 * q + 1], a1 = ct[5 * q + 2], n0 = ct[5 * q + 3], n1 = ct[5 * q + 4];
           const bool plus = (fl_ >> (4 + q)) & 1, ai = (fl_ >> (2 * q)) & 1, ni = (fl_ >> (2 * q + 1)) & 1;
           const T ta = s_cg[j][4 + 2 * q], tn = s_cg[j][5 + 2 * q];
 #pragma unroll
-          for (int f = 0; f < 5; ++f) cc[q][f] = wf[f * WW + ic];
+          for (int f = 0; f < 5; ++f) ccq[f] = wf[f * WW + ic];
 #pragma unroll
           for (int f = 0; f < 4; ++f) {
-            const T c0 = cc[q][f];
+            const T c0 = ccq[f];
             const T xa = wf[f * WW + a0], xn = wf[f * WW + n0];
             const T across = ai ? xa + ta * (wf[f * WW + a1] - xa) : xa;
             const T inward = ni ? xn + tn * (wf[f * WW + n1] - xn) : xn;
-            fv2[q][f] = plus ? c0 + half_slope<LIM>(c0 - inward, across - c0)
-                             : c0 - half_slope<LIM>(c0 - across, inward - c0);
+            fvq[f] = plus ? c0 + half_slope<LIM>(c0 - inward, across - c0)
+                          : c0 - half_slope<LIM>(c0 - across, inward - c0);
           }
         }
-        T fl[4];
-        swe_flux<T>(fv2[0], fv2[1], cc[0], cc[1], s_cg[j][0], s_cg[j][1], s_cg[j][2], s_cg[j][3], a.g, fl);
-        const int fc = ct[10], fd = ct[11];
-        const bool pc = (fl_ >> 4) & 1, pd = (fl_ >> 5) & 1;
+        T fvp[4], ccp[5];                                   // the partner lane's side
 #pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          if (fc >= 0) s_fl[f][fc] = pc ? fl[f] : -fl[f];
-          if (fd >= 0) s_fl[f][fd] = pd ? -fl[f] : fl[f];
+        for (int f = 0; f < 4; ++f) fvp[f] = pair_swap(fvq[f]);
+#pragma unroll
+        for (int f = 0; f < 5; ++f) ccp[f] = pair_swap(ccq[f]);
+        if (live && q == 0) {
+          T fl[4];
+          swe_flux<T>(fvq, fvp, ccq, ccp, s_cg[j][0], s_cg[j][1], s_cg[j][2], s_cg[j][3], a.g, fl);
+          const int fc = s_ct[j][10], fd = s_ct[j][11];
+          const bool pc = (fl_ >> 4) & 1, pd = (fl_ >> 5) & 1;
+#pragma unroll
+          for (int f = 0; f < 4; ++f) {
+            if (fc >= 0) s_fl[f][fc] = pc ? fl[f] : -fl[f];
+            if (fd >= 0) s_fl[f][fd] = pd ? -fl[f] : fl[f];
+          }
         }
       }
     }

@@ -43,6 +43,102 @@ def test_fused_torch_matches_stage_oracle(N, t, B, case, lim):
     assert fe.step_count == 2
 
 
+@pytest.mark.parametrize("B", [8, 12, 16, 18, 20])
+def test_pass_schedule_covers_every_pass_once(B):
+    """Every face pass of every stage runs on exactly one wave (the kernel's
+    per-wave masks), the corner wave and the ghost waves exist in the thread
+    count, and the balanced schedule's busiest SIMD group never carries more
+    than round 4's placement ("legacy")."""
+    from stsphere.ops.fused import fused_threads, pass_masks, pass_schedule, stage_face_counts
+    nw = fused_threads(B) // 64
+    ncor = np.array([0, 0, 7, 30])
+    edge = np.array([False, True, True, True])
+    counts = stage_face_counts(B)
+    for w in ("8:1", "legacy"):
+        sc = pass_schedule(B, ncor, edge, 88, weights=w)
+        m = pass_masks(B, sc)
+        assert m.shape == (4, 3, 17) and int(sc.max()) < nw
+        for s_, cnt in enumerate(counts):
+            npass = -(-cnt // 64)
+            assert npass <= 32
+            allp = np.bitwise_or.reduce(m[:, s_, :16], axis=1)
+            assert (allp == np.uint32((1 << npass) - 1)).all()
+            for b in range(4):       # no pass twice
+                bits = sum(bin(int(x)).count("1") for x in m[b, s_, :16])
+                assert bits == npass
+
+    def group_load(sc, b, s_, wc=8, wg=1):
+        cw = 1 if ncor[b] else 0
+        gw = 2 if edge[b] else 0
+        wl = [0] * nw
+        if cw:
+            wl[0] += wc
+        for w_ in range(cw, cw + gw):
+            wl[w_] += wg
+        for p in range(-(-counts[s_] // 64)):
+            wl[int(sc[b, s_, p])] += 4
+        return max(sum(wl[w_] for w_ in range(g, nw, 4)) for g in range(4))
+
+    new, old = pass_schedule(B, ncor, edge, 88), pass_schedule(B, ncor, edge, 88, weights="legacy")
+    for b in range(4):
+        for s_ in range(3):
+            assert group_load(new, b, s_) <= group_load(old, b, s_)
+
+
+def test_near_pass_masks_flag_every_near_face():
+    """A face pass the host does not flag must hold no face within one line
+    of a panel-edge line (those faces read neighbour codes and ghost entries;
+    an unflagged one would read the raw window), and interior blocks flag
+    nothing."""
+    from stsphere.ops.fused import near_pass_masks, stage_face_coords
+    N, B = 48, 16
+    L = TileLayout(N, 1, 1, ng=2)
+    P = FusedPlan(L, 0, CubedSphereGrid(N), B=B, ns=3)
+    flags = np.array([sum(1 << int(r) for r in np.unique(P.reg[b]) if r >= 0) for b in range(P.nb)])
+    nm = near_pass_masks(B, P.org, flags, N)
+    coords = stage_face_coords(B)
+    W = P.d.W
+    for b in range(P.nb):
+        X0, Y0 = int(P.org[b, 0]), int(P.org[b, 1])
+        if flags[b] == 1:
+            assert (nm[b] == 0).all()
+            continue
+        lines = {0: [k for k in range(W + 1) if ((flags[b] & 2) and abs(k - (-X0)) <= 1)
+                     or ((flags[b] & 4) and abs(k - (N - X0)) <= 1)],
+                 1: [k for k in range(W + 1) if ((flags[b] & 8) and abs(k - (-Y0)) <= 1)
+                     or ((flags[b] & 16) and abs(k - (N - Y0)) <= 1)]}
+        for s_, (ax, k, _) in enumerate(coords):
+            for t in range(len(k)):
+                if int(k[t]) in lines[int(ax[t])]:
+                    assert (int(nm[b, s_]) >> (t // 64)) & 1, (b, s_, t)
+    assert nm.any()
+
+
+def test_face_normals_match_region_tables():
+    """The per-face normal table of panel-edge blocks is the region line-normal
+    table at the face's lower-cell region (the kernel's non-PFN path)."""
+    from stsphere.ops.fused import face_normals
+    N, B = 32, 16
+    L = TileLayout(N, 2, 1, ng=2)
+    P = FusedPlan(L, 0, CubedSphereGrid(N), B=B, ns=3)
+    flags = np.array([sum(1 << int(r) for r in np.unique(P.reg[b]) if r >= 0) for b in range(P.nb)])
+    nf = face_normals(P, flags)
+    d = P.d
+    rng = np.random.default_rng(0)
+    for b in np.nonzero(flags != 1)[0][:6]:
+        for j in rng.integers(0, 2 * d.nfx, 40):
+            yf = j >= d.nfx
+            jj = j - d.nfx if yf else j
+            r, c = divmod(int(jj), d.H1 if yf else d.H1 + 1)
+            fu, fv = d.L1 + c, d.L1 + r
+            k = fv if yf else fu
+            lu, lv = (fu, fv - 1) if yf else (fu - 1, fv)
+            ra = int(region(P.org[b, 0] + lu, P.org[b, 1] + lv, N))
+            ra = max(ra, 0)
+            assert np.array_equal(nf[b, :, j], P.nrm[b, int(yf), ra, k, :])
+    assert (nf[flags == 1] == 0).all()
+
+
 def test_fused_plan_invariants():
     N, B = 32, 16
     L = TileLayout(N, 2, 1, ng=2)
