@@ -438,17 +438,46 @@ extern "C" int stsp_nccl_selftest(void* comm, void* stream) {
 // garbage from fresh torch buffers in 5 of 6 runs; never with the ring kept,
 // profiles/r4_ring/README.md), and a ring peers have mapped should not
 // return to the driver under them anyway.
+//
+// Diagnostics (STSP_RING_GUARD=1): every ring gets a guard region of
+// RING_GUARD bytes on each side, filled with a pattern at allocation and
+// checked by stsp_xg_check_guards() (the GPU tests call it after every test
+// in that mode): a kernel store past either end of a ring shows up there.
+// STSP_XG_POOL=0 hands rings back with hipFree again (the experiment of
+// profiles/r4_ring, kept for re-runs).
 namespace {
 std::mutex g_ring_mu;
 std::unordered_map<void*, size_t> g_ring_bytes;   // every ring ever allocated
 std::vector<void*> g_ring_free;                   // of those, the free ones
+constexpr size_t RING_GUARD = 65536;
+constexpr unsigned GUARD_WORD = 0x5A17C0DEu;
+bool env_on(const char* name, bool dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) != 0 : dflt;
+}
+bool ring_guard() {
+  static const bool on = env_on("STSP_RING_GUARD", false);
+  return on;
+}
+bool ring_pool() {
+  static const bool on = env_on("STSP_XG_POOL", true);
+  return on;
+}
+__global__ void guard_fill_kernel(unsigned* p, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = GUARD_WORD;
+}
+__global__ void guard_check_kernel(const unsigned* p, size_t n, unsigned* bad) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    if (p[i] != GUARD_WORD) atomicAdd(bad, 1u);
+}
 }  // namespace
 
 extern "C" int stsp_xg_alloc(size_t bytes, void** out) {
   *out = nullptr;
   void* p = nullptr;
   size_t have = 0;
-  {
+  if (ring_pool()) {
     std::lock_guard<std::mutex> lk(g_ring_mu);
     size_t best = 0;
     for (size_t k = 0; k < g_ring_free.size(); ++k) {   // smallest free ring that fits
@@ -458,7 +487,14 @@ extern "C" int stsp_xg_alloc(size_t bytes, void** out) {
     if (p) g_ring_free.erase(g_ring_free.begin() + best);
   }
   if (!p) {
-    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) return -1;
+    const size_t g = ring_guard() ? RING_GUARD : 0;
+    void* raw = nullptr;
+    if (hipExtMallocWithFlags(&raw, bytes + 2 * g, hipDeviceMallocUncached) != hipSuccess) return -1;
+    if (g) {
+      hipLaunchKernelGGL(guard_fill_kernel, dim3(64), dim3(256), 0, 0, (unsigned*)raw, g / 4);
+      hipLaunchKernelGGL(guard_fill_kernel, dim3(64), dim3(256), 0, 0, (unsigned*)((char*)raw + g + bytes), g / 4);
+    }
+    p = (char*)raw + g;
     have = bytes;
     std::lock_guard<std::mutex> lk(g_ring_mu);
     g_ring_bytes[p] = bytes;
@@ -470,6 +506,32 @@ extern "C" int stsp_xg_alloc(size_t bytes, void** out) {
   }
   *out = p;
   return 0;
+}
+
+// Guard words of every ring this process holds that differ from the pattern
+// (STSP_RING_GUARD=1; 0 otherwise or when clean, < 0 on a HIP error).
+extern "C" long long stsp_xg_check_guards(void) {
+  if (!ring_guard()) return 0;
+  std::vector<void*> rings;
+  std::vector<size_t> sizes;
+  {
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    for (auto& kv : g_ring_bytes) { rings.push_back(kv.first); sizes.push_back(kv.second); }
+  }
+  unsigned* d = nullptr;
+  if (hipMalloc(&d, sizeof(unsigned)) != hipSuccess) return -1;
+  hipMemset(d, 0, sizeof(unsigned));
+  for (size_t k = 0; k < rings.size(); ++k) {
+    char* p = (char*)rings[k];
+    hipLaunchKernelGGL(guard_check_kernel, dim3(64), dim3(256), 0, 0, (const unsigned*)(p - RING_GUARD),
+                       RING_GUARD / 4, d);
+    hipLaunchKernelGGL(guard_check_kernel, dim3(64), dim3(256), 0, 0, (const unsigned*)(p + sizes[k]),
+                       RING_GUARD / 4, d);
+  }
+  unsigned h = 0;
+  const bool ok = hipMemcpy(&h, d, sizeof(unsigned), hipMemcpyDeviceToHost) == hipSuccess;
+  hipFree(d);
+  return ok ? (long long)h : -2;
 }
 
 // Device allocation with explicit hipExtMallocWithFlags flags (zeroed):
@@ -493,6 +555,12 @@ extern "C" int stsp_xg_free(void* p) {
   if (!g_ring_bytes.count(p)) return -1;   // not a ring of this process
   for (void* q : g_ring_free)
     if (q == p) return -1;                 // freed twice
+  if (!ring_pool()) {                      // STSP_XG_POOL=0: back to the driver (diagnostics)
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    const size_t g = ring_guard() ? RING_GUARD : 0;
+    g_ring_bytes.erase(p);
+    return hipFree((char*)p - g) == hipSuccess ? 0 : -3;
+  }
   g_ring_free.push_back(p);
   return 0;
 }

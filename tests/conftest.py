@@ -54,3 +54,25 @@ def _heap_canary(request):
           flush=True)
     del xs
 
+
+
+@pytest.fixture(autouse=True)
+def _ring_guard(request):
+    """STSP_RING_GUARD=1 (GPU runs): every xGMI ring carries 64 KiB guard
+    regions on both sides (ops/csrc/runtime.cpp); after every GPU test they
+    are checked, and a store past either end of a ring fails the test that
+    made it (the round-4 post-free corruption hunt, profiles/r4_ring)."""
+    yield
+    if os.environ.get("STSP_RING_GUARD") != "1" or "gpu" not in request.keywords:
+        return
+    import torch
+    if not torch.cuda.is_available():
+        return
+    from stsphere.ops import native
+    L = native.require_native()
+    import ctypes
+    L.stsp_xg_check_guards.restype = ctypes.c_longlong
+    torch.cuda.synchronize()
+    bad = int(L.stsp_xg_check_guards())
+    print(f"\n[ring-guard] after {request.node.nodeid}: {bad} guard words changed", flush=True)
+    assert bad == 0, f"{bad} guard words around the xGMI rings changed (a store past a ring's end)"

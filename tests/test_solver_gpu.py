@@ -46,15 +46,20 @@ def test_single_gpu_solver_matches_cpu(limiter, tmp_path):
     assert type(g.runner).__name__ == "NativeStepper"
 
 
-def _spmd_worker(rank, world, port, t, outdir, comm):
+def _spmd_worker(rank, world, port, t, outdir, comm, fused="auto"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), STSP_SHARE_GPU="1")
     import torch.distributed as dist
     try:
-        s = Solver(_cfg(world, t, out=os.path.join(outdir, "run"), comm=comm), verbose=False)
+        c = _cfg(world, t, out=os.path.join(outdir, "run"), comm=comm)
+        c["runtime"]["fused"] = fused
+        s = Solver(c, verbose=False)
         s.initialize()
         assert s.comm == comm
         s.run(nsteps=6)
+        # the default SPMD runtime is the fused step with the xGMI ring inside
+        # it (every block of the rank's share resident); "off": stage kernels
+        assert (s.fused is not None) == (fused != "off"), s.fused
         s.save_checkpoint()
         s.run(nsteps=4)
         a = s.gather_global()
@@ -69,15 +74,24 @@ def _spmd_worker(rank, world, port, t, outdir, comm):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,t", [(2, 1), (4, 2)])
-def test_spmd_xgmi_solver_matches_single_and_restarts(world, t, tmp_path):
+@pytest.mark.parametrize("world,t,fused", [(2, 1, "auto"), (4, 2, "auto"), (2, 1, "off")])
+def test_spmd_xgmi_solver_matches_single_and_restarts(world, t, fused, tmp_path):
+    """SPMD ranks sharing one GPU with the default configuration take the
+    fused step (xGMI ring inside the kernel); the one-GPU reference runs the
+    same kernels (the fused step with the ranks' block size, or the stage
+    kernels with fused = off), so the states agree bitwise, restart included."""
     out = str(tmp_path)
-    mp.spawn(_spmd_worker, args=(world, _free_port(), t, out, "xgmi"), nprocs=world, join=True)
+    mp.spawn(_spmd_worker, args=(world, _free_port(), t, out, "xgmi", fused), nprocs=world, join=True)
     c = _cfg(1, t, out=str(tmp_path / "ref"))
-    c["runtime"]["fused"] = "off"              # the stage kernels the SPMD ranks run
+    c["runtime"]["fused"] = fused
     ref = Solver(c, verbose=False)
     ref.initialize()
     ref.run(nsteps=10)
+    if fused != "off":
+        from stsphere.ops.fused import fused_block
+        n = ref.layout.n
+        B_rank = fused_block(n, 6 * t * t // world, torch.cuda.get_device_properties(0).multi_processor_count // world)
+        assert ref.fused is not None and ref.fused.plan.B == B_rank, (ref.fused, B_rank)
     r = ref.gather_global()
     a = np.load(os.path.join(out, "a.npy"))
     b = np.load(os.path.join(out, "b.npy"))

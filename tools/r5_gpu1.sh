@@ -1,0 +1,9 @@
+#!/bin/bash
+# round-5 GPU check: fused + solver GPU tests, fused probe + bench, shared-GPU
+# rehearsals of BASELINE config 3 (C96, one panel per rank: 6 ranks; 3 ranks)
+set -o pipefail
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $ROOT
+TAG=r5_a TESTS="tests/test_fused.py tests/test_solver_gpu.py" ARMS="new:" REPS=3 bash tools/env_ab.sh || exit $?
+TAG=r5_a ROWS="6:--N 96 --tiles-per-edge 1 --steps 20 --warmup 5;3:--N 96 --tiles-per-edge 1 --steps 20 --warmup 5" bash tools/rehearse.sh || exit $?
+echo "== all done"
