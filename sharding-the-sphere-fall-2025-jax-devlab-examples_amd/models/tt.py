@@ -369,6 +369,47 @@ class LowRankDiffusion:
             A, B = torch.cat([A, c * (self.D @ A)], dim=1), torch.cat([B + c * (self.D @ B), B], dim=1)
         return recompress(A, B, self.eps, self.max_rank)
 
+    def run_persistent(self, U: LowRankField, dt: float, ncalls: int,
+                       stamps: Optional[torch.Tensor] = None) -> LowRankField:
+        """``ncalls`` factored steps (each ``substeps`` explicit substeps and
+        one CholeskyQR3 recompression, the numerics of ``qr="cholqr3n"``) in
+        ONE launch of the persistent kernel (ops/csrc/tt_persist.hip): two
+        workgroups keep the factors in LDS across the steps and hand the k x k
+        core between them on the device.  fp64, N <= 1024, 2^substeps r <= 16,
+        N k <= 12288.  The new rank is read once, after the launch.
+        ``stamps``: optional int64 [ncalls, 2, 16] device tensor of per-phase
+        shader clocks (expand, three QR passes, core hand-offs, product)."""
+        from ..ops import native
+        L = native.require_native()
+        N, r = U.A.shape
+        ns = self.substeps
+        if U.A.dtype != torch.float64 or U.A.device.type != "cuda":
+            raise ValueError("persistent factored step: fp64 CUDA factors")
+        A = U.A if U.A.stride(1) == 1 else U.A.contiguous()
+        B = U.B if U.B.stride(1) == 1 else U.B.contiguous()
+        dev = A.device
+        kmax = 16
+        out = torch.empty((2, N, kmax), dtype=torch.float64, device=dev)
+        key = ("persist", dev)
+        if getattr(self, "_pkey", None) != key:
+            self._pxch = torch.zeros(512, dtype=torch.float64, device=dev)
+            self._pflags = torch.zeros(4, dtype=torch.int32, device=dev)
+            self._prn = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._pkey = key
+        mr = self.max_rank or 0
+        rc = L.stsp_tt_persist(native.ptr(A), A.stride(0), native.ptr(B), B.stride(0), N, r, int(ncalls), ns,
+                               dt * self.kappa, 1.0 / (self.h * self.h), int(self.bc == "periodic"), self.eps, mr,
+                               native.ptr(self._pxch), native.ptr(self._pflags), native.ptr(out[0]),
+                               native.ptr(out[1]), kmax, native.ptr(self._prn),
+                               native.ptr(stamps) if stamps is not None else None, 2.0,
+                               native.current_stream_handle())
+        if rc != 0:
+            raise RuntimeError(f"stsp_tt_persist failed ({rc})")
+        rn = int(self._prn.item())
+        if rn <= 0 or int(self._pflags[3].item()) != 0:
+            raise RuntimeError(f"persistent factored step failed (rank {rn}, error word {int(self._pflags[3].item())})")
+        return LowRankField(out[0, :, :rn], out[1, :, :rn])
+
     def _step_hip_cqr(self, U: LowRankField, dt: float) -> LowRankField:
         if self.qr == "cholqr3n":
             return self._step_hip_cqr_native(U, dt)

@@ -18,7 +18,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libstsp.so")
-SOURCES = ["stage_kernel.hip", "march_kernel.hip", "fused_step.hip", "tt_kernels.hip", "runtime.cpp"]
+SOURCES = ["stage_kernel.hip", "march_kernel.hip", "fused_step.hip", "tt_kernels.hip", "tt_persist.hip", "runtime.cpp"]
 HEADERS = ["stsp_kernels.h", "stage_common.h", "runtime.h", "rccl_abi.h"]
 ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
 # library variants: "" = production; "diag" = in-kernel phase stamps (-DSTSP_STAMPS);

@@ -177,6 +177,12 @@ def _declare_tt(L):
     L.stsp_tt_lr_step3.restype = ci
     L.stsp_tt_step_workspace3.argtypes = [ci, ci, ci]
     L.stsp_tt_step_workspace3.restype = ctypes.c_size_t
+    # persistent factored step (tt_persist.hip)
+    L.stsp_tt_persist.argtypes = [vp, ci, vp, ci, ci, ci, ci, ci, cd, cd, ci, cd, ci, vp, vp, vp, vp, ci, vp, vp,
+                                  cd, vp]
+    L.stsp_tt_persist.restype = ci
+    L.stsp_tt_persist_limits.argtypes = [ctypes.POINTER(ci), ctypes.POINTER(ci)]
+    L.stsp_tt_persist_limits.restype = ci
 
 
 def available() -> bool:

@@ -337,3 +337,35 @@ def test_device_core_matches_host_core(dtype, tol, ns, max_rank):
         assert a.rank == b.rank
         da, db = a.dense().double(), b.dense().double()
         assert float((da - db).norm() / db.norm()) < tol
+
+
+def _modes(N, device):
+    x = torch.linspace(0, 1, N + 2, dtype=torch.float64, device=device)[1:-1]
+    A = torch.stack([torch.sin(math.pi * x), 0.3 * torch.sin(3 * math.pi * x), 0.1 * torch.sin(5 * math.pi * x)], 1)
+    B = torch.stack([torch.sin(2 * math.pi * x), torch.sin(math.pi * x), torch.sin(4 * math.pi * x)], 1)
+    return A.contiguous(), B.contiguous()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,substeps,ncalls,bc", [(1024, 2, 1, "dirichlet"), (1024, 2, 6, "dirichlet"),
+                                                  (512, 1, 4, "periodic"), (200, 2, 3, "dirichlet")])
+def test_persistent_factored_step_matches_native_chain(N, substeps, ncalls, bc):
+    """The one-launch persistent step (ops/csrc/tt_persist.hip: factors in LDS,
+    CholeskyQR3 and the core on the device, ncalls steps per launch) against
+    the round-4 kernel chain (stsp_tt_lr_step3) of the same numerics, and
+    against dense stepping of the same explicit scheme."""
+    A, B = _modes(N, "cuda")
+    s = tt.LowRankDiffusion(N, kappa=1.0, eps=1e-10, backend="hip", device="cuda", substeps=substeps, bc=bc)
+    dt = 0.5 * s.dt_max
+    ref = tt.LowRankField(A.clone(), B.clone())
+    for _ in range(ncalls):
+        ref = s.step(ref, dt)
+    got = s.run_persistent(tt.LowRankField(A.clone(), B.clone()), dt, ncalls)
+    R, G = ref.dense(), got.dense()
+    assert got.rank == ref.rank
+    assert float((G - R).norm() / R.norm()) < 1e-12
+    sd = tt.LowRankDiffusion(N, kappa=1.0, bc=bc, device="cuda")
+    U = A @ B.T
+    for _ in range(ncalls * substeps):
+        U = sd.dense_step(U, dt)
+    assert float((G - U).norm() / U.norm()) < 1e-9
