@@ -61,7 +61,7 @@ def parse(argv=None):
                          "per RK stage (C++ op list, any rank count); auto: fused where it applies")
     ap.add_argument("--steps-per-launch", type=int, default=0,
                     help="fused runtime: steps inside one kernel launch (0 = auto: the largest even divisor of "
-                         "--steps up to 64 when every block fits on the GPU at once; 1 = one launch per step)")
+                         "--steps up to 512 when every block fits on the GPU at once; 1 = one launch per step)")
     ap.add_argument("--launch", default="auto", choices=["auto", "direct", "graph"],
                     help="fused runtime: issue each multi-step kernel launch directly or replay it from a "
                          "hipGraph (a one-kernel graph only adds hipGraphLaunch's host floor); auto: direct on "

@@ -21,17 +21,18 @@ LIB = os.path.join(HERE, "libstsp.so")
 SOURCES = ["stage_kernel.hip", "march_kernel.hip", "fused_step.hip", "tt_kernels.hip", "tt_persist.hip", "runtime.cpp"]
 HEADERS = ["stsp_kernels.h", "stage_common.h", "runtime.h", "rccl_abi.h"]
 ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
-# library variants: "" = production; "diag" = in-kernel phase stamps (-DSTSP_STAMPS);
-# "xgc" = the arrival-counter hand-off of the xGMI halo instead of tagged granules
-# (STSP_XG_TAG=0), "xgf0" / "xgf2" = its publish-protocol probes (STSP_XG_FENCE)
+# library variants: "" = production; "diag" = in-kernel phase stamps of the
+# stage kernel (-DSTSP_STAMPS); "xgc" = the arrival-counter hand-off of the
+# xGMI halo instead of tagged granules (STSP_XG_TAG=0); the others are A/B
+# switches of kept alternatives (unfused faces, block-wide panel-edge fix-up,
+# own-cell wave placement, nine waves, library sqrt, compare+select slopes,
+# march waves per SIMD) and the timing-only fused-step probes fp_alledge /
+# fp_nogwait (the latter computes wrong numbers by design)
 VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgc": ["-DSTSP_XG_TAG=0"],
-                 "xgf0": ["-DSTSP_XG_TAG=0", "-DSTSP_XG_FENCE=0"], "xgf2": ["-DSTSP_XG_TAG=0", "-DSTSP_XG_FENCE=2"],
                  "unfused": ["-DSTSP_FUSE_FACES=0"], "pe0": ["-DSTSP_PE_WAVE=0"],
-                 "pnotab": ["-DSTSP_PROBE_NOTAB=1"], "pnoslot": ["-DSTSP_PROBE_NOSLOT=1"],
                  "ownw0": ["-DSTSP_OWN_SKIP0=0"], "w9": ["-DSTSP_W10=0"], "swsqrt": ["-DSTSP_HW_SQRT=0"],
                  "selslope": ["-DSTSP_SIGN_SLOPE=0"], "wpe6": ["-DSTSP_WPE=6"], "wpe7": ["-DSTSP_WPE=7"],
-                 "fp_alledge": ["-DSTSP_FPROBE_ALLEDGE=1"], "fp_nogwait": ["-DSTSP_FPROBE_NOGWAIT=1"],
-                 "mprobe": ["-DSTSP_MARCH_PROBE_NOWE=1", "-DSTSP_MARCH_WPE64=3", "-DSTSP_MARCH_WPE32=5"]}
+                 "fp_alledge": ["-DSTSP_FPROBE_ALLEDGE=1"], "fp_nogwait": ["-DSTSP_FPROBE_NOGWAIT=1"]}
 
 
 def lib_for(variant: str = "") -> str:

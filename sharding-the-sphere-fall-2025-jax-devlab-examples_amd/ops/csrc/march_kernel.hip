@@ -81,11 +81,6 @@ __device__ __forceinline__ void frame_to_global(int fr, T xi, T xj, T xn, T& o0,
 #ifndef STSP_MARCH_WPE32
 #define STSP_MARCH_WPE32 4
 #endif
-// timing-only probe (wrong numerics; build variant "mprobe"): no W / E
-// panel-edge treatment, to price its registers
-#ifndef STSP_MARCH_PROBE_NOWE
-#define STSP_MARCH_PROBE_NOWE 0
-#endif
 // ACC: the RK4 accumulator operands (acc_in / acc_out); the SSP-RK3 and Euler
 // stages run the instantiation without them (4 fewer live values per lane).
 // CG: compact geometry: the panel-shared tables of the fused step (1/A,
@@ -200,8 +195,8 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   // ---- panel edges of this wave's part of the tile (wave-uniform) -------------
   const int pe = a.pedge[tile];
   const int lnE = n - cs * MO + 2;                   // lane of column n
-  const bool peW = !STSP_MARCH_PROBE_NOWE && (pe & 1) && cs == 0;
-  const bool peE = !STSP_MARCH_PROBE_NOWE && (pe & 2) && lnE >= 0 && lnE < MW;
+  const bool peW = (pe & 1) && cs == 0;
+  const bool peE = (pe & 2) && lnE >= 0 && lnE < MW;
   // a segment reads rows y0 - 2 .. y1 + 1: the S ghost row -1 when y0 <= 1 and
   // the N ghost row n when y1 >= n - 1 (a segment ending one row short of the
   // tile still takes the slope of row n - 1 across the panel edge)

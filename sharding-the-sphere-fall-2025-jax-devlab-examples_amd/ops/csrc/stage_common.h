@@ -6,17 +6,13 @@
 #pragma once
 #include "stsp_kernels.h"
 
-// Publish protocol of the arrival-counter hand-off (STSP_XG_TAG=0 below; probe
-// variants, tools/xg_fence_probe.py, profiles/r1_xg_fence_probe.jsonl; loopback
-// C96 µs/step, plain step 17.1):
-//   0 = __threadfence_system() + release add: 117.5 (the fence is seq_cst, so
-//       every wave also invalidates L2 and the whole grid re-reads from HBM)
-//   1 = release add only (one L2 write-back per producing block): 28.6  <- default
-//   2 = relaxed add after the storing waves drain: 26.8 (relies on the ring
-//       stores being system-scope write-through; not a release in the model)
-#ifndef STSP_XG_FENCE
-#define STSP_XG_FENCE 1
-#endif
+// Publish protocol of the arrival-counter hand-off (STSP_XG_TAG=0 below):
+// every storing wave drains, then a release add per peer (one L2 write-back
+// per producing block).  Measured alternatives (profiles/r1_xg_fence_probe.jsonl,
+// loopback C96 us/step, plain step 17.1): a __threadfence_system() before the
+// add 117.5 (the fence is seq_cst: every wave also invalidates L2), the
+// release add 28.6, a relaxed add after the drain 26.8 (not a release in the
+// model); the probes are gone, the release add stays.
 // Halo hand-off form (stsp_kernels.h, xg fields):
 //   0 = arrival counters (drain + release add per producing block, block-level poll)
 //   1 = tagged granules: the data is the flag.  Each 32-bit word of a ghost cell
@@ -99,14 +95,6 @@ template <int BX, int BY> struct Geom {
 // (tests/test_kernel_contracts.py mirrors it).
 #ifndef STSP_PE_WAVE
 #define STSP_PE_WAVE 1
-#endif
-// timing-only probes (wrong numerics; build variants "pnotab" / "pnoslot"):
-// skip the panel-edge table loads / the edge threads' panel-edge selects
-#ifndef STSP_PROBE_NOTAB
-#define STSP_PROBE_NOTAB 0
-#endif
-#ifndef STSP_PROBE_NOSLOT
-#define STSP_PROBE_NOSLOT 0
 #endif
 constexpr int PEW_SX = 7, PEW_SY = 5;
 template <int BX, int BY>

@@ -349,7 +349,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   // three VGPRs there, which is what decides the waves per SIMD.
   constexpr bool LATE_TAB = !Geom<BX, BY>::W10;
   auto load_tab = [&]() {
-    if (pin && !STSP_PROBE_NOTAB) {
+    if (pin) {
 #pragma unroll
       for (int k = 0; k < KG; ++k) {
         const unsigned ti = (unsigned)(((tile * 4 + pside) * 3 + k) * n + pj);
@@ -669,7 +669,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   // fix-up slot pslot (the neighbour is on the left of the edge when plo)
   int pslot = -1;
   bool plo = false;
-  if (RECON && bsides && edge_ok && !STSP_PROBE_NOSLOT) {
+  if (RECON && bsides && edge_ok) {
     if (is_x && ex_ == 0 && (bsides & 1)) { pslot = 0 * BM + ey_ - y0; plo = true; }
     else if (is_x && ex_ == n && (bsides & 2)) { pslot = 1 * BM + ey_ - y0; }
     else if (!is_x && ey_ == 0 && (bsides & 4)) { pslot = 2 * BM + ex_ - x0; plo = true; }
@@ -693,7 +693,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
         wl = s_fp[0][fl_];
         wr = s_fm[0][fl_ + fst];
       }
-      if (!STSP_PROBE_NOSLOT && pslot >= 0) {
+      if (pslot >= 0) {
         if (plo) wl = s_pf[0][pslot];
         else wr = s_pf[0][pslot];
       }
@@ -716,7 +716,7 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
 #pragma unroll
         for (int f = 0; f < 4; ++f) { wl[f] = s_fp[f][fl_]; wr[f] = s_fm[f][fl_ + fst]; }
       }
-      if (!STSP_PROBE_NOSLOT && pslot >= 0) {   // panel edge: the neighbour's state and raw cell
+      if (pslot >= 0) {   // panel edge: the neighbour's state and raw cell
         if (plo) {
 #pragma unroll
           for (int f = 0; f < 4; ++f) wl[f] = s_pf[f][pslot];
@@ -862,17 +862,10 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
   }
   if constexpr (XG) {
     if (!STSP_XG_TAG && feed) {   // publish: every storing wave drains, then one lane per peer counts
-#if STSP_XG_FENCE == 0
-      __threadfence_system();
-#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid < 32 && ((feed >> tid) & 1))
-#if STSP_XG_FENCE == 2
-        __hip_atomic_fetch_add((gu64*)a.peer_cnt[tid], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#else
         __hip_atomic_fetch_add((gu64*)a.peer_cnt[tid], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-#endif
     }
     if (tid == 0) a.epoch[bid] = xe + 1;
   }
