@@ -68,9 +68,11 @@ def parse(argv=None):
                          "one GPU, graph across GPUs (the path the multi-rank rehearsals validated)")
     ap.add_argument("--steps-per-graph", type=int, default=0,
                     help="steps recorded per graph (0 = the whole timed run in one graph)")
-    ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "rccl"],
+    ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "ipc", "rccl"],
                     help="multi-GPU halo exchange of the native runtime: direct xGMI stores from the stage "
-                         "kernels (graph-captured; default) or RCCL grouped send/recv (eager)")
+                         "kernels (graph-captured; default), IPC copies into the peers' receive slots "
+                         "(hipMemcpyAsync + signal / wait kernels, graph-captured) or RCCL grouped send/recv "
+                         "(eager)")
     ap.add_argument("--partition", default="auto")
     ap.add_argument("--dt", type=float, default=None)
     ap.add_argument("--block", default=None, help="stage block shape BXxBY (default: chosen per grid)")
@@ -328,14 +330,17 @@ def main():
             # C++ runtime, hipGraph replay; between GPUs either direct xGMI
             # stores from the stage kernels (graph-captured) or RCCL grouped
             # P2P on a high-priority stream + interior/boundary overlap (eager)
-            from stsphere.ops.native_runtime import NativeStepper, create_nccl_comm
-            nc = None
+            from stsphere.ops.native_runtime import IpcExchange, NativeStepper, create_nccl_comm
+            nc = ipc = None
             if comm == "xgmi":
                 from stsphere.ops.xgmi import XgmiHalo
                 xg = XgmiHalo(eng, timeout_s=2.0)      # collective; raises on every rank alike
+            elif comm == "ipc":
+                ipc = xg = IpcExchange(eng, IpcExchange.slots_for(eng), timeout_s=2.0)   # collective
             elif comm == "rccl":
                 nc = create_nccl_comm(rank, world, local)
-            runner = NativeStepper(eng, nccl_comm=nc, use_graph=True, steps_per_graph=spg, xgmi=xg)
+            runner = NativeStepper(eng, nccl_comm=nc, use_graph=True, steps_per_graph=spg,
+                                   xgmi=xg if comm == "xgmi" else None, ipc=ipc)
         elif runtime == "graph":
             runner = GraphStepper(eng, spg)
         return eng, runner, xg

@@ -203,10 +203,10 @@ class Solver:
             if comm == "auto":
                 # GPUs: the native runtime with the direct xGMI exchange
                 comm = "xgmi" if (backend == "hip" and c.runtime.graph and not c.runtime.canary) else "torch"
-            if comm in ("xgmi", "rccl") and backend != "hip":
+            if comm in ("xgmi", "rccl", "ipc") and backend != "hip":
                 raise ValueError(f"runtime.comm = {comm} needs the HIP backend")
             self.comm = comm
-            if comm in ("xgmi", "rccl"):
+            if comm in ("xgmi", "rccl", "ipc"):
                 tr = NativeBuffers(self.layout.plan(self.rank), phys0.F, dtype, device)
             else:
                 tr = TorchDistTransport(self.layout.plan(self.rank), phys0.F, dtype, device,
@@ -360,7 +360,7 @@ class Solver:
             return False
         if self.mode == "single":
             return c.graph
-        return self.mode == "spmd" and self.comm in ("xgmi", "rccl")
+        return self.mode == "spmd" and self.comm in ("xgmi", "rccl", "ipc")
 
     def _fused_plan(self, chunks):
         """(use the fused step, steps per launch) for this run.  The fused
@@ -429,7 +429,7 @@ class Solver:
                       f"{spl} step(s) per launch, " + ("direct launches" if self.mode == "single" else "graph replay"))
             return NativeStepper(e, use_graph=True, steps_per_graph=c.steps_per_graph, fused=fk,
                                  steps_per_launch=spl, direct=self.mode == "single")
-        xg = nc = None
+        xg = nc = ipc = None
         if self.mode == "spmd" and self.comm == "xgmi":
             from .ops.xgmi import XgmiHalo
             xg = XgmiHalo(e)
@@ -437,8 +437,13 @@ class Solver:
             if self._nccl is None:
                 self._nccl = create_nccl_comm(self.rank, self.world, self.device.index or 0)
             nc = self._nccl
+        elif self.mode == "spmd" and self.comm == "ipc":
+            from .ops.native_runtime import IpcExchange
+            ipc = IpcExchange(e, IpcExchange.slots_for(e))        # collective (IPC handles)
         self.xgmi = xg
-        return NativeStepper(e, nccl_comm=nc, use_graph=c.graph, steps_per_graph=c.steps_per_graph, xgmi=xg)
+        self._ipc = ipc
+        return NativeStepper(e, nccl_comm=nc, use_graph=c.graph, steps_per_graph=c.steps_per_graph, xgmi=xg,
+                             ipc=ipc)
 
     def step(self, nsteps: int = 1) -> None:
         if nsteps <= 0:

@@ -103,7 +103,8 @@ extern "C" int stsp_device_flags(void) {
 
 // sizes of the C ABI descriptors, checked against the ctypes mirrors (ops/native.py)
 extern "C" int stsp_desc_size(int which) {
-  return which == 0 ? (int)sizeof(StageDesc) : which == 1 ? (int)sizeof(FusedDesc) : -1;
+  return which == 0 ? (int)sizeof(StageDesc) : which == 1 ? (int)sizeof(FusedDesc)
+       : which == 2 ? (int)sizeof(StspOp) : -1;
 }
 
 extern "C" int stsp_rccl_version(void) {
@@ -150,6 +151,35 @@ struct Runtime {
   } while (0)
 
 ncclDataType_t nccl_type(int dtype) { return dtype == 1 ? ncclFloat64 : ncclFloat32; }
+
+// IPC copy transport: the signal and the wait of one exchange (StspOp docs)
+struct IpcFlags { unsigned* f[STSP_MAX_PEERS]; };
+typedef __attribute__((address_space(1))) unsigned rt_gu32;
+__global__ void ipc_signal_kernel(unsigned* counters, IpcFlags fl, int n) {
+  if (threadIdx.x != 0) return;
+  const unsigned v = counters[0] + 1u;
+  counters[0] = v;
+  for (int k = 0; k < n; ++k) __hip_atomic_store((rt_gu32*)fl.f[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void ipc_wait_kernel(unsigned* counters, const unsigned* my, int n, unsigned* err, long long ticks) {
+  __shared__ unsigned want;
+  if (threadIdx.x == 0) want = counters[1] + 1u;
+  __syncthreads();
+  const int k = threadIdx.x;
+  if (k < n) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load((rt_gu32*)(my + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+      if (__hip_atomic_load((rt_gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > ticks) {
+        __hip_atomic_store((rt_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) counters[1] = want;
+}
 size_t elem_bytes(int dtype) { return dtype == 1 ? 8 : 4; }
 
 int run_op(Runtime* rt, const StspOp& op) {
@@ -205,6 +235,39 @@ int run_op(Runtime* rt, const StspOp& op) {
       RT_CHECK(hipStreamWaitEvent(rt->stream, rt->ev_join, 0));
       return 0;
     }
+    case STSP_OP_IPC_SEND: {
+      if (!op.ipc_counters || op.npeers > STSP_MAX_PEERS) {
+        rt->err = "IPC_SEND op without counters";
+        return -4;
+      }
+      RT_CHECK(hipEventRecord(rt->ev_fork, rt->stream));
+      RT_CHECK(hipStreamWaitEvent(rt->comm_stream, rt->ev_fork, 0));
+      const size_t eb = elem_bytes(op.dtype);
+      IpcFlags fl;
+      for (int k = 0; k < op.npeers; ++k) {
+        const char* p = static_cast<const char*>(op.sendbuf) + (size_t)op.send_off[k] * op.slot_elems * eb;
+        RT_CHECK(hipMemcpyAsync(op.ipc_dst[k], p, (size_t)op.send_cnt[k] * op.slot_elems * eb,
+                                hipMemcpyDeviceToDevice, rt->comm_stream));
+        fl.f[k] = op.ipc_flag[k];
+      }
+      hipLaunchKernelGGL(ipc_signal_kernel, dim3(1), dim3(64), 0, rt->comm_stream, op.ipc_counters, fl, op.npeers);
+      RT_CHECK(hipGetLastError());
+      // joined by the IPC_WAIT after the interior stage (the copies overlap it;
+      // the next PACK, which overwrites sendbuf, comes after that join)
+      RT_CHECK(hipEventRecord(rt->ev_join, rt->comm_stream));
+      return 0;
+    }
+    case STSP_OP_IPC_WAIT: {
+      if (!op.ipc_counters || !op.ipc_my_flag || !op.ipc_err || op.nrecv > 64) {
+        rt->err = "IPC_WAIT op without flags";
+        return -4;
+      }
+      RT_CHECK(hipStreamWaitEvent(rt->stream, rt->ev_join, 0));      // this rank's copies are out
+      hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, rt->stream, op.ipc_counters, op.ipc_my_flag,
+                         op.nrecv, op.ipc_err, op.ipc_timeout_ticks);
+      RT_CHECK(hipGetLastError());
+      return 0;
+    }
   }
   rt->err = "unknown op type " + std::to_string(op.type);
   return -5;
@@ -226,8 +289,8 @@ int run_period(Runtime* rt, bool mark) {
       std::fflush(stderr);
     }
     if (mark) {
-      const char* names[] = {"?", "stage", "pack", "comm", "comm_wait", "fused_step"};
-      roctxRangePush(names[op.type >= 1 && op.type <= 5 ? op.type : 0]);
+      const char* names[] = {"?", "stage", "pack", "comm", "comm_wait", "fused_step", "ipc_send", "ipc_wait"};
+      roctxRangePush(names[op.type >= 1 && op.type <= 7 ? op.type : 0]);
     }
     const int rc = run_op(rt, op);
     if (mark) roctxRangePop();

@@ -7,7 +7,7 @@
 extern "C" {
 
 enum StspOpType { STSP_OP_STAGE = 1, STSP_OP_PACK = 2, STSP_OP_COMM_START = 3, STSP_OP_COMM_WAIT = 4,
-                  STSP_OP_FUSED = 5 };
+                  STSP_OP_FUSED = 5, STSP_OP_IPC_SEND = 6, STSP_OP_IPC_WAIT = 7 };
 
 #define STSP_MAX_PEERS 32
 
@@ -33,6 +33,22 @@ typedef struct StspOp {
   // FUSED: one whole SSP-RK step (fused_step.hip); the descriptor is owned by
   // the caller and must outlive the runtime (dt is rewritten by stsp_rt_set_dt)
   void* fused;
+  // IPC copy transport (ops/native_runtime.py::IpcExchange; graph-capturable,
+  // no RCCL).  IPC_SEND, on the comm stream after an event fork: one
+  // hipMemcpyAsync per send peer k of send_cnt[k] slot_elems-element cells from
+  // sendbuf + send_off[k] into ipc_dst[k] (the peer's receive slot this op
+  // fills, IPC-mapped), then one signal kernel: counters[0] += 1 and every
+  // ipc_flag[k] (the peer's flag word for this rank) = counters[0], system
+  // scope.  IPC_WAIT, on the compute stream: counters[1] += 1 and a bounded
+  // spin until every ipc_my_flag[k] (k < nrecv) >= counters[1] (then the
+  // boundary stage reads the slot); a timeout sets ipc_err.  The counters only
+  // grow, so replayed graphs keep their meaning.
+  void* ipc_dst[STSP_MAX_PEERS];
+  unsigned* ipc_flag[STSP_MAX_PEERS];
+  unsigned* ipc_my_flag;
+  unsigned* ipc_counters;
+  unsigned* ipc_err;
+  long long ipc_timeout_ticks;
 } StspOp;
 
 typedef struct StspRtDesc {

@@ -21,7 +21,7 @@ from . import native
 from .native import StageDesc
 
 MAX_PEERS = 32
-OP_STAGE, OP_PACK, OP_COMM_START, OP_COMM_WAIT, OP_FUSED = 1, 2, 3, 4, 5
+OP_STAGE, OP_PACK, OP_COMM_START, OP_COMM_WAIT, OP_FUSED, OP_IPC_SEND, OP_IPC_WAIT = 1, 2, 3, 4, 5, 6, 7
 
 _I32x = ctypes.c_int * MAX_PEERS
 
@@ -37,6 +37,9 @@ class StspOp(ctypes.Structure):
         ("nrecv", ctypes.c_int), ("recv_peer", _I32x), ("recv_off", _I32x), ("recv_cnt", _I32x),
         ("sendbuf", ctypes.c_void_p), ("recvbuf", ctypes.c_void_p), ("slot_elems", ctypes.c_int),
         ("fused", ctypes.c_void_p),
+        ("ipc_dst", ctypes.c_void_p * MAX_PEERS), ("ipc_flag", ctypes.c_void_p * MAX_PEERS),
+        ("ipc_my_flag", ctypes.c_void_p), ("ipc_counters", ctypes.c_void_p), ("ipc_err", ctypes.c_void_p),
+        ("ipc_timeout_ticks", ctypes.c_longlong),
     ]
 
 
@@ -50,6 +53,9 @@ class StspRtDesc(ctypes.Structure):
 
 def _declare(L):
     vp, ci, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    if L.stsp_desc_size(2) != ctypes.sizeof(StspOp):
+        raise RuntimeError(f"StspOp: ctypes mirror is {ctypes.sizeof(StspOp)} bytes, the library's "
+                           f"{L.stsp_desc_size(2)} (stale libstsp.so?)")
     L.stsp_rt_create.argtypes = [ctypes.POINTER(StspRtDesc)]
     L.stsp_rt_create.restype = vp
     L.stsp_rt_destroy.argtypes = [vp]
@@ -124,6 +130,78 @@ def nccl_selftest(comm: int) -> None:
         raise RuntimeError(f"RCCL self send/recv failed ({rc})")
 
 
+class IpcExchange:
+    """IPC copy transport between ranks (``comm: ipc``): the RCCL op list's
+    shape (pack -> exchange on a side stream -> interior blocks -> wait ->
+    boundary blocks) with the exchange done by ``hipMemcpyAsync`` into the
+    peers' IPC-mapped receive slots plus a signal kernel, and a spin kernel
+    in place of the RCCL wait, so the whole step is graph-captured (RCCL
+    2.26.6, the copy torch loads, crashed under capture: round 3).
+
+    Memory (one uncached allocation per rank, ``xgmi.IpcRing``; peers map it):
+    ``nslots`` receive slots of [max num_recv, F] values, then one flag word
+    per receive peer.  Op j of the step's op list fills / reads slot j, so a
+    slot is reused ``nslots`` exchanges later: a peer can be at most one
+    exchange ahead (its exchange j + 1 starts after its stage j, which waited
+    for our exchange j, and our exchange j + 1 is issued after our stage j has
+    read slot j), so two slots would do.  Flags and the rank's own counters
+    only grow, so replayed graphs and restarts keep their meaning; no priming
+    is needed (each stage sends its own input)."""
+
+    def __init__(self, engine, nslots: int, group=None, timeout_s: float = 2.0):
+        from .xgmi import IpcRing, _declare
+        e = engine
+        if nslots < 2:
+            raise ValueError("the IPC exchange needs at least two receive slots")
+        L = _declare(lib())
+        lay = e.layout
+        world, rank = lay.num_ranks, e.rank
+        self.plans = [lay.plan(p) for p in range(world)]
+        plan = self.plans[rank]
+        self.F = e.physics.F
+        esize = torch.tensor([], dtype=e.dtype).element_size()
+        self.esize = esize
+        self.nslots = nslots
+        rmax = max(max(p.num_recv for p in self.plans), 1)
+        self.slot_bytes = -(-rmax * self.F * esize // 256) * 256
+        flag_bytes = 256
+        peers = sorted(set(int(q) for q in plan.send_peers) | set(int(q) for q in plan.recv_peers) | {rank})
+        if len(plan.send_peers) > MAX_PEERS or len(plan.recv_peers) > 64:
+            raise RuntimeError("too many peers for the IPC exchange")
+        self.mem = IpcRing(L, e.device, world, rank, peers, nslots * self.slot_bytes + flag_bytes, group)
+        self.counters = torch.zeros(4, dtype=torch.int32, device=e.device)
+        self.err = torch.zeros(4, dtype=torch.int32, device=e.device)
+        self.timeout_ticks = int(timeout_s * 1e8)
+        self.base = self.mem.base
+        self.my_flag = self.base + nslots * self.slot_bytes
+        # per send peer q: where this rank's cells land in q's slots, and q's flag word for it
+        self.dst0, self.flag = [], []
+        for q in plan.send_peers:
+            qp = self.plans[int(q)]
+            idx = list(int(x) for x in qp.recv_peers).index(rank)
+            off = int(qp.recv_offsets[idx]) * self.F * esize
+            b = int(self.mem.bases[int(q)])
+            self.dst0.append(b + off)
+            self.flag.append(b + nslots * self.slot_bytes + 4 * idx)
+
+    @staticmethod
+    def slots_for(engine) -> int:
+        """Receive slots of a NativeStepper op list: one per exchange in it."""
+        return max(2, engine.integ.period * len(engine.integ.stages))
+
+    def recv_slot(self, j: int) -> int:
+        return self.base + (j % self.nslots) * self.slot_bytes
+
+    def check(self) -> None:
+        if int(self.err[0].item()) != 0:
+            raise RuntimeError("IPC exchange: a peer's cells did not arrive in time (poll timeout)")
+
+    def close(self) -> None:
+        if getattr(self, "mem", None) is not None:
+            self.mem.close()
+            self.mem = None
+
+
 class NativeStepper:
     """Steps an ``Engine(backend='hip')`` entirely from C++.
 
@@ -133,7 +211,7 @@ class NativeStepper:
 
     def __init__(self, engine, nccl_comm: Optional[int] = None, use_graph: bool = True,
                  steps_per_graph: int = 30, roctx: bool = False, stream: Optional[torch.cuda.Stream] = None,
-                 xgmi=None, fused=None, steps_per_launch: int = 1, direct: bool = False):
+                 xgmi=None, fused=None, steps_per_launch: int = 1, direct: bool = False, ipc=None):
         from .hip_compute import HipCompute
         e = engine
         if not isinstance(e.compute, HipCompute):
@@ -151,8 +229,10 @@ class NativeStepper:
             self.remote = False      # remote window cells arrive inside the fused kernel
         if xgmi is not None:
             self.remote = False      # the exchange lives inside the stage kernels
-        if self.remote and not nccl_comm:
-            raise RuntimeError("rank has remote neighbours: pass an RCCL communicator (create_nccl_comm)")
+        self.ipc = ipc
+        if self.remote and not nccl_comm and ipc is None:
+            raise RuntimeError("rank has remote neighbours: pass an RCCL communicator (create_nccl_comm) "
+                               "or an IpcExchange")
         if len(plan.send_peers) > MAX_PEERS or len(plan.recv_peers) > MAX_PEERS:
             raise RuntimeError("too many peers for the native runtime")
         F = e.physics.F
@@ -174,6 +254,7 @@ class NativeStepper:
         ops: List[StspOp] = []
         pool = list(e.pool)
         saved_pool = e.pool
+        xj = 0                       # exchanges so far (IPC receive slot of the next one)
         fdescs = [] if fused is None else ([fused.multi_desc(self.spl)] if self.spl > 1 else list(fused.descs))
         for fd in fdescs:
             op = StspOp()
@@ -200,14 +281,29 @@ class NativeStepper:
                 op.ns = plan.num_send
                 op.send = native.ptr(self.send)
                 ops.append(op)
-                ops.append(self._comm_op(hc.dcode, F))
+                if ipc is not None:
+                    ops.append(self._ipc_send_op(hc.dcode, F, xj))
+                else:
+                    ops.append(self._comm_op(hc.dcode, F))
                 if hc.blk_interior.numel():
                     ops.append(self._stage_op(hc.desc(st, e.dt, hc.blk_interior, hc.blk_interior.numel())))
                 w = StspOp()
-                w.type = OP_COMM_WAIT
+                if ipc is not None:
+                    w.type = OP_IPC_WAIT
+                    w.nrecv = len(plan.recv_peers)
+                    w.ipc_my_flag = ipc.my_flag
+                    w.ipc_counters = native.ptr(ipc.counters)
+                    w.ipc_err = native.ptr(ipc.err)
+                    w.ipc_timeout_ticks = ipc.timeout_ticks
+                else:
+                    w.type = OP_COMM_WAIT
                 ops.append(w)
                 if hc.blk_boundary.numel():
-                    ops.append(self._stage_op(hc.desc(st, e.dt, hc.blk_boundary, hc.blk_boundary.numel(), remote=True)))
+                    bd = hc.desc(st, e.dt, hc.blk_boundary, hc.blk_boundary.numel(), remote=True)
+                    if ipc is not None:
+                        bd.recv = ipc.recv_slot(xj)       # this exchange's receive slot
+                    ops.append(self._stage_op(bd))
+                xj += 1
             pool = [pool[r] for r in e.integ.rotation]
         e.pool = saved_pool
         self._ops = (StspOp * len(ops))(*ops)
@@ -219,7 +315,7 @@ class NativeStepper:
         # ships with this PyTorch (measured: eager loopback exact, captured crash), so
         # op lists with comm run eagerly from C++ unless STSP_GRAPH_COMM=1.
         import os
-        graph_ok = (not self.remote) or os.environ.get("STSP_GRAPH_COMM") == "1"
+        graph_ok = (not self.remote) or ipc is not None or os.environ.get("STSP_GRAPH_COMM") == "1"
         self.use_graph = bool(use_graph and graph_ok)
         # Graph container: the C++ runtime's eager op list recorded by
         # torch.cuda.graph and replayed on torch's current stream.  Measured on
@@ -264,6 +360,22 @@ class NativeStepper:
         op.stage = sd
         return op
 
+    def _ipc_send_op(self, dcode: int, F: int, j: int) -> StspOp:
+        p = self.e.plan
+        ipc = self.ipc
+        op = StspOp()
+        op.type = OP_IPC_SEND
+        op.dtype = dcode
+        op.npeers = len(p.send_peers)
+        for k, (off, cnt) in enumerate(zip(p.send_offsets, p.send_counts)):
+            op.send_off[k], op.send_cnt[k] = off, cnt
+            op.ipc_dst[k] = ipc.dst0[k] + (j % ipc.nslots) * ipc.slot_bytes
+            op.ipc_flag[k] = ipc.flag[k]
+        op.sendbuf = native.ptr(self.send)
+        op.slot_elems = F
+        op.ipc_counters = native.ptr(ipc.counters)
+        return op
+
     def _comm_op(self, dcode: int, F: int) -> StspOp:
         p = self.e.plan
         op = StspOp()
@@ -288,6 +400,8 @@ class NativeStepper:
     def check(self) -> None:
         if self.xgmi is not None:
             self.xgmi.check()
+        if self.ipc is not None:
+            self.ipc.check()
         if self.fused is not None:
             self.fused.check()
 
@@ -297,6 +411,8 @@ class NativeStepper:
         out = []
         if self.xgmi is not None:
             out.append(self.xgmi.err)
+        if self.ipc is not None:
+            out.append(self.ipc.err)
         if self.fused is not None:
             out.append(self.fused.tens["err"])
         return out

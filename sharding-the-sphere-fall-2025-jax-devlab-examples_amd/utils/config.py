@@ -84,7 +84,7 @@ class RuntimeConfig:
     backend: str = "auto"              # auto | hip | torch
     graph: bool = True
     steps_per_graph: int = 30
-    comm: str = "auto"                 # auto | xgmi | rccl | torch | staged  (auto: xgmi on GPUs)
+    comm: str = "auto"                 # auto | xgmi | ipc | rccl | torch | staged  (auto: xgmi on GPUs)
     watchdog_interval: int = 0         # steps; 0 = off
     canary: bool = False               # NaN-prefill ghost slots and check after exchanges (debug)
     block: Optional[List[int]] = None

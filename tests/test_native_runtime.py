@@ -125,3 +125,32 @@ def test_rccl_loopback_full_multigpu_path(nccl_comm, use_graph, phys):
     assert torch.equal(ref.tiles_view(), e.tiles_view())
     ns.close()
 
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+@pytest.mark.parametrize("integ", ["ssprk3", "rk4"])
+def test_ipc_copy_loopback_full_multigpu_path(use_graph, integ):
+    """The IPC copy transport (pack -> hipMemcpyAsync into the peer's receive
+    slot + signal kernel on the comm stream -> interior blocks -> spin-wait
+    kernel -> boundary blocks) on the loopback layout, where every ghost
+    crosses it: bitwise equal to the single-rank engine, and, unlike the RCCL
+    op list, recorded into a graph and replayed."""
+    from stsphere.ops.native_runtime import IpcExchange, NativeStepper
+    g, ref = _single(integ=integ)
+    L = TileLayout(24, 2, 1, ng=2, loopback=True)
+    p = L.plan(0)
+    e = Engine(ShallowWater("tc5"), L, grid=g, device="cuda", backend="hip", dt=ref.dt, integrator=integ,
+               transport=NativeBuffers(p, 4, torch.float64, torch.device("cuda")))
+    assert e.compute.remote and e.compute.blk_boundary.numel() > 0
+    ipc = IpcExchange(e, IpcExchange.slots_for(e))
+    ns = NativeStepper(e, use_graph=use_graph, steps_per_graph=3, ipc=ipc)
+    assert ns.use_graph == use_graph
+    ref.step(9)
+    ns.run(9)
+    torch.cuda.synchronize()
+    ns.check()
+    assert torch.equal(ref.tiles_view(), e.tiles_view())
+    if use_graph:
+        assert ns.stats["graph_steps"] >= 6 and ns.stats["eager_steps"] <= 3
+    ns.close()
+    ipc.close()

@@ -58,8 +58,11 @@ def _spmd_worker(rank, world, port, t, outdir, comm, fused="auto"):
         assert s.comm == comm
         s.run(nsteps=6)
         # the default SPMD runtime is the fused step with the xGMI ring inside
-        # it (every block of the rank's share resident); "off": stage kernels
-        assert (s.fused is not None) == (fused != "off"), s.fused
+        # it (every block of the rank's share resident); "off", or another
+        # exchange: stage kernels (ipc: graph-replayed IPC copies)
+        assert (s.fused is not None) == (fused != "off" and comm == "xgmi"), s.fused
+        if comm == "ipc":
+            assert s.runner.use_graph and s.runner.stats["graph_steps"] > 0, s.runner.stats
         s.save_checkpoint()
         s.run(nsteps=4)
         a = s.gather_global()
@@ -74,14 +77,15 @@ def _spmd_worker(rank, world, port, t, outdir, comm, fused="auto"):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,t,fused", [(2, 1, "auto"), (4, 2, "auto"), (2, 1, "off")])
-def test_spmd_xgmi_solver_matches_single_and_restarts(world, t, fused, tmp_path):
+@pytest.mark.parametrize("world,t,fused,comm", [(2, 1, "auto", "xgmi"), (4, 2, "auto", "xgmi"), (2, 1, "off", "xgmi"),
+                                               (2, 2, "off", "ipc")])
+def test_spmd_xgmi_solver_matches_single_and_restarts(world, t, fused, comm, tmp_path):
     """SPMD ranks sharing one GPU with the default configuration take the
     fused step (xGMI ring inside the kernel); the one-GPU reference runs the
     same kernels (the fused step with the ranks' block size, or the stage
     kernels with fused = off), so the states agree bitwise, restart included."""
     out = str(tmp_path)
-    mp.spawn(_spmd_worker, args=(world, _free_port(), t, out, "xgmi", fused), nprocs=world, join=True)
+    mp.spawn(_spmd_worker, args=(world, _free_port(), t, out, comm, fused), nprocs=world, join=True)
     c = _cfg(1, t, out=str(tmp_path / "ref"))
     c["runtime"]["fused"] = fused
     ref = Solver(c, verbose=False)
