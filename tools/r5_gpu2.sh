@@ -1,6 +1,6 @@
 #!/bin/bash
-# round-5 GPU check 2: persistent TT step (tests + probe), the standalone
-# uncached-memory reproducer
+# round-5 GPU check 2: persistent TT step (tests + probe), the host cost of a
+# timed region, and last the standalone uncached-memory reproducer
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/r5_b
@@ -9,5 +9,7 @@ cd $ROOT
 timeout -k 10 300 python -u -m pytest tests/test_tt_kernels.py -m gpu -x -v --timeout 120 --timeout-method thread -k persistent > $OUT/pytest_tt.log 2>&1; rc=$?; tail -3 $OUT/pytest_tt.log; [ $rc = 0 ] || exit $rc
 timeout -k 10 240 python -u tools/tt_persist_probe.py > $OUT/tt_persist.json 2> $OUT/tt_persist.err || exit $?
 cat $OUT/tt_persist.json
+timeout -k 10 120 python -u tools/launch_overhead.py > $OUT/launch_overhead.json 2> $OUT/launch_overhead.err || exit $?
+cat $OUT/launch_overhead.json
 timeout -k 10 120 ./tools/ring_repro 60 4 > $OUT/ring_repro.json 2> $OUT/ring_repro.err; echo "ring_repro rc=$?"; cat $OUT/ring_repro.json
 echo "== all done"
