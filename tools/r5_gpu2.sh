@@ -11,5 +11,10 @@ timeout -k 10 240 python -u tools/tt_persist_probe.py > $OUT/tt_persist.json 2> 
 cat $OUT/tt_persist.json
 timeout -k 10 120 python -u tools/launch_overhead.py > $OUT/launch_overhead.json 2> $OUT/launch_overhead.err || exit $?
 cat $OUT/launch_overhead.json
+# C720 on one GPU: the fused step, one launch per step (not resident), against the streaming stage
+for dt in fp64 fp32; do
+  timeout -k 10 420 python -u bench.py --N 720 --tiles-per-edge 1 --runtime fused --dtype $dt --steps 10 --warmup 3 > $OUT/c720_fused_$dt.json 2> $OUT/c720_fused_$dt.err || exit $?
+  cat $OUT/c720_fused_$dt.json
+done
 timeout -k 10 120 ./tools/ring_repro 60 4 > $OUT/ring_repro.json 2> $OUT/ring_repro.err; echo "ring_repro rc=$?"; cat $OUT/ring_repro.json
 echo "== all done"
