@@ -75,7 +75,7 @@ def parse(argv=None):
                          "(eager)")
     ap.add_argument("--partition", default="auto")
     ap.add_argument("--dt", type=float, default=None)
-    ap.add_argument("--block", default=None, help="stage block shape BXxBY (default: chosen per grid)")
+    ap.add_argument("--block", default=None, help="stage block shape BXxBY, or the fused runtime's square block size B (default: chosen per grid)")
     ap.add_argument("--timeout", type=float, default=float(os.environ.get("STSP_BENCH_TIMEOUT", "480")),
                     help="--gpus N > 1 (self-launched): kill every rank and print a status=timeout JSON line "
                          "after this many seconds (0 = no deadline)")
@@ -303,7 +303,7 @@ def main():
                 transport = NativeBuffers(layout.plan(rank), phys.F, dtype, device)
             else:
                 transport = TorchDistTransport(layout.plan(rank), phys.F, dtype, device)
-        blk = tuple(int(v) for v in a.block.lower().split("x")) if a.block else None
+        blk = tuple(int(v) for v in a.block.lower().split("x")) if a.block and "x" in a.block.lower() else None
         eng = Engine(phys_factory(), layout, rank, grid=grid, dtype=dtype, device=device, transport=transport,
                      backend=backend, integrator=a.integrator, dt=a.dt, block=blk)
         runner, xg = None, None
@@ -312,7 +312,8 @@ def main():
             # between GPUs the remote window cells travel through the kernel's own xGMI ring
             from stsphere.ops.fused import FusedKernel, rank_cus as _rank_cus
             from stsphere.ops.native_runtime import NativeStepper
-            fk = FusedKernel(eng, timeout_s=2.0)      # collective with several ranks
+            fB = int(a.block) if a.block and a.block.isdigit() else None    # --block B: the fused block size
+            fk = FusedKernel(eng, B=fB, timeout_s=2.0)      # collective with several ranks
             xg = fk if world > 1 else None
             spl = a.steps_per_launch
             if spl == 0:

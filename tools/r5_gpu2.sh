@@ -12,9 +12,10 @@ cat $OUT/tt_persist.json
 timeout -k 10 120 python -u tools/launch_overhead.py > $OUT/launch_overhead.json 2> $OUT/launch_overhead.err || exit $?
 cat $OUT/launch_overhead.json
 # C720 on one GPU: the fused step, one launch per step (not resident), against the streaming stage
-for dt in fp64 fp32; do
-  timeout -k 10 420 python -u bench.py --N 720 --tiles-per-edge 1 --runtime fused --dtype $dt --steps 10 --warmup 3 > $OUT/c720_fused_$dt.json 2> $OUT/c720_fused_$dt.err || exit $?
-  cat $OUT/c720_fused_$dt.json
+for cfg in fp64:20 fp64:16 fp32:20; do
+  dt=${cfg%%:*}; B=${cfg##*:}
+  timeout -k 10 420 python -u bench.py --N 720 --tiles-per-edge 1 --runtime fused --block $B --dtype $dt --steps 10 --warmup 3 > $OUT/c720_fused_${dt}_B$B.json 2> $OUT/c720_fused_${dt}_B$B.err || exit $?
+  cat $OUT/c720_fused_${dt}_B$B.json
 done
 timeout -k 10 120 ./tools/ring_repro 60 4 > $OUT/ring_repro.json 2> $OUT/ring_repro.err; echo "ring_repro rc=$?"; cat $OUT/ring_repro.json
 echo "== all done"
