@@ -659,6 +659,15 @@ extern "C" int stsp_ipc_open(const void* handle, void** out) {
   return e == hipSuccess ? 0 : (int)e;
 }
 
+// Offset of p inside its allocation (an IPC mapping opens at the allocation's
+// base: a ring behind a guard region, STSP_RING_GUARD=1, starts past it).
+extern "C" long long stsp_ipc_offset(void* p) {
+  hipDeviceptr_t base = nullptr;
+  size_t sz = 0;
+  if (hipMemGetAddressRange(&base, &sz, (hipDeviceptr_t)p) != hipSuccess) return -1;
+  return (long long)((char*)p - (char*)base);
+}
+
 extern "C" int stsp_ipc_close(void* p) { return hipIpcCloseMemHandle(p) == hipSuccess ? 0 : -1; }
 
 // Best effort: map every other visible GPU for peer access (already-enabled and

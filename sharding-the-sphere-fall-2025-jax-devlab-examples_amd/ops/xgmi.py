@@ -391,6 +391,7 @@ class IpcRing:
         if not distributed and any(p != rank for p in peers):
             raise RuntimeError("remote peers but no initialised torch.distributed group to exchange IPC handles")
         err = None
+        off = 0
         hb = L.stsp_ipc_handle_bytes()
         h = (ctypes.c_char * hb)()
         try:
@@ -405,22 +406,26 @@ class IpcRing:
                 rc = L.stsp_ipc_get(ctypes.c_void_p(self.base), h)
                 if rc != 0:
                     raise RuntimeError(f"hipIpcGetMemHandle failed ({rc})")
+                off = int(L.stsp_ipc_offset(ctypes.c_void_p(self.base)))
+                if off < 0:
+                    raise RuntimeError("hipMemGetAddressRange failed on the ring")
         except RuntimeError as exc:
             err = exc
         self._agreed(err)
         if distributed:
             allh = [None] * world
-            dist.all_gather_object(allh, bytes(h), group=group)
+            dist.all_gather_object(allh, (bytes(h), off), group=group)
             try:
                 for p in peers:
                     if p == rank:
                         continue
                     ptr = ctypes.c_void_p()
-                    rc = L.stsp_ipc_open((ctypes.c_char * hb).from_buffer_copy(allh[p]), ctypes.byref(ptr))
+                    hp, offp = allh[p]
+                    rc = L.stsp_ipc_open((ctypes.c_char * hb).from_buffer_copy(hp), ctypes.byref(ptr))
                     if rc != 0:
                         raise RuntimeError(f"hipIpcOpenMemHandle of rank {p} failed ({rc})")
                     self.opened.append(ptr.value)
-                    self.bases[p] = ptr.value
+                    self.bases[p] = ptr.value + offp       # the mapping opens at the allocation's base
             except RuntimeError as exc:
                 err = exc
             self._agreed(err)
@@ -467,6 +472,8 @@ def _declare(L):
     L.stsp_ipc_handle_bytes.restype = ci
     L.stsp_ipc_get.argtypes = [vp, vp]
     L.stsp_ipc_get.restype = ci
+    L.stsp_ipc_offset.argtypes = [vp]
+    L.stsp_ipc_offset.restype = ctypes.c_longlong
     L.stsp_ipc_open.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p)]
     L.stsp_ipc_open.restype = ci
     L.stsp_ipc_close.argtypes = [vp]
