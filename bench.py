@@ -293,8 +293,8 @@ def main():
             torch.cuda.synchronize(device)
         if world > 1:
             dist.barrier()
-        if device.type == "cuda":
-            torch.cuda.synchronize(device)
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
 
     def build(comm):
         transport = None

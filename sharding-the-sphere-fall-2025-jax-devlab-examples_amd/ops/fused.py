@@ -49,6 +49,11 @@ from ..models.base import panel_edge_tables
 from ..parallel.layout import TileLayout, ghost_xy
 from ..parallel.topology import neighbor_cells
 
+
+def native_stream(device) -> int:
+    from .native import current_stream_handle
+    return current_stream_handle(device)
+
 REG_P, REG_W, REG_E, REG_S, REG_N = 0, 1, 2, 3, 4
 NREG = 5
 # window sides: 0 = -x, 1 = +x, 2 = -y, 3 = +y
@@ -1387,7 +1392,7 @@ class FusedKernel:
         many steps in one launch, the state back in pool[0]."""
         d = self.descs[parity] if nsteps == 1 else self.multi_desc(nsteps)
         if stream is None:
-            stream = int(torch.cuda.current_stream().cuda_stream)
+            stream = native_stream(self.e.device)
         rc = self._launch_fn(self.dcode, d, stream)
         if rc:
             raise RuntimeError(f"fused step failed with code {rc}")

@@ -214,8 +214,19 @@ def ptr(t) -> int:
     return 0 if t is None else int(t.data_ptr())
 
 
-def current_stream_handle() -> int:
-    return int(torch.cuda.current_stream().cuda_stream)
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def current_stream_handle(device=None) -> int:
+    """hipStream_t of torch's current stream on ``device`` (default: the
+    current device).  The raw query skips building a torch.cuda.Stream object
+    (microseconds on every launch of a timed region)."""
+    if _RAW_STREAM is not None:
+        idx = torch.cuda.current_device() if device is None else (
+            device.index if isinstance(device, torch.device) and device.index is not None
+            else (device if isinstance(device, int) else torch.cuda.current_device()))
+        return int(_RAW_STREAM(idx))
+    return int(torch.cuda.current_stream(device).cuda_stream)
 
 
 def check(rc: int, what: str) -> None:

@@ -341,6 +341,8 @@ class NativeStepper:
         if direct and fused is None:
             raise ValueError("direct launches are the fused runtime's")
         self.direct = bool(direct)
+        self._dev_index = e.device.index if e.device.index is not None else (
+            torch.cuda.current_device() if e.device.type == "cuda" else 0)
         if self.direct:
             self.use_graph = False
         self._warmed = False
@@ -481,9 +483,12 @@ class NativeStepper:
             chunks.append(periods % k)
         return chunks
 
+    def _dev_stream(self) -> int:
+        return native.current_stream_handle(self._dev_index)
+
     def _run_direct(self, nsteps: int) -> None:
         """nsteps (a multiple of the period) as direct fused launches."""
-        st = int(torch.cuda.current_stream(self.e.device).cuda_stream)
+        st = self._dev_stream()
         for _ in range(nsteps // self.period):
             if self.spl > 1:
                 self.fused.launch(0, st, nsteps=self.spl)
