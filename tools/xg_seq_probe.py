@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--K", type=int, default=20)
     ap.add_argument("--launch", default="graph", choices=["graph", "direct"])
     a = ap.parse_args()
+    import numpy as np
     import torch
     import torch.distributed as dist
     from stsphere.engine import Engine
@@ -70,7 +71,18 @@ def main():
         torch.cuda.synchronize(dev)
         t2 = time.time() - T0
         err = [int(x) for x in fk.tens["err"].cpu().tolist()]
-        out["pieces"].append({"name": name, "t0": round(t1, 4), "t1": round(t2, 4), "err": err})
+        rec = {"name": name, "t0": round(t1, 4), "t1": round(t2, 4), "err": err}
+        if err[0]:
+            # where progress stopped: per-block completed-step counters
+            ep = fk.tens["epoch"].cpu().numpy()
+            lo = int(ep.min())
+            stuck = [int(b) for b in np.nonzero(ep == lo)[0]]
+            org = fk.plan.org
+            rec["epoch_min"], rec["epoch_max"] = lo, int(ep.max())
+            rec["epoch_hist"] = {str(int(v)): int((ep == v).sum()) for v in np.unique(ep)}
+            rec["stuck_blocks"] = [[b, int(org[b, 0]), int(org[b, 1]), int(org[b, 2])] for b in stuck[:24]]
+            rec["tiles"] = [int(x) for x in eng.plan.tiles]
+        out["pieces"].append(rec)
         return err[0] == 0
 
     saved = {}
