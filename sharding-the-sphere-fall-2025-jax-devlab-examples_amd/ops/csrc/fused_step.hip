@@ -186,6 +186,20 @@ struct FArgs {
   const T* nrmf;          // [nb][3][NFL] per-face normals of panel-edge blocks (PFN builds)
 };
 
+// The launch's first failure, for the host's message (err[0..5]): the code
+// (1: a remote window cell never arrived, 2: an in-launch producer block never
+// finished its step), the waiting block, its step, what it waited for (ring
+// slot / producer block) and what it saw there (tag / producer's step).
+// First writer wins (compare-and-swap on the code word); vector atomics only.
+__device__ __forceinline__ void fused_fail(int* err, unsigned code, int bid, int xe, int what, int seen) {
+  if (atomicCAS((unsigned*)err, 0u, code) == 0u) {
+    __hip_atomic_store(err + 1, bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(err + 2, xe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(err + 3, what, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(err + 4, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // phase stamp (profiling): lane 0 of every wave, when a.stamps is set;
 // stamps[block][wave < 16][FST_W]: slots 0-15 clocks, 16 HW_ID (SIMD, CU, SE
 // of the wave), 17 XCC_ID (the XCD), 18 the dispatch-order blockIdx.x
@@ -463,7 +477,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         if (ok) break;
         if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
         if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
-          __hip_atomic_store((gu32*)a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          fused_fail(a.err, 1u, bid, xe_, -2 - src, (int)(gr[0] >> 32));
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -742,7 +756,8 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
       if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
       if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
-        if (tid == 0) __hip_atomic_store((gu32*)a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!ok) fused_fail(a.err, 2u, bid, xe, p, __hip_atomic_load(a.epoch + p, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT));
         break;
       }
       __builtin_amdgcn_s_sleep(1);

@@ -213,14 +213,29 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
           }
           if (!s_i[0]) break;
         }
-        if (lane < k) {
-          Ri[lane][lane] = 1.0 / Tm[lane][lane];
-          for (int i = lane - 1; i >= 0; --i) {
-            double s = 0.0;
-            for (int l = i + 1; l <= lane; ++l) s += Tm[i][l] * Ri[l][lane];
-            Ri[i][lane] = -s / Tm[i][i];
+        wsync();
+        // R^-1 by columns in registers: ri[i] = (R^-1)[i][c] for lane c, rows
+        // from the bottom, R's rows as LDS broadcasts (round 5's first version
+        // did this through LDS, each term a dependent LDS round trip: O(k^3/6)
+        // of them on one lane)
+        double ri[TP_KP];
+#pragma unroll
+        for (int i = TP_KP - 1; i >= 0; --i) {
+          asm volatile("" ::: "memory");                   // row i's loads stay in this trip
+          ri[i] = 0.0;
+          if (i < k) {
+            const double rii = Tm[i][i];
+            double sum = 0.0;
+#pragma unroll
+            for (int l = i + 1; l < TP_KP; ++l)
+              if (l < k) sum += Tm[i][l] * ri[l];
+            ri[i] = i == lane ? 1.0 / rii : (i < lane ? -sum / rii : 0.0);
           }
-          for (int i = lane + 1; i < k; ++i) Ri[i][lane] = 0.0;
+        }
+        if (lane < k) {
+#pragma unroll
+          for (int i = 0; i < TP_KP; ++i)
+            if (i < k) Ri[i][lane] = ri[i];
         }
         if (lane == 0 && s_i[0]) __hip_atomic_store((tp_gu32*)(a.flags + 3), 2u, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
@@ -294,52 +309,56 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
       __syncthreads();
       const double tiny = 1e-30 * s_d[1];
       const int m = (k + 1) & ~1;
-      const int pr = tid >> 4, ln = tid & 15;
-      for (int sweep = 0; sweep < 60; ++sweep) {
-        if (tid == 0) s_i[1] = 0;
-        __syncthreads();
-        for (int rd = 0; rd < m - 1; ++rd) {
-          if (pr < m / 2) {
-            const int qa = pr, qb = m - 1 - pr;
-            int p = qa == 0 ? 0 : 1 + (qa - 1 + rd) % (m - 1);
-            int q = qb == 0 ? 0 : 1 + (qb - 1 + rd) % (m - 1);
-            if (p > q) { const int x = p; p = q; q = x; }
-            if (q < k) {
-              double al = 0, be = 0, ga = 0;
-              for (int rr = ln; rr < k; rr += 16) {
-                const double x = sC[rr][p], y = sC[rr][q];
-                al += x * x;
-                be += y * y;
-                ga += x * y;
-              }
-#pragma unroll
-              for (int o = 8; o >= 1; o >>= 1) {
-                al += __shfl_xor(al, o, 16);
-                be += __shfl_xor(be, o, 16);
-                ga += __shfl_xor(ga, o, 16);
-              }
-              if (!(al <= tiny || be <= tiny || fabs(ga) <= 1e-15 * sqrt(al * be))) {
-                const double ze = (be - al) / (2.0 * ga);
-                const double t = (ze >= 0 ? 1.0 : -1.0) / (fabs(ze) + sqrt(1.0 + ze * ze));
-                const double cs = 1.0 / sqrt(1.0 + t * t), sn = cs * t;
-                for (int rr = ln; rr < k; rr += 16) {
+      // one-sided Jacobi on wave 0 alone (round-robin pairs, 8 lanes per pair,
+      // two rows per lane): the rounds synchronise the wave, not the 16-wave
+      // workgroup (round 5's first version: two workgroup barriers per round,
+      // ~47k cycles per core)
+      if (wv == 0) {
+        const int pr = lane >> 3, ln = lane & 7;
+        for (int sweep = 0; sweep < 60; ++sweep) {
+          bool rotated = false;
+          for (int rd = 0; rd < m - 1; ++rd) {
+            if (pr < m / 2) {
+              const int qa = pr, qb = m - 1 - pr;
+              int p = qa == 0 ? 0 : 1 + (qa - 1 + rd) % (m - 1);
+              int q = qb == 0 ? 0 : 1 + (qb - 1 + rd) % (m - 1);
+              if (p > q) { const int x = p; p = q; q = x; }
+              if (q < k) {
+                double al = 0, be = 0, ga = 0;
+                for (int rr = ln; rr < k; rr += 8) {
                   const double x = sC[rr][p], y = sC[rr][q];
-                  sC[rr][p] = cs * x - sn * y;
-                  sC[rr][q] = sn * x + cs * y;
-                  const double u = sW[rr][p], w = sW[rr][q];
-                  sW[rr][p] = cs * u - sn * w;
-                  sW[rr][q] = sn * u + cs * w;
+                  al += x * x;
+                  be += y * y;
+                  ga += x * y;
                 }
-                if (ln == 0) s_i[1] = 1;
+#pragma unroll
+                for (int o = 4; o >= 1; o >>= 1) {
+                  al += __shfl_xor(al, o, 8);
+                  be += __shfl_xor(be, o, 8);
+                  ga += __shfl_xor(ga, o, 8);
+                }
+                if (!(al <= tiny || be <= tiny || fabs(ga) <= 1e-15 * sqrt(al * be))) {
+                  const double ze = (be - al) / (2.0 * ga);
+                  const double t = (ze >= 0 ? 1.0 : -1.0) / (fabs(ze) + sqrt(1.0 + ze * ze));
+                  const double cs = 1.0 / sqrt(1.0 + t * t), sn = cs * t;
+                  for (int rr = ln; rr < k; rr += 8) {
+                    const double x = sC[rr][p], y = sC[rr][q];
+                    sC[rr][p] = cs * x - sn * y;
+                    sC[rr][q] = sn * x + cs * y;
+                    const double u = sW[rr][p], w = sW[rr][q];
+                    sW[rr][p] = cs * u - sn * w;
+                    sW[rr][q] = sn * u + cs * w;
+                  }
+                  rotated = true;
+                }
               }
             }
+            wsync();
           }
-          __syncthreads();
+          if (__builtin_amdgcn_ballot_w64(rotated) == 0) break;
         }
-        const int rot = s_i[1];
-        __syncthreads();
-        if (!rot) break;
       }
+      __syncthreads();
       if (tid < k) {
         double s2 = 0;
         for (int rr = 0; rr < k; ++rr) s2 += sC[rr][tid] * sC[rr][tid];

@@ -1232,7 +1232,7 @@ class FusedKernel:
         self.mem = None
         # per-block step counters (xGMI tags; waits inside a multi-step launch)
         self.tens["epoch"] = torch.zeros(nb, dtype=torch.int32, device=dev)
-        self.tens["err"] = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.tens["err"] = torch.zeros(8, dtype=torch.int32, device=dev)   # code, block, step, what, seen
         self.tens["prod"] = torch.as_tensor(producer_table(P), dtype=torch.int32, device=dev).contiguous()
         # face passes per wave, balanced over the SIMDs (pass_schedule)
         edge_b = np.array([any(int(x) > 0 for x in np.unique(P.reg[b])) for b in range(nb)])
@@ -1371,11 +1371,14 @@ class FusedKernel:
             dist.barrier(group=self.group)
 
     def check(self) -> None:
-        err = int(self.tens["err"][0].item())
+        w = [int(x) for x in self.tens["err"].cpu().tolist()]
+        err = w[0]
         if err == 1:
-            raise RuntimeError("fused step: a peer's window cells did not arrive in time (poll timeout)")
+            raise RuntimeError("fused step: a peer's window cells did not arrive in time (poll timeout; "
+                               f"block {w[1]} at step {w[2]} waited on ring slot {w[3]}, last tag seen {w[4]})")
         if err:
-            raise RuntimeError("fused step: a producer block did not finish its step in time (multi-step launch)")
+            raise RuntimeError("fused step: a producer block did not finish its step in time (multi-step launch; "
+                               f"block {w[1]} at step {w[2]} waited on block {w[3]}, which had finished {w[4]})")
 
     def close(self) -> None:
         if self.mem is not None:
