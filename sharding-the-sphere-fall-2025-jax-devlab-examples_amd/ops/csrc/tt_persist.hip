@@ -171,6 +171,7 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) red[wv][((lane >> 4) + 4 * rr) * TP_KP + col] = acc[rr];
       __syncthreads();
+      if (pass == 0) TP_STAMP(8);
       if (tid < k * k) {
         const int i = tid / k, j = tid - i * k;
         double s = 0.0;
@@ -179,6 +180,7 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
         Gm[i][j] = s;
       }
       __syncthreads();
+      if (pass == 0) TP_STAMP(9);
       if (wv == 0) {
         // shifted Cholesky G + s I = R^T R (pass 0 always shifted; passes 1, 2
         // plain unless a pivot fails), then R^-1 by columns
@@ -241,6 +243,7 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
                                                     __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
+      if (pass == 0) TP_STAMP(10);
       // X <- X R^-1 (own row): y = sum_l x_l Ri[l][.], one Ri row per trip (a
       // fully unrolled product hoisted all k^2 Ri loads into registers)
       if (tid < N) {

@@ -104,6 +104,10 @@ def main():
         for k in range(1, 8):
             d[f"{names[k - 1]}->{names[k]}"] = float(((v[2:, side_, k] - v[2:, side_, k - 1])).mean())
         d["step"] = float(((v[3:, side_, 0] - v[2:-1, side_, 0])).mean())
+        # inside CholeskyQR pass 1: Gram partials, Gram reduce, Cholesky + R^-1, row update
+        for lab2, (k0, k1) in (("qr1_gram", (1, 8)), ("qr1_reduce", (8, 9)), ("qr1_chol", (9, 10)),
+                               ("qr1_update", (10, 2))):
+            d[lab2] = float(((v[2:, side_, k1] - v[2:, side_, k0])).mean())
         ph[lab] = d
     out["persist_phase_cycles"] = ph
     print(json.dumps(out), flush=True)
