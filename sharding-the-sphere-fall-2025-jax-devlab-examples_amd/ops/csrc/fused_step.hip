@@ -50,6 +50,12 @@
 #ifndef STSP_FPROBE_ALLEDGE
 #define STSP_FPROBE_ALLEDGE 0
 #endif
+// Diagnostic build (variant xgfence): system-scope release after each step's
+// ring stores and acquire before each ring poll, to tell a visibility problem
+// of the IPC-mapped rings from a protocol one (multi-rank shared-GPU runs)
+#ifndef STSP_XG_FENCE
+#define STSP_XG_FENCE 0
+#endif
 #ifndef STSP_FPROBE_NOGWAIT
 #define STSP_FPROBE_NOGWAIT 0
 #endif
@@ -469,6 +475,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
         bool ok = true;
+        if (STSP_XG_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 #pragma unroll
         for (int k = 0; k < 4 * G; ++k) {
           gr[k] = __hip_atomic_load(rp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1013,6 +1020,10 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         }
       }
     }
+  }
+  if (XG && STSP_XG_FENCE) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   if (epoch_on) {
     // every storing wave drains its stores, then one lane publishes the step
