@@ -81,6 +81,47 @@ __device__ bool tp_wait(unsigned* f, unsigned want, unsigned* err, long long tic
   }
 }
 
+// X (N x k, row stride k, LDS) times M (k x m, M[l][j] in an LDS array of
+// TP_KP + 1 columns) on the matrix cores: 16-row blocks of X, v_mfma_f64_16x16x4
+// over k in steps of 4 (operands beyond k / m read as 0).  Returns each wave's
+// TP_XB output blocks in registers: the caller
+// synchronises before xmul_store overwrites X (the product is in place).
+// Layouts (checked by the Gram above and tests/test_tt_kernels.py): A 16x4,
+// lane l holds A[l % 16][l / 16]; B 4x16, lane l holds B[l / 16][l % 16];
+// D 16x16, lane l, register i holds D[l / 16 + 4 i][l % 16].
+constexpr int TP_XB = 1024 / 16 / TP_W;           // 16-row blocks per wave at N = 1024
+__device__ __forceinline__ void xmul(const double* X, int N, int k, const double (*M)[TP_KP + 1], int m, int wv,
+                                     int lane, d4 (&acc)[TP_XB]) {
+  const int nb = (N + 15) >> 4;
+#pragma unroll
+  for (int q = 0; q < TP_XB; ++q) {
+    const int b = wv + q * TP_W;
+    d4 c = {0, 0, 0, 0};
+    if (b < nb) {
+      for (int c0 = 0; c0 < k; c0 += 4) {
+        const int row = 16 * b + (lane & 15), kk = c0 + (lane >> 4), col = lane & 15;
+        const double av = (row < N && kk < k) ? X[row * k + kk] : 0.0;
+        const double bv = (kk < k && col < m) ? M[kk][col] : 0.0;
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c, 0, 0, 0);
+      }
+    }
+    acc[q] = c;
+  }
+}
+__device__ __forceinline__ void xmul_store(double* X, int N, int m, int wv, int lane, const d4 (&acc)[TP_XB]) {
+  const int nb = (N + 15) >> 4;
+#pragma unroll
+  for (int q = 0; q < TP_XB; ++q) {
+    const int b = wv + q * TP_W;
+    if (b >= nb) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 16 * b + (lane >> 4) + 4 * i, col = lane & 15;
+      if (row < N && col < m) X[row * m + col] = acc[q][i];
+    }
+  }
+}
+
 #define TP_STAMP(k)                                                                           \
   do {                                                                                        \
     if (a.stamps && tid == 0) a.stamps[((long)call * 2 + side) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
@@ -160,14 +201,24 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
     if (tid < TP_KP * TP_KP) Rt[tid / TP_KP][tid % TP_KP] = (tid / TP_KP == tid % TP_KP) ? 1.0 : 0.0;
     for (int pass = 0; pass < 3; ++pass) {
       // G = X^T X: one MFMA per 4-row group, both operands X[row][col]
-      d4 acc = {0, 0, 0, 0};
+      // (four independent accumulator chains per wave: one chain of 16
+      // dependent MFMAs was ~9k cycles)
+      d4 acc = {0, 0, 0, 0}, acc1 = acc, acc2 = acc, acc3 = acc;
       const int ng = (N + 3) >> 2;
       const int col = lane & 15;
-      for (int g = wv; g < ng; g += TP_W) {
-        const int row = 4 * g + (lane >> 4);
-        const double v = (row < N && col < k) ? X[row * k + col] : 0.0;
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
+      for (int g = wv; g < ng; g += 4 * TP_W) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int row = 4 * (g + u * TP_W) + (lane >> 4);
+          v[u] = (row < N && col < k) ? X[row * k + col] : 0.0;
+        }
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v[0], v[0], acc, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(v[1], v[1], acc1, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(v[2], v[2], acc2, 0, 0, 0);
+        acc3 = __builtin_amdgcn_mfma_f64_16x16x4f64(v[3], v[3], acc3, 0, 0, 0);
       }
+      acc = (acc + acc1) + (acc2 + acc3);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) red[wv][((lane >> 4) + 4 * rr) * TP_KP + col] = acc[rr];
       __syncthreads();
@@ -208,65 +259,61 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
             if (lane > j && lane < k) Tm[j][lane] /= Tm[j][j];
             wsync();
             if (lane > j && lane < k) {
+              // row j and the own column in batches of 4 independent loads
+              // (statically distinct addresses), then the updates: not one
+              // dependent LDS round trip per term
               const double rt = Tm[j][lane];
-              for (int i = j + 1; i <= lane; ++i) Tm[i][lane] -= Tm[j][i] * rt;
+#pragma unroll 1
+              for (int h = (j + 1) & ~3; h <= lane; h += 4) {
+                double rj[4], cl[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {                   // (clamped: h + q may pass k)
+                  const int hq = h + q < TP_KP ? h + q : TP_KP - 1;
+                  rj[q] = Tm[j][hq];
+                  cl[q] = Tm[hq][lane];
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  if (h + q > j && h + q <= lane) Tm[h + q][lane] = cl[q] - rj[q] * rt;
+              }
             }
             wsync();
           }
           if (!s_i[0]) break;
         }
         wsync();
-        // R^-1 by columns in registers: ri[i] = (R^-1)[i][c] for lane c, rows
-        // from the bottom, R's rows as LDS broadcasts (round 5's first version
-        // did this through LDS, each term a dependent LDS round trip: O(k^3/6)
-        // of them on one lane)
-        double ri[TP_KP];
-#pragma unroll
-        for (int i = TP_KP - 1; i >= 0; --i) {
-          asm volatile("" ::: "memory");                   // row i's loads stay in this trip
-          ri[i] = 0.0;
-          if (i < k) {
-            const double rii = Tm[i][i];
+        // R^-1 by columns (lane c: column c), rows from the bottom: each row's
+        // terms are independent LDS loads (R's row i broadcast, the column's
+        // rows below i), one pipelined batch per row (round 5's first version:
+        // a dependent LDS round trip per term, O(k^3 / 6) of them on one lane)
+#pragma unroll 1
+        for (int i = k - 1; i >= 0; --i) {
+          if (lane < k) {
             double sum = 0.0;
 #pragma unroll
-            for (int l = i + 1; l < TP_KP; ++l)
-              if (l < k) sum += Tm[i][l] * ri[l];
-            ri[i] = i == lane ? 1.0 / rii : (i < lane ? -sum / rii : 0.0);
+            for (int l = 1; l < TP_KP; ++l)
+              if (i + l < k) sum += Tm[i][i + l] * Ri[i + l][lane];
+            const double rii = Tm[i][i];
+            Ri[i][lane] = i == lane ? 1.0 / rii : (i < lane ? -sum / rii : 0.0);
           }
-        }
-        if (lane < k) {
-#pragma unroll
-          for (int i = 0; i < TP_KP; ++i)
-            if (i < k) Ri[i][lane] = ri[i];
+          wsync();
         }
         if (lane == 0 && s_i[0]) __hip_atomic_store((tp_gu32*)(a.flags + 3), 2u, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
       if (pass == 0) TP_STAMP(10);
-      // X <- X R^-1 (own row): y = sum_l x_l Ri[l][.], one Ri row per trip (a
-      // fully unrolled product hoisted all k^2 Ri loads into registers)
-      if (tid < N) {
-        double y[TP_KP];
-#pragma unroll
-        for (int j = 0; j < TP_KP; ++j) y[j] = 0.0;
-#pragma unroll 1
-        for (int l = 0; l < k; ++l) {
-          const double xl = X[tid * k + l];
-#pragma unroll
-          for (int j = 0; j < TP_KP; ++j)
-            if (j >= l && j < k) y[j] += xl * Ri[l][j];
-        }
-#pragma unroll
-        for (int j = 0; j < TP_KP; ++j)
-          if (j < k) X[tid * k + j] = y[j];
-      }
+      // X <- X R^-1 on the matrix cores (round 5's first version: one row per
+      // thread, k trips of 16 LDS broadcasts and FMAs: ~21k cycles per pass)
+      d4 xacc[TP_XB];
+      xmul(X, N, k, Ri, k, wv, lane, xacc);
       double rv = 0.0;
       if (tid < k * k) {
         const int i = tid / k, j = tid - i * k;
         for (int l = i; l < k; ++l) rv += Tm[i][l] * Rt[l][j];
       }
       __syncthreads();
+      xmul_store(X, N, k, wv, lane, xacc);
       if (tid < k * k) Rt[tid / k][tid - (tid / k) * k] = rv;
       __syncthreads();
       TP_STAMP(2 + pass);
@@ -410,24 +457,12 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
       __syncthreads();
       TP_STAMP(6);
     }
-    // ---- the new factor X <- X M (k x rn), still in LDS ------------------------
-    double nv[TP_KP];
-#pragma unroll
-    for (int jj = 0; jj < TP_KP; ++jj) nv[jj] = 0.0;
-    if (tid < N) {
-#pragma unroll 1
-      for (int l = 0; l < k; ++l) {
-        const double xl = X[tid * k + l];
-#pragma unroll
-        for (int jj = 0; jj < TP_KP; ++jj)
-          if (jj < rn) nv[jj] += xl * sC[l][jj];
-      }
-    }
-    __syncthreads();
-    if (tid < N) {
-#pragma unroll
-      for (int jj = 0; jj < TP_KP; ++jj)
-        if (jj < rn) X[tid * rn + jj] = nv[jj];
+    // ---- the new factor X <- X M (k x rn), still in LDS (matrix cores) ---------
+    {
+      d4 xacc[TP_XB];
+      xmul(X, N, k, sC, rn, wv, lane, xacc);
+      __syncthreads();
+      xmul_store(X, N, rn, wv, lane, xacc);
     }
     r = rn;
     __syncthreads();
