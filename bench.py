@@ -146,6 +146,13 @@ def launch_ranks(a) -> int:
            *sys.argv[1:]]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if share:
+        # several ranks on ONE GPU: one hardware queue per process.  With the
+        # default four, three or more processes oversubscribe the queues the
+        # scheduler maps at once, it time-slices them, and a multi-step fused
+        # kernel (every rank's blocks resident together) times out
+        # (profiles/r5_rehearse/README.md).  A real node has a GPU per rank.
+        env.setdefault("GPU_MAX_HW_QUEUES", "1")
     env.setdefault("OMP_NUM_THREADS", "1")
     pdir = tempfile.mkdtemp(prefix="stsp_phase_")
     env["STSP_PHASE_DIR"] = pdir

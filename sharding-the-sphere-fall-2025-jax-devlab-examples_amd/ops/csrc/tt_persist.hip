@@ -259,23 +259,8 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
             if (lane > j && lane < k) Tm[j][lane] /= Tm[j][j];
             wsync();
             if (lane > j && lane < k) {
-              // row j and the own column in batches of 4 independent loads
-              // (statically distinct addresses), then the updates: not one
-              // dependent LDS round trip per term
               const double rt = Tm[j][lane];
-#pragma unroll 1
-              for (int h = (j + 1) & ~3; h <= lane; h += 4) {
-                double rj[4], cl[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {                   // (clamped: h + q may pass k)
-                  const int hq = h + q < TP_KP ? h + q : TP_KP - 1;
-                  rj[q] = Tm[j][hq];
-                  cl[q] = Tm[hq][lane];
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                  if (h + q > j && h + q <= lane) Tm[h + q][lane] = cl[q] - rj[q] * rt;
-              }
+              for (int i = j + 1; i <= lane; ++i) Tm[i][lane] -= Tm[j][i] * rt;
             }
             wsync();
           }
