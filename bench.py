@@ -152,7 +152,9 @@ def launch_ranks(a) -> int:
         # scheduler maps at once, it time-slices them, and a multi-step fused
         # kernel (every rank's blocks resident together) times out
         # (profiles/r5_rehearse/README.md).  A real node has a GPU per rank.
-        env.setdefault("GPU_MAX_HW_QUEUES", "1")
+        # (The box exports GPU_MAX_HW_QUEUES=4, so this overrides it;
+        # STSP_SHARE_HW_QUEUES chooses another count.)
+        env["GPU_MAX_HW_QUEUES"] = os.environ.get("STSP_SHARE_HW_QUEUES", "1")
     env.setdefault("OMP_NUM_THREADS", "1")
     pdir = tempfile.mkdtemp(prefix="stsp_phase_")
     env["STSP_PHASE_DIR"] = pdir
