@@ -305,6 +305,12 @@ def main():
             if device.type == "cuda":
                 torch.cuda.synchronize(device)
 
+    # bound of every in-kernel wait for another rank (the kernels set an error
+    # word instead of hanging).  Ranks sharing one GPU (rehearsals) can be
+    # time-sliced by the scheduler for longer than a real node ever waits
+    # (six processes: profiles/r5_rehearse/README.md), hence the longer bound
+    xg_timeout = float(os.environ.get("STSP_XG_TIMEOUT", "30" if share else "2"))
+
     def build(comm):
         transport = None
         if world > 1:
@@ -322,7 +328,7 @@ def main():
             from stsphere.ops.fused import FusedKernel, rank_cus as _rank_cus
             from stsphere.ops.native_runtime import NativeStepper
             fB = int(a.block) if a.block and a.block.isdigit() else None    # --block B: the fused block size
-            fk = FusedKernel(eng, B=fB, timeout_s=2.0)      # collective with several ranks
+            fk = FusedKernel(eng, B=fB, timeout_s=xg_timeout)      # collective with several ranks
             xg = fk if world > 1 else None
             spl = a.steps_per_launch
             if spl == 0:
@@ -344,9 +350,9 @@ def main():
             nc = ipc = None
             if comm == "xgmi":
                 from stsphere.ops.xgmi import XgmiHalo
-                xg = XgmiHalo(eng, timeout_s=2.0)      # collective; raises on every rank alike
+                xg = XgmiHalo(eng, timeout_s=xg_timeout)      # collective; raises on every rank alike
             elif comm == "ipc":
-                ipc = xg = IpcExchange(eng, IpcExchange.slots_for(eng), timeout_s=2.0)   # collective
+                ipc = xg = IpcExchange(eng, IpcExchange.slots_for(eng), timeout_s=xg_timeout)   # collective
             elif comm == "rccl":
                 nc = create_nccl_comm(rank, world, local)
             runner = NativeStepper(eng, nccl_comm=nc, use_graph=True, steps_per_graph=spg,
