@@ -34,7 +34,10 @@
 
 namespace {
 
-constexpr int TP_T = 1024, TP_W = 16, TP_KP = 16, TP_NK = 12288, TP_RPT = 1;
+// 512 threads (8 waves, 2 per SIMD): a 256-VGPR budget, so the k x k
+// Cholesky and R^-1 run from registers (at 1024 threads the 128-VGPR budget
+// forced them through LDS: ~39k cycles per CholeskyQR pass at k = 12)
+constexpr int TP_T = 512, TP_W = 8, TP_KP = 16, TP_NK = 12288, TP_RPT = 2;
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) unsigned long long tp_gu64;
 typedef __attribute__((address_space(1))) unsigned tp_gu32;
@@ -234,57 +237,54 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
       if (pass == 0) TP_STAMP(9);
       if (wv == 0) {
         // shifted Cholesky G + s I = R^T R (pass 0 always shifted; passes 1, 2
-        // plain unless a pivot fails), then R^-1 by columns
+        // plain unless a pivot fails), then R^-1, in registers: lane c holds
+        // column c (g[i] = entry (i, c)), padded to TP_KP with an identity
+        // block (R = diag(R_k, I)) so every loop has static bounds; entries
+        // of other columns arrive by lane shuffles
         const bool adaptive = pass > 0;
+        double trace = 0.0;
+        for (int i = 0; i < k; ++i) trace += Gm[i][i];
+        double g[TP_KP];
+        int fail = 0;
         for (int attempt = adaptive ? 0 : 1; attempt < 2; ++attempt) {
-          if (lane < k)
-            for (int i = 0; i < k; ++i) Tm[i][lane] = Gm[i][lane];
-          wsync();
-          if (lane == 0) {
-            double t = 0.0;
-            for (int i = 0; i < k; ++i) t += Tm[i][i];
-            s_d[0] = t;
-            s_i[0] = 0;
-          }
-          wsync();
-          if (attempt == 1 && lane < k) Tm[lane][lane] += shc * s_d[0];
-          wsync();
-          for (int j = 0; j < k; ++j) {
-            if (lane == 0) {
-              double d = Tm[j][j];
-              if (!(d > 0.0)) { if (!s_i[0]) s_i[0] = j + 1; d = 1.0; }
-              Tm[j][j] = sqrt(d);
-            }
-            wsync();
-            if (lane > j && lane < k) Tm[j][lane] /= Tm[j][j];
-            wsync();
-            if (lane > j && lane < k) {
-              const double rt = Tm[j][lane];
-              for (int i = j + 1; i <= lane; ++i) Tm[i][lane] -= Tm[j][i] * rt;
-            }
-            wsync();
-          }
-          if (!s_i[0]) break;
-        }
-        wsync();
-        // R^-1 by columns (lane c: column c), rows from the bottom: each row's
-        // terms are independent LDS loads (R's row i broadcast, the column's
-        // rows below i), one pipelined batch per row (round 5's first version:
-        // a dependent LDS round trip per term, O(k^3 / 6) of them on one lane)
-#pragma unroll 1
-        for (int i = k - 1; i >= 0; --i) {
-          if (lane < k) {
-            double sum = 0.0;
 #pragma unroll
-            for (int l = 1; l < TP_KP; ++l)
-              if (i + l < k) sum += Tm[i][i + l] * Ri[i + l][lane];
-            const double rii = Tm[i][i];
-            Ri[i][lane] = i == lane ? 1.0 / rii : (i < lane ? -sum / rii : 0.0);
+          for (int i = 0; i < TP_KP; ++i) {
+            g[i] = (i < k && lane < k) ? Gm[i][lane] : (i == lane ? 1.0 : 0.0);
+            if (attempt == 1 && i == lane && lane < k) g[i] += shc * trace;
           }
-          wsync();
+          fail = 0;
+#pragma unroll
+          for (int j = 0; j < TP_KP; ++j) {
+            double d = __shfl(g[j], j);
+            if (!(d > 0.0)) { if (!fail) fail = j + 1; d = 1.0; }
+            const double sq = sqrt(d);
+            if (lane == j) g[j] = sq;
+            if (lane > j) g[j] /= sq;
+            const double rt = g[j];
+#pragma unroll
+            for (int i = j + 1; i < TP_KP; ++i) {
+              const double rji = __shfl(g[j], i);             // R[j][i]: lane i's column
+              if (i <= lane) g[i] -= rji * rt;
+            }
+          }
+          if (!fail) break;
         }
-        if (lane == 0 && s_i[0]) __hip_atomic_store((tp_gu32*)(a.flags + 3), 2u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
+        double ri[TP_KP];
+#pragma unroll
+        for (int i = TP_KP - 1; i >= 0; --i) {
+          const double rii = __shfl(g[i], i);
+          double sum = 0.0;
+#pragma unroll
+          for (int l = i + 1; l < TP_KP; ++l) sum += __shfl(g[i], l) * ri[l];
+          ri[i] = i == lane ? 1.0 / rii : (i < lane ? -sum / rii : 0.0);
+        }
+        if (lane < k) {
+#pragma unroll
+          for (int i = 0; i < TP_KP; ++i)
+            if (i < k) { Tm[i][lane] = g[i]; Ri[i][lane] = ri[i]; }
+        }
+        if (lane == 0 && fail) __hip_atomic_store((tp_gu32*)(a.flags + 3), 2u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
       if (pass == 0) TP_STAMP(10);
