@@ -942,11 +942,13 @@ def pass_schedule(B: int, ncorner: np.ndarray, edge: np.ndarray, G: int, ns: int
     least-loaded wave.  Loads in quarter passes: a regular pass 4, the cube-
     corner wave (wave 0 of a corner block) ``corner``, each ghost-entry wave
     (the waves after it in a panel-edge block) ``ghost``.  ``weights`` (or
-    STSP_FUSED_SCHED) = "corner:ghost" (default "8:1"), or "legacy": round 4's
+    STSP_FUSED_SCHED) = "corner:ghost" (default "5:1": with the lane-pair
+    corner faces the corner wave costs about 1.25 passes; "8:1" measured 2.5 %
+    slower, profiles/r5_fused/sched_weights), or "legacy": round 4's
     placement (one pass per wave in wave order, then the second round from the
     wave after the ghost waves), kept for A/B runs."""
     import os
-    weights = weights or os.environ.get("STSP_FUSED_SCHED", "8:1")
+    weights = weights or os.environ.get("STSP_FUSED_SCHED", "5:1")
     nt = fused_threads(B, ns)
     nw = nt // 64
     counts = stage_face_counts(B, ns)
