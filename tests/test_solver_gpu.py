@@ -190,3 +190,22 @@ def test_solver_run_uses_fused_multi_step_launches(tmp_path):
     h = read_history(str(tmp_path / "f" / "history.zarr"), "h")
     assert h.shape[0] == 5 and np.isfinite(h).all()
     assert ckpt.list_checkpoints(s.checkpoint_root())[-1] == 80
+
+
+def test_solver_run_raises_when_a_fused_wait_times_out(tmp_path, monkeypatch):
+    """a timed-out in-launch producer wait sets the kernel's error
+    word and the state can no longer be trusted; Solver.run must raise (after
+    its pending host work) instead of returning as if the run succeeded.  A
+    zero wait bound makes the first wait that polls at all time out."""
+    import stsphere.ops.fused as F
+    orig = F.FusedKernel.__init__
+
+    def init_zero_timeout(self, engine, B=None, timeout_s=2.0, group=None):
+        orig(self, engine, B=B, timeout_s=0.0, group=group)
+
+    monkeypatch.setattr(F.FusedKernel, "__init__", init_zero_timeout)
+    s = Solver(_cfg(1, 2, out=str(tmp_path / "run")), verbose=False)
+    s.initialize()
+    with pytest.raises(RuntimeError, match="did not finish its step in time"):
+        s.run(nsteps=40)
+    assert s.fused is not None and s.fused.timeout_ticks == 0
