@@ -146,14 +146,17 @@ def launch_ranks(a) -> int:
            *sys.argv[1:]]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    if share:
+    if share and a.comm != "ipc":
         # several ranks on ONE GPU: one hardware queue per process.  With the
         # default four, three or more processes oversubscribe the queues the
         # scheduler maps at once, it time-slices them, and a multi-step fused
         # kernel (every rank's blocks resident together) times out
         # (profiles/r5_rehearse/README.md).  A real node has a GPU per rank.
         # (The box exports GPU_MAX_HW_QUEUES=4, so this overrides it;
-        # STSP_SHARE_HW_QUEUES chooses another count.)
+        # STSP_SHARE_HW_QUEUES chooses another count.  Not for the IPC copy
+        # transport: its comm-stream copies and graph replays crashed inside
+        # hipGraphLaunch with one queue per process, and it needs no
+        # co-residency, only its bounded spin-wait kernels.)
         env["GPU_MAX_HW_QUEUES"] = os.environ.get("STSP_SHARE_HW_QUEUES", "1")
     env.setdefault("OMP_NUM_THREADS", "1")
     pdir = tempfile.mkdtemp(prefix="stsp_phase_")

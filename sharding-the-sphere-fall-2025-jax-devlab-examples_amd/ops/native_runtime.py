@@ -21,7 +21,6 @@ from . import native
 from .native import StageDesc
 
 MAX_PEERS = 32
-IPC_GRAPH_STEPS = 4
 OP_STAGE, OP_PACK, OP_COMM_START, OP_COMM_WAIT, OP_FUSED, OP_IPC_SEND, OP_IPC_WAIT = 1, 2, 3, 4, 5, 6, 7
 
 _I32x = ctypes.c_int * MAX_PEERS
@@ -327,13 +326,6 @@ class NativeStepper:
         self._cxx_graph = self.use_graph and os.environ.get("STSP_NATIVE_GRAPH") == "1"
         d.use_graph = 1 if self._cxx_graph else 0
         self.graph_periods = max(1, steps_per_graph // period)
-        if ipc is not None:
-            # IPC copies: at most IPC_GRAPH_STEPS steps per graph.  A graph of
-            # 20 C96 steps (60 comm-stream forks and joins, 60 copies into
-            # IPC-mapped memory) crashed inside hipGraphLaunch on the host
-            # (SIGSEGV, profiles/r5_rehearse/README.md); 4-step graphs replay
-            # fine (tests/test_solver_gpu.py)
-            self.graph_periods = max(1, min(self.graph_periods, IPC_GRAPH_STEPS // period))
         d.graph_periods = self.graph_periods
         self._graphs = {}          # (periods, copy) -> torch.cuda.CUDAGraph
         self._primed = set()       # (periods, copy) replayed at least once
