@@ -597,6 +597,25 @@ extern "C" long long stsp_xg_check_guards(void) {
   return ok ? (long long)h : -2;
 }
 
+// Ordinary device memory for IPC payload slots (zeroed), and its release.
+extern "C" int stsp_dev_alloc(size_t bytes, void** out) {
+  *out = nullptr;
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) return -1;
+  if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    hipFree(p);
+    return -2;
+  }
+  *out = p;
+  return 0;
+}
+
+extern "C" int stsp_dev_free(void* p) {
+  if (!p) return 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  return hipFree(p) == hipSuccess ? 0 : -3;
+}
+
 // Device allocation with explicit hipExtMallocWithFlags flags (zeroed):
 // 1 = fine-grained, 3 = uncached (exchange-buffer memory-type experiments).
 extern "C" int stsp_alloc_flags(size_t bytes, unsigned flags, void** out) {

@@ -138,9 +138,11 @@ class IpcExchange:
     in place of the RCCL wait, so the whole step is graph-captured (RCCL
     2.26.6, the copy torch loads, crashed under capture: round 3).
 
-    Memory (one uncached allocation per rank, ``xgmi.IpcRing``; peers map it):
-    ``nslots`` receive slots of [max num_recv, F] values, then one flag word
-    per receive peer.  Op j of the step's op list fills / reads slot j, so a
+    Memory (two allocations per rank, ``xgmi.IpcRing``; peers map both):
+    ``nslots`` receive slots of [max num_recv, F] values in ordinary device
+    memory (read only by the boundary blocks, a kernel launched after the
+    wait), and one flag word per receive peer in an uncached ring (polled
+    inside the wait kernel).  Op j of the step's op list fills / reads slot j, so a
     slot is reused ``nslots`` exchanges later: a peer can be at most one
     exchange ahead (its exchange j + 1 starts after its stage j, which waited
     for our exchange j, and our exchange j + 1 is issued after our stage j has
@@ -168,21 +170,25 @@ class IpcExchange:
         peers = sorted(set(int(q) for q in plan.send_peers) | set(int(q) for q in plan.recv_peers) | {rank})
         if len(plan.send_peers) > MAX_PEERS or len(plan.recv_peers) > 64:
             raise RuntimeError("too many peers for the IPC exchange")
-        self.mem = IpcRing(L, e.device, world, rank, peers, nslots * self.slot_bytes + flag_bytes, group)
+        # payload slots in ordinary device memory (written by the peers' copies,
+        # read by the boundary blocks, a later kernel than the wait); the flag
+        # words, polled inside the wait kernel, in an uncached ring.  An uncached
+        # payload ran 383 us per C96 step on a shared GPU (the copies into it)
+        self.mem = IpcRing(L, e.device, world, rank, peers, nslots * self.slot_bytes, group, cached=True)
+        self.fmem = IpcRing(L, e.device, world, rank, peers, flag_bytes, group)
         self.counters = torch.zeros(4, dtype=torch.int32, device=e.device)
         self.err = torch.zeros(4, dtype=torch.int32, device=e.device)
         self.timeout_ticks = int(timeout_s * 1e8)
         self.base = self.mem.base
-        self.my_flag = self.base + nslots * self.slot_bytes
+        self.my_flag = self.fmem.base
         # per send peer q: where this rank's cells land in q's slots, and q's flag word for it
         self.dst0, self.flag = [], []
         for q in plan.send_peers:
             qp = self.plans[int(q)]
             idx = list(int(x) for x in qp.recv_peers).index(rank)
             off = int(qp.recv_offsets[idx]) * self.F * esize
-            b = int(self.mem.bases[int(q)])
-            self.dst0.append(b + off)
-            self.flag.append(b + nslots * self.slot_bytes + 4 * idx)
+            self.dst0.append(int(self.mem.bases[int(q)]) + off)
+            self.flag.append(int(self.fmem.bases[int(q)]) + 4 * idx)
 
     @staticmethod
     def slots_for(engine) -> int:
@@ -197,9 +203,11 @@ class IpcExchange:
             raise RuntimeError("IPC exchange: a peer's cells did not arrive in time (poll timeout)")
 
     def close(self) -> None:
-        if getattr(self, "mem", None) is not None:
-            self.mem.close()
-            self.mem = None
+        for k in ("mem", "fmem"):
+            m = getattr(self, k, None)
+            if m is not None:
+                m.close()
+                setattr(self, k, None)
 
 
 class NativeStepper:

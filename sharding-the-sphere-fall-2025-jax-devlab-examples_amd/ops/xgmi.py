@@ -378,9 +378,14 @@ class IpcRing:
     releasing what they hold) instead of leaving peers inside another
     collective."""
 
-    def __init__(self, L, device, world: int, rank: int, peers, nbytes: int, group=None):
+    def __init__(self, L, device, world: int, rank: int, peers, nbytes: int, group=None, cached: bool = False):
+        """``cached``: ordinary device memory (``hipMalloc``) instead of an
+        uncached ring, for payloads that are only read by a LATER kernel than
+        the one that waited for them (the kernel boundary orders them); flags
+        and tagged granules polled inside a kernel need the uncached ring."""
         import torch.distributed as dist
         self._lib = L
+        self.cached = bool(cached)
         self.device = device
         self.group = group
         self.base = None
@@ -396,7 +401,7 @@ class IpcRing:
         h = (ctypes.c_char * hb)()
         try:
             base = ctypes.c_void_p()
-            rc = L.stsp_xg_alloc(ctypes.c_size_t(nbytes), ctypes.byref(base))
+            rc = (L.stsp_dev_alloc if self.cached else L.stsp_xg_alloc)(ctypes.c_size_t(nbytes), ctypes.byref(base))
             if rc != 0:
                 raise RuntimeError(f"uncached allocation for the xGMI ring failed ({rc})")
             self.base = base.value
@@ -456,7 +461,10 @@ class IpcRing:
         if self.distributed and dist.is_initialized():
             dist.barrier(group=self.group)       # every rank, with or without a ring
         if self.base:
-            L.stsp_xg_free(ctypes.c_void_p(self.base))     # back to the process's ring pool
+            if self.cached:
+                L.stsp_dev_free(ctypes.c_void_p(self.base))
+            else:
+                L.stsp_xg_free(ctypes.c_void_p(self.base))     # back to the process's ring pool
             self.base = None
 
 
@@ -466,6 +474,10 @@ def _declare(L):
     L.stsp_xg_alloc.restype = ci
     L.stsp_xg_free.argtypes = [vp]
     L.stsp_xg_free.restype = ci
+    L.stsp_dev_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]
+    L.stsp_dev_alloc.restype = ci
+    L.stsp_dev_free.argtypes = [vp]
+    L.stsp_dev_free.restype = ci
     L.stsp_xg_pool.argtypes = [ctypes.POINTER(ctypes.c_longlong)]
     L.stsp_xg_pool.restype = ci
     L.stsp_ipc_handle_bytes.argtypes = []
