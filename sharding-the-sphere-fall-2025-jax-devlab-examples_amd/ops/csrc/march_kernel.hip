@@ -81,17 +81,6 @@ __device__ __forceinline__ void frame_to_global(int fr, T xi, T xj, T xn, T& o0,
 #ifndef STSP_MARCH_WPE32
 #define STSP_MARCH_WPE32 4
 #endif
-// Interior strips (no W / E panel-edge column in the wave: PEWE = false) have
-// no edge-column code and fit 3 fp64 waves per SIMD (168 VGPRs); the strips
-// that can hold a W / E panel edge (the first and the last one or two of a
-// tile) run the full kernel in a second launch (round 5: the W / E code alone
-// held the whole stage at two waves per SIMD).
-#ifndef STSP_MARCH_WPE64_INT
-#define STSP_MARCH_WPE64_INT 3
-#endif
-template <typename T, bool PEWE>
-constexpr int march_wpe() { return sizeof(T) == 8 ? (PEWE ? STSP_MARCH_WPE64 : STSP_MARCH_WPE64_INT) : STSP_MARCH_WPE32; }
-
 // ACC: the RK4 accumulator operands (acc_in / acc_out); the SSP-RK3 and Euler
 // stages run the instantiation without them (4 fewer live values per lane).
 // CG: compact geometry: the panel-shared tables of the fused step (1/A,
@@ -99,12 +88,9 @@ constexpr int march_wpe() { return sizeof(T) == 8 ? (PEWE ? STSP_MARCH_WPE64 : S
 // edge lengths by panel-local index) instead of the per-tile records, and the
 // topography gradient formed from b itself (104 instead of 176 B per fp64 cell
 // through HBM; the shared tables are read by all six panels)
-// Job -> column strip: strips [cs0, cs0 + ncsl) of every tile, except that
-// with ``e1`` >= 0 the launch's strip index 0 is strip 0 and index i >= 1 is
-// strip e1 + i - 1 (the edge launch: strip 0 and the last strips).
-template <typename T, int LIM, int R, bool ACC, bool CG, bool XG, bool PEWE>
-__global__ __launch_bounds__(MW * MWPB) __attribute__((amdgpu_waves_per_eu(march_wpe<T, PEWE>())))
-void march_kernel(Args<T> a, int ncsl, int nrs, int njobs, int cs0, int e1) {
+template <typename T, int LIM, int R, bool ACC, bool CG, bool XG>
+__global__ __launch_bounds__(MW * MWPB) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 8 ? STSP_MARCH_WPE64 : STSP_MARCH_WPE32)))
+void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
   pin_args(a);
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -114,8 +100,7 @@ void march_kernel(Args<T> a, int ncsl, int nrs, int njobs, int cs0, int e1) {
   const int gw = xcd_remap(blockIdx.x, gridDim.x) * MWPB + wv;
   if (gw >= njobs) return;
   const int rs = gw % nrs, rest = gw / nrs;
-  const int ci = rest % ncsl, tile = rest / ncsl;
-  const int cs = e1 >= 0 ? (ci == 0 ? 0 : e1 + ci - 1) : cs0 + ci;
+  const int cs = rest % ncs, tile = rest / ncs;
   const int n = a.n, S = a.S, mg = a.mg, pw = a.pw;
   const int x = cs * MO + lane - 2;
   const int xc = x < n + 1 ? x : n + 1;            // lanes past the padded tile load column n + 1
@@ -210,8 +195,8 @@ void march_kernel(Args<T> a, int ncsl, int nrs, int njobs, int cs0, int e1) {
   // ---- panel edges of this wave's part of the tile (wave-uniform) -------------
   const int pe = a.pedge[tile];
   const int lnE = n - cs * MO + 2;                   // lane of column n
-  const bool peW = PEWE && (pe & 1) && cs == 0;
-  const bool peE = PEWE && (pe & 2) && lnE >= 0 && lnE < MW;
+  const bool peW = (pe & 1) && cs == 0;
+  const bool peE = (pe & 2) && lnE >= 0 && lnE < MW;
   // a segment reads rows y0 - 2 .. y1 + 1: the S ghost row -1 when y0 <= 1 and
   // the N ghost row n when y1 >= n - 1 (a segment ending one row short of the
   // tile still takes the slope of row n - 1 across the panel edge)
@@ -547,55 +532,30 @@ void march_kernel(Args<T> a, int ncsl, int nrs, int njobs, int cs0, int e1) {
   }
 }
 
-// One instance over a strip range (see march_kernel's job mapping).
-template <typename T, int LIM, int R, bool ACC, bool CG, bool XG, bool PEWE>
-int march_launch(const Args<T>& a, int ntile, int ncsl, int nrs, int cs0, int e1, hipStream_t s) {
-  const int njobs = ntile * ncsl * nrs;
-  if (njobs <= 0) return 0;
-  const int nb = (njobs + MWPB - 1) / MWPB;
-  hipLaunchKernelGGL((march_kernel<T, LIM, R, ACC, CG, XG, PEWE>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncsl, nrs, njobs,
-                     cs0, e1);
-  return (int)hipGetLastError();
-}
-
-#ifndef STSP_MARCH_SPLIT
-#define STSP_MARCH_SPLIT 1      // 0 (build variant "msplit0"): one launch, every strip the full kernel
-#endif
-template <typename T, int LIM, int R, bool ACC, bool CG>
-int march_split(const Args<T>& a, int n, int ntile, int nrs, hipStream_t s) {
-  if (!STSP_MARCH_SPLIT) return march_launch<T, LIM, R, ACC, CG, false, true>(a, ntile, (n + MO - 1) / MO, nrs, 0, -1, s);
-  // strips that can hold a W / E panel-edge column: 0, and every strip whose
-  // lane of column n (n - cs MO + 2) lies inside the wave
-  const int ncs = (n + MO - 1) / MO;
-  int e1 = ncs;                                   // first strip that can hold column n
-  for (int cs = 1; cs < ncs; ++cs)
-    if (n - cs * MO + 2 < MW) { e1 = cs; break; }
-  const int nint = e1 - 1;                        // interior strips 1 .. e1 - 1
-  const int nedge = 1 + (ncs - e1);
-  int rc = march_launch<T, LIM, R, ACC, CG, false, false>(a, ntile, nint, nrs, 1, -1, s);
-  if (rc) return rc;
-  return march_launch<T, LIM, R, ACC, CG, false, true>(a, ntile, nedge, nrs, 0, e1, s);
-}
-
 template <typename T, int LIM, int R>
 int march_l(const StageDesc* d, hipStream_t s) {
   Args<T> a = make_args<T>(d);
   const int ncs = (d->n + MO - 1) / MO, nrs = (d->n + R - 1) / R;
+  const int njobs = d->ntile * ncs * nrs;
+  const int nb = (njobs + MWPB - 1) / MWPB;
   const bool cg = d->crec && d->lxt && d->torg;
-  if (d->xg) {      // several ranks, direct xGMI exchange (SSP-RK3 / Euler stages, rows R = 4): one launch
+  if (d->xg) {      // several ranks, direct xGMI exchange (SSP-RK3 / Euler stages, rows R = 4)
     if constexpr (R == 4) {
       if (d->acc_out) return -13;
-      if (cg) return march_launch<T, LIM, R, false, true, true, true>(a, d->ntile, ncs, nrs, 0, -1, s);
-      return march_launch<T, LIM, R, false, false, true, true>(a, d->ntile, ncs, nrs, 0, -1, s);
+      if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, false, true, true>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+      else hipLaunchKernelGGL((march_kernel<T, LIM, R, false, false, true>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+      return (int)hipGetLastError();
     }
     return -13;
   }
   if (d->acc_out) {
-    if (cg) return march_split<T, LIM, R, true, true>(a, d->n, d->ntile, nrs, s);
-    return march_split<T, LIM, R, true, false>(a, d->n, d->ntile, nrs, s);
+    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, true, true, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+    else hipLaunchKernelGGL((march_kernel<T, LIM, R, true, false, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+  } else {
+    if (cg) hipLaunchKernelGGL((march_kernel<T, LIM, R, false, true, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
+    else hipLaunchKernelGGL((march_kernel<T, LIM, R, false, false, false>), dim3(nb), dim3(MW * MWPB), 0, s, a, ncs, nrs, njobs);
   }
-  if (cg) return march_split<T, LIM, R, false, true>(a, d->n, d->ntile, nrs, s);
-  return march_split<T, LIM, R, false, false>(a, d->n, d->ntile, nrs, s);
+  return (int)hipGetLastError();
 }
 
 template <typename T, int R>
