@@ -28,14 +28,13 @@ ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
 # own-cell wave placement, nine waves, library sqrt, compare+select slopes,
 # march waves per SIMD) and the timing-only fused-step probes fp_alledge /
 # fp_nogwait (the latter computes wrong numbers by design); xgfence: system-scope
-# fences around the fused step's xGMI ring (multi-rank visibility diagnostic);
-# m32w3: the fp32 streaming stage at 3 waves per SIMD (no spills) instead of 4
+# fences around the fused step's xGMI ring (multi-rank visibility diagnostic)
 VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgc": ["-DSTSP_XG_TAG=0"],
                  "unfused": ["-DSTSP_FUSE_FACES=0"], "pe0": ["-DSTSP_PE_WAVE=0"],
                  "ownw0": ["-DSTSP_OWN_SKIP0=0"], "w9": ["-DSTSP_W10=0"], "swsqrt": ["-DSTSP_HW_SQRT=0"],
                  "selslope": ["-DSTSP_SIGN_SLOPE=0"], "wpe6": ["-DSTSP_WPE=6"], "wpe7": ["-DSTSP_WPE=7"],
                  "fp_alledge": ["-DSTSP_FPROBE_ALLEDGE=1"], "fp_nogwait": ["-DSTSP_FPROBE_NOGWAIT=1"],
-                 "xgfence": ["-DSTSP_XG_FENCE=1"], "m32w3": ["-DSTSP_MARCH_WPE32=3"]}
+                 "xgfence": ["-DSTSP_XG_FENCE=1"]}
 
 
 def lib_for(variant: str = "") -> str:

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Streaming-stage A/B at C720 on one GPU: the march GPU tests on the production
 # build, then bench.py rows (fp64, fp32) per library variant, interleaved.
-#   TAG=r5_march VARIANTS="prod m32w3" bash tools/march_ab.sh   (prod: the default library)
+#   TAG=r5_march VARIANTS="prod <variant>" bash tools/march_ab.sh   (prod: the default library)
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/${TAG:-march_ab}
