@@ -56,6 +56,10 @@
 #ifndef STSP_XG_FENCE
 #define STSP_XG_FENCE 0
 #endif
+// the producer poll: both loads per round trip (1) or round 4's order (0, A/B)
+#ifndef STSP_POLL_1RT
+#define STSP_POLL_1RT 1
+#endif
 #ifndef STSP_FPROBE_NOGWAIT
 #define STSP_FPROBE_NOGWAIT 0
 #endif
@@ -477,12 +481,12 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         bool ok = true;
         if (STSP_XG_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 #pragma unroll
-        for (int k = 0; k < 4 * G; ++k) {
-          gr[k] = __hip_atomic_load(rp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          ok &= (unsigned)(gr[k] >> 32) == want;
-        }
+        for (int k = 0; k < 4 * G; ++k) gr[k] = __hip_atomic_load(rp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned er = __hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < 4 * G; ++k) ok &= (unsigned)(gr[k] >> 32) == want;
         if (ok) break;
-        if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+        if (er != 0) break;
         if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
           fused_fail(a.err, 1u, bid, xe_, -2 - src, (int)(gr[0] >> 32));
           break;
@@ -757,11 +761,24 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   if (wait && tid < 64) {
     // wait for the producers' previous step (wave 0 polls) ...
     const int p = tid < a.PM ? a.prod[(long)bid * a.PM + tid] : -1;
+    const int pa = p >= 0 ? p : bid;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-      const bool ok = p < 0 || __hip_atomic_load(a.epoch + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= xe;
+      // the producers' step counters and the error word in ONE round trip per
+      // poll (read one after the other, a poll took two)
+      // (every lane loads: lanes without a producer read the block's own
+      // counter, so no branch splits the two loads)
+#if STSP_POLL_1RT
+      const unsigned er = __hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int e = __hip_atomic_load(a.epoch + pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool ok = p < 0 || e >= xe;
+      if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+      if (er != 0) break;
+#else
+      const bool ok = p < 0 || __hip_atomic_load(a.epoch + pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= xe;
       if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
       if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+#endif
       if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
         if (!ok) fused_fail(a.err, 2u, bid, xe, p, __hip_atomic_load(a.epoch + p, __ATOMIC_RELAXED,
                                                                       __HIP_MEMORY_SCOPE_AGENT));
