@@ -34,7 +34,7 @@ VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgc": ["-DSTSP_XG_TAG=0"],
                  "ownw0": ["-DSTSP_OWN_SKIP0=0"], "w9": ["-DSTSP_W10=0"], "swsqrt": ["-DSTSP_HW_SQRT=0"],
                  "selslope": ["-DSTSP_SIGN_SLOPE=0"], "wpe6": ["-DSTSP_WPE=6"], "wpe7": ["-DSTSP_WPE=7"],
                  "fp_alledge": ["-DSTSP_FPROBE_ALLEDGE=1"], "fp_nogwait": ["-DSTSP_FPROBE_NOGWAIT=1"],
-                 "xgfence": ["-DSTSP_XG_FENCE=1"], "poll2": ["-DSTSP_POLL_1RT=0"]}
+                 "xgfence": ["-DSTSP_XG_FENCE=1"]}
 
 
 def lib_for(variant: str = "") -> str:

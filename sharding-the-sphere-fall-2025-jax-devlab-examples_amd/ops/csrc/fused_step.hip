@@ -56,10 +56,6 @@
 #ifndef STSP_XG_FENCE
 #define STSP_XG_FENCE 0
 #endif
-// the producer poll: both loads per round trip (1) or round 4's order (0, A/B)
-#ifndef STSP_POLL_1RT
-#define STSP_POLL_1RT 1
-#endif
 #ifndef STSP_FPROBE_NOGWAIT
 #define STSP_FPROBE_NOGWAIT 0
 #endif
@@ -764,21 +760,16 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     const int pa = p >= 0 ? p : bid;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-      // the producers' step counters and the error word in ONE round trip per
-      // poll (read one after the other, a poll took two)
+      // the producers' step counters and the error word in one round trip per
+      // poll (round 4 read them one after the other: no measurable difference
+      // at C96, profiles/r5_fused/poll_ab)
       // (every lane loads: lanes without a producer read the block's own
       // counter, so no branch splits the two loads)
-#if STSP_POLL_1RT
       const unsigned er = __hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int e = __hip_atomic_load(a.epoch + pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const bool ok = p < 0 || e >= xe;
       if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
       if (er != 0) break;
-#else
-      const bool ok = p < 0 || __hip_atomic_load(a.epoch + pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= xe;
-      if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-      if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
-#endif
       if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
         if (!ok) fused_fail(a.err, 2u, bid, xe, p, __hip_atomic_load(a.epoch + p, __ATOMIC_RELAXED,
                                                                       __HIP_MEMORY_SCOPE_AGENT));
