@@ -310,7 +310,9 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   __shared__ T s_len[NFL];                 // face lengths
   __shared__ T s_nrm[2][NRG][3][W + 1];    // line normals per region, component-major
   __shared__ T s_nrmf[PFN ? 3 * NFL : 1];  // PFN: per-face normals of edge blocks, component-major
-  __shared__ unsigned long long s_code[W * W];   // neighbour codes (edge blocks)
+  constexpr int CS = W + 1;                // s_code row stride: odd in 8-byte words, so an x-face
+                                           // pass (lanes down a column) reads it without bank conflicts
+  __shared__ unsigned long long s_code[W * CS];  // neighbour codes (edge blocks)
   __shared__ short s_gs[D::GMAX][2];       // ghost entry: interpolation pair (LDS window index)
   __shared__ T s_gt[D::GMAX];              //              and weight
   // cube-corner faces, resolved on the host (ops/fused.py::corner_tables):
@@ -565,7 +567,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     }
   }
   if (edge) {
-    if (owner) s_code[v * W + u] = cdv;
+    if (owner) s_code[v * CS + u] = cdv;
     if (tid < a.G) { s_gs[tid][0] = (short)gs0; s_gs[tid][1] = (short)gs1; s_gt[tid] = gtv; }
     if (tid < ncor) {
 #pragma unroll
@@ -601,7 +603,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       owner_cell<NS, B>(idx, tu, tv);
       tl_src[k] = cell_src(tu, tv, g_, I_, J_);
       tl_wi[k] = tv * WS + tu;
-      if (edge) s_code[tv * W + tu] = a.code[(long)bid * W * W + tv * W + tu];
+      if (edge) s_code[tv * CS + tu] = a.code[(long)bid * W * W + tv * W + tu];
     }
   }
   auto tail_load = [&](const T* Qin, int xe_, T (&tq)[TPT][4]) {
@@ -653,7 +655,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       if (wnear && !STSP_FPROBE_NOGWAIT) gwait();          // this wave reads ghost entries
       if (near) {
         const int sm = ax ? 2 : 0;                         // side index of -axis; +axis = sm + 1
-        const int ci = fv * W + fu, cj = ci - (ax ? W : 1);  // window indices of b and a
+        const int ci = fv * CS + fu, cj = ci - (ax ? CS : 1);  // code indices of b and a
         const unsigned long long ca = s_code[cj], cb = s_code[ci];
         const int eam = ncode(ca, sm), eap = ncode(ca, sm + 1);
         const int ebm = ncode(cb, sm), ebp = ncode(cb, sm + 1);
