@@ -150,16 +150,65 @@ struct Runtime {
     }                                                                                      \
   } while (0)
 
+bool ipc_fork() {
+  static const bool f = [] {
+    const char* e = getenv("STSP_IPC_FORK");
+    return e && e[0] == '1';
+  }();
+  return f;
+}
+
 ncclDataType_t nccl_type(int dtype) { return dtype == 1 ? ncclFloat64 : ncclFloat32; }
 
-// IPC copy transport: the signal and the wait of one exchange (StspOp docs)
-struct IpcFlags { unsigned* f[STSP_MAX_PEERS]; };
+// IPC copy transport: the copies and signals of one exchange, and its wait
+// (StspOp docs).  counters[0]: exchanges this rank has sent, counters[1]:
+// exchanges it has received (both advanced by the wait kernel, which runs
+// after the copy kernel has finished), counters[4 + k]: slices of peer k
+// copied so far (monotonic).
+struct IpcCopy {
+  const char* src[STSP_MAX_PEERS];
+  char* dst[STSP_MAX_PEERS];
+  unsigned long long bytes[STSP_MAX_PEERS];
+  unsigned* flag[STSP_MAX_PEERS];
+};
+constexpr int IPC_SLICES = 4;        // workgroups per peer
 typedef __attribute__((address_space(1))) unsigned rt_gu32;
-__global__ void ipc_signal_kernel(unsigned* counters, IpcFlags fl, int n) {
-  if (threadIdx.x != 0) return;
-  const unsigned v = counters[0] + 1u;
-  counters[0] = v;
-  for (int k = 0; k < n; ++k) __hip_atomic_store((rt_gu32*)fl.f[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+typedef __attribute__((address_space(1))) unsigned long long rt_gu64;
+// One kernel per exchange instead of a hipMemcpyAsync per peer and a signal
+// kernel (each copy node cost ~30 us per stage, profiles/r5_rehearse).  Slice
+// sl of peer k is copied in V-sized words, four loads in flight per thread;
+// every wave drains its stores, workgroup 0-thread releases them to system
+// scope (L2 write-back), and the last slice of a peer to finish (told by a
+// monotonic per-peer counter) stores the peer's flag.
+template <typename V>
+__global__ void __launch_bounds__(256) ipc_copy_signal_kernel(unsigned* counters, IpcCopy c) {
+  const int k = blockIdx.x / IPC_SLICES, sl = blockIdx.x % IPC_SLICES;
+  const unsigned long long n = c.bytes[k] / sizeof(V);   // host checked: a multiple of sizeof(V), aligned
+  const unsigned long long per = (n + IPC_SLICES - 1) / IPC_SLICES;
+  const unsigned long long b0 = per * sl, b1 = b0 + per < n ? b0 + per : n;
+  const V* src = reinterpret_cast<const V*>(c.src[k]);
+  V* dst = reinterpret_cast<V*>(c.dst[k]);
+  constexpr unsigned U = 4;
+  unsigned long long i = b0 + threadIdx.x;
+  for (; i + (U - 1) * 256 < b1; i += U * 256) {
+    V r[U];
+#pragma unroll
+    for (unsigned u = 0; u < U; ++u) r[u] = src[i + u * 256];
+#pragma unroll
+    for (unsigned u = 0; u < U; ++u) dst[i + u * 256] = r[u];
+  }
+  for (; i < b1; i += 256) dst[i] = src[i];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __atomic_thread_fence(__ATOMIC_RELEASE);                // system scope: write back L2
+    const unsigned done = __hip_atomic_fetch_add((rt_gu32*)(counters + 4 + k), 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    if (done % IPC_SLICES == 0) {
+      __atomic_thread_fence(__ATOMIC_SEQ_CST);
+      __hip_atomic_store((rt_gu32*)c.flag[k], counters[0] + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 __global__ void ipc_wait_kernel(unsigned* counters, const unsigned* my, int n, unsigned* err, long long ticks) {
   __shared__ unsigned want;
@@ -178,7 +227,10 @@ __global__ void ipc_wait_kernel(unsigned* counters, const unsigned* my, int n, u
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) counters[1] = want;
+  if (threadIdx.x == 0) {
+    counters[1] = want;
+    counters[0] += 1u;                 // this rank's copy kernel of the exchange has finished (join)
+  }
 }
 size_t elem_bytes(int dtype) { return dtype == 1 ? 8 : 4; }
 
@@ -240,21 +292,45 @@ int run_op(Runtime* rt, const StspOp& op) {
         rt->err = "IPC_SEND op without counters";
         return -4;
       }
-      RT_CHECK(hipEventRecord(rt->ev_fork, rt->stream));
-      RT_CHECK(hipStreamWaitEvent(rt->comm_stream, rt->ev_fork, 0));
-      const size_t eb = elem_bytes(op.dtype);
-      IpcFlags fl;
-      for (int k = 0; k < op.npeers; ++k) {
-        const char* p = static_cast<const char*>(op.sendbuf) + (size_t)op.send_off[k] * op.slot_elems * eb;
-        RT_CHECK(hipMemcpyAsync(op.ipc_dst[k], p, (size_t)op.send_cnt[k] * op.slot_elems * eb,
-                                hipMemcpyDeviceToDevice, rt->comm_stream));
-        fl.f[k] = op.ipc_flag[k];
+      // STSP_IPC_FORK=1: the copy kernel runs on the comm stream, overlapping
+      // the interior stage; default: in order on the compute stream (the
+      // cross-stream fork and join of a graph cost more than the copy).
+      const bool fork = ipc_fork();
+      hipStream_t cs = fork ? rt->comm_stream : rt->stream;
+      if (fork) {
+        RT_CHECK(hipEventRecord(rt->ev_fork, rt->stream));
+        RT_CHECK(hipStreamWaitEvent(rt->comm_stream, rt->ev_fork, 0));
       }
-      hipLaunchKernelGGL(ipc_signal_kernel, dim3(1), dim3(64), 0, rt->comm_stream, op.ipc_counters, fl, op.npeers);
-      RT_CHECK(hipGetLastError());
+      const size_t eb = elem_bytes(op.dtype);
+      IpcCopy cp;
+      for (int k = 0; k < op.npeers; ++k) {
+        cp.src[k] = static_cast<const char*>(op.sendbuf) + (size_t)op.send_off[k] * op.slot_elems * eb;
+        cp.dst[k] = static_cast<char*>(op.ipc_dst[k]);
+        cp.bytes[k] = (unsigned long long)op.send_cnt[k] * op.slot_elems * eb;
+        cp.flag[k] = op.ipc_flag[k];
+      }
+      if (op.npeers > 0) {
+        bool w16 = true;                 // 16-byte words when every pointer and size allows
+        for (int k = 0; k < op.npeers; ++k)
+          w16 = w16 && (((uintptr_t)cp.src[k] | (uintptr_t)cp.dst[k] | (uintptr_t)cp.bytes[k]) % 16 == 0);
+        bool w4 = true;
+        for (int k = 0; k < op.npeers; ++k)
+          w4 = w4 && (((uintptr_t)cp.src[k] | (uintptr_t)cp.dst[k] | (uintptr_t)cp.bytes[k]) % 4 == 0);
+        if (!w4) {
+          rt->err = "IPC_SEND: payloads must be 4-byte aligned";
+          return -1;
+        }
+        if (w16)
+          hipLaunchKernelGGL(ipc_copy_signal_kernel<uint4>, dim3(op.npeers * IPC_SLICES), dim3(256), 0,
+                             cs, op.ipc_counters, cp);
+        else
+          hipLaunchKernelGGL(ipc_copy_signal_kernel<unsigned>, dim3(op.npeers * IPC_SLICES), dim3(256), 0,
+                             cs, op.ipc_counters, cp);
+        RT_CHECK(hipGetLastError());
+      }
       // joined by the IPC_WAIT after the interior stage (the copies overlap it;
       // the next PACK, which overwrites sendbuf, comes after that join)
-      RT_CHECK(hipEventRecord(rt->ev_join, rt->comm_stream));
+      if (fork) RT_CHECK(hipEventRecord(rt->ev_join, rt->comm_stream));
       return 0;
     }
     case STSP_OP_IPC_WAIT: {
@@ -262,7 +338,7 @@ int run_op(Runtime* rt, const StspOp& op) {
         rt->err = "IPC_WAIT op without flags";
         return -4;
       }
-      RT_CHECK(hipStreamWaitEvent(rt->stream, rt->ev_join, 0));      // this rank's copies are out
+      if (ipc_fork()) RT_CHECK(hipStreamWaitEvent(rt->stream, rt->ev_join, 0));   // this rank's copies are out
       hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, rt->stream, op.ipc_counters, op.ipc_my_flag,
                          op.nrecv, op.ipc_err, op.ipc_timeout_ticks);
       RT_CHECK(hipGetLastError());

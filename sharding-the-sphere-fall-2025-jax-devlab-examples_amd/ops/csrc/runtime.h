@@ -34,15 +34,18 @@ typedef struct StspOp {
   // the caller and must outlive the runtime (dt is rewritten by stsp_rt_set_dt)
   void* fused;
   // IPC copy transport (ops/native_runtime.py::IpcExchange; graph-capturable,
-  // no RCCL).  IPC_SEND, on the comm stream after an event fork: one
-  // hipMemcpyAsync per send peer k of send_cnt[k] slot_elems-element cells from
-  // sendbuf + send_off[k] into ipc_dst[k] (the peer's receive slot this op
-  // fills, IPC-mapped), then one signal kernel: counters[0] += 1 and every
-  // ipc_flag[k] (the peer's flag word for this rank) = counters[0], system
-  // scope.  IPC_WAIT, on the compute stream: counters[1] += 1 and a bounded
-  // spin until every ipc_my_flag[k] (k < nrecv) >= counters[1] (then the
-  // boundary stage reads the slot); a timeout sets ipc_err.  The counters only
-  // grow, so replayed graphs keep their meaning.
+  // no RCCL).  IPC_SEND, in order on the compute stream (on the comm stream
+  // after an event fork, joined by IPC_WAIT, with STSP_IPC_FORK=1): one
+  // copy kernel (4 workgroups per send peer k) stores send_cnt[k]
+  // slot_elems-element cells from sendbuf + send_off[k] into ipc_dst[k] (the
+  // peer's receive slot this op fills, IPC-mapped) and releases them at
+  // system scope; the last workgroup of peer k sets ipc_flag[k] (the peer's
+  // flag word for this rank) = counters[0] + 1.  IPC_WAIT, on the compute stream (after the
+  // join): a bounded spin until every ipc_my_flag[k] (k < nrecv) >=
+  // counters[1] + 1, then counters[1] += 1 and counters[0] += 1 (the boundary
+  // stage then reads the slot); a timeout sets ipc_err.  counters[4 + k] count
+  // peer k's finished slices.  The counters only grow, so replayed graphs keep
+  // their meaning.
   void* ipc_dst[STSP_MAX_PEERS];
   unsigned* ipc_flag[STSP_MAX_PEERS];
   unsigned* ipc_my_flag;

@@ -176,7 +176,7 @@ class IpcExchange:
         # payload ran 383 us per C96 step on a shared GPU (the copies into it)
         self.mem = IpcRing(L, e.device, world, rank, peers, nslots * self.slot_bytes, group, cached=True)
         self.fmem = IpcRing(L, e.device, world, rank, peers, flag_bytes, group)
-        self.counters = torch.zeros(4, dtype=torch.int32, device=e.device)
+        self.counters = torch.zeros(4 + MAX_PEERS, dtype=torch.int32, device=e.device)   # runtime.cpp ipc kernels
         self.err = torch.zeros(4, dtype=torch.int32, device=e.device)
         self.timeout_ticks = int(timeout_s * 1e8)
         self.base = self.mem.base
