@@ -130,8 +130,8 @@ def test_rccl_loopback_full_multigpu_path(nccl_comm, use_graph, phys):
 @pytest.mark.parametrize("use_graph", [True, False])
 @pytest.mark.parametrize("integ", ["ssprk3", "rk4"])
 def test_ipc_copy_loopback_full_multigpu_path(use_graph, integ):
-    """The IPC copy transport (pack -> hipMemcpyAsync into the peer's receive
-    slot + signal kernel on the comm stream -> interior blocks -> spin-wait
+    """The IPC copy transport (pack -> one copy kernel into the peer's receive
+    slot, which also stores the peer's flag -> interior blocks -> spin-wait
     kernel -> boundary blocks) on the loopback layout, where every ghost
     crosses it: bitwise equal to the single-rank engine, and, unlike the RCCL
     op list, recorded into a graph and replayed."""
@@ -152,5 +152,31 @@ def test_ipc_copy_loopback_full_multigpu_path(use_graph, integ):
     assert torch.equal(ref.tiles_view(), e.tiles_view())
     if use_graph:
         assert ns.stats["graph_steps"] >= 6 and ns.stats["eager_steps"] <= 3
+    ns.close()
+    ipc.close()
+
+
+@pytest.mark.parametrize("phys,dtype", [("adv", torch.float32), ("adv", torch.float64), ("swe", torch.float32)])
+def test_ipc_copy_kernel_word_sizes(phys, dtype):
+    """The IPC copy kernel (runtime.cpp::ipc_copy_signal_kernel) copies
+    16-byte words when every payload allows, else 4-byte words: one field in
+    fp32 (tracer advection) gives payloads that are not 16-byte multiples.
+    Each case is bitwise equal to the single-rank engine of the same dtype,
+    graph-replayed."""
+    from stsphere.ops.native_runtime import IpcExchange, NativeStepper
+    mk = {"swe": lambda: ShallowWater("tc5"), "adv": lambda: Advection()}[phys]
+    g = CubedSphereGrid(24)
+    ref = Engine(mk(), TileLayout(24, 2, 1, ng=2), grid=g, dtype=dtype, device="cuda", backend="hip")
+    L = TileLayout(24, 2, 1, ng=2, loopback=True)
+    F = ref.physics.F
+    e = Engine(mk(), L, grid=g, dtype=dtype, device="cuda", backend="hip", dt=ref.dt,
+               transport=NativeBuffers(L.plan(0), F, dtype, torch.device("cuda")))
+    ipc = IpcExchange(e, IpcExchange.slots_for(e))
+    ns = NativeStepper(e, use_graph=True, steps_per_graph=3, ipc=ipc)
+    ref.step(6)
+    ns.run(6)
+    torch.cuda.synchronize()
+    ns.check()
+    assert torch.equal(ref.tiles_view(), e.tiles_view())
     ns.close()
     ipc.close()
