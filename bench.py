@@ -71,7 +71,7 @@ def parse(argv=None):
     ap.add_argument("--comm", default="auto", choices=["auto", "xgmi", "ipc", "rccl"],
                     help="multi-GPU halo exchange of the native runtime: direct xGMI stores from the stage "
                          "kernels (graph-captured; default), IPC copies into the peers' receive slots "
-                         "(hipMemcpyAsync + signal / wait kernels, graph-captured) or RCCL grouped send/recv "
+                         "(a copy+signal kernel and a wait kernel, graph-captured) or RCCL grouped send/recv "
                          "(eager)")
     ap.add_argument("--partition", default="auto")
     ap.add_argument("--dt", type=float, default=None)

@@ -132,11 +132,13 @@ def nccl_selftest(comm: int) -> None:
 
 class IpcExchange:
     """IPC copy transport between ranks (``comm: ipc``): the RCCL op list's
-    shape (pack -> exchange on a side stream -> interior blocks -> wait ->
-    boundary blocks) with the exchange done by ``hipMemcpyAsync`` into the
-    peers' IPC-mapped receive slots plus a signal kernel, and a spin kernel
-    in place of the RCCL wait, so the whole step is graph-captured (RCCL
-    2.26.6, the copy torch loads, crashed under capture: round 3).
+    shape (pack -> exchange -> interior blocks -> wait -> boundary blocks)
+    with the exchange done by one copy kernel that stores into the peers'
+    IPC-mapped receive slots and sets their flags (runtime.cpp
+    ``ipc_copy_signal_kernel``; in order on the compute stream, or on the
+    comm stream with ``STSP_IPC_FORK=1``), and a spin kernel in place of the
+    RCCL wait, so the whole step is graph-captured (RCCL 2.26.6, the copy
+    torch loads, crashed under capture: round 3).
 
     Memory (two allocations per rank, ``xgmi.IpcRing``; peers map both):
     ``nslots`` receive slots of [max num_recv, F] values in ordinary device
