@@ -1140,14 +1140,19 @@ int launch_fused(const FusedDesc* d, hipStream_t s) {
 
 }  // namespace
 
-// Block sizes: 8 and 12 for ranks that hold few blocks (a rank's share of a
-// multi-GPU run: C96 over 8 GPUs is 3 tiles of 48 per rank, 108 blocks of 8;
+// Block sizes: 6, 8 and 12 for ranks that hold few blocks (a rank's share of
+// a multi-GPU run: C96 over 8 GPUs is 3 tiles of 48 per rank, 192 blocks of 6;
 // the per-block latency, which sets the step while every block is resident,
-// falls with the window: 1000 faces per step at B = 8 against 2584 at 16),
-// 16 (C96 on one GPU: 216 blocks), 18 and 20 (C180 tiles).
+// falls with the window: 724 faces per step at B = 6, 1000 at 8, 2584 at 16;
+// 216 resident blocks step in 8.7 us at B = 6 against 9.1 at 8, 9.8 against
+// 10.6 through the xGMI ring, profiles/r5_rehearse/b6), 16 (C96 on one GPU:
+// 216 blocks), 18 and 20 (C180 tiles).
 extern "C" int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stream) {
   if (d->ns != 3) return -1;
-  if (d->B == 8) {
+  if (d->B == 6) {
+    if (dtype == 1) return launch_fused<double, 3, 6>(d, stream);
+    if (dtype == 0) return launch_fused<float, 3, 6>(d, stream);
+  } else if (d->B == 8) {
     if (dtype == 1) return launch_fused<double, 3, 8>(d, stream);
     if (dtype == 0) return launch_fused<float, 3, 8>(d, stream);
   } else if (d->B == 12) {

@@ -873,7 +873,7 @@ class FusedTorch:
 # Device tables + descriptors of the gfx950 kernel (fused_step.hip)
 # ---------------------------------------------------------------------------
 
-FUSED_BLOCKS = (8, 12, 16, 18, 20)  # block sizes the kernel is instantiated for
+FUSED_BLOCKS = (6, 8, 12, 16, 18, 20)  # block sizes the kernel is instantiated for
 
 
 def rank_cus(device) -> int:

@@ -173,7 +173,7 @@ def test_fused_supported_reasons():
     e = Engine(ShallowWater("tc5"), L, integrator="rk4")
     assert "SSP-RK3" in fused_supported(e)
     e = Engine(ShallowWater("tc5"), TileLayout(28, 2, 1, ng=2))
-    assert "multiple of 8 or 12 or 16 or 18 or 20" in fused_supported(e)
+    assert "multiple of 6 or 8 or 12 or 16 or 18 or 20" in fused_supported(e)
     assert fused_supported(Engine(ShallowWater("tc5"), TileLayout(24, 2, 1, ng=2))) is None   # B = 12
     assert fused_supported(Engine(ShallowWater("tc5"), TileLayout(36, 2, 1, ng=2))) is None   # B = 18
     assert fused_supported(Engine(ShallowWater("tc5"), TileLayout(40, 2, 1, ng=2))) is None   # B = 20
@@ -199,8 +199,8 @@ def _gpu_pair(N, t, dtype=torch.float64, case="tc5", lim=2):
                                           (54, 1, "tc2", 1), (40, 2, "tc5", 2), (60, 3, "tc6", 2),
                                           (48, 4, "tc5", 2), (72, 3, "tc5", 2)])
 def test_fused_kernel_fp64_matches_oracle(N, t, case, lim):
-    """Every block size through the residency-aware choice: 8 ((32, 2), (48, 1),
-    (48, 3), (32, 1)), 12 ((48, 4), (72, 3)), 16 (96, 2), 18 ((36, 2), (54, 1)), 20."""
+    """Every block size through the residency-aware choice: 6 (36, 2), 8 ((32, 2),
+    (48, 1), (48, 3), (32, 1)), 12 ((48, 4), (72, 3)), 16 (96, 2), 18 (54, 1), 20."""
     from stsphere.ops.fused import FusedKernel
     ref, hip = _gpu_pair(N, t, case=case, lim=lim)
     fk = FusedKernel(hip)
@@ -209,6 +209,34 @@ def test_fused_kernel_fp64_matches_oracle(N, t, case, lim):
         fk.step(1)
         torch.cuda.synchronize()
         assert _relerr(ref, hip) < 1e-11
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,t,case,lim", [(36, 1, "tc5", 2), (24, 2, "tc6", 3), (12, 1, "tc2", 1)])
+def test_fused_kernel_b6_matches_oracle_and_multi_step(N, t, case, lim):
+    """The B = 6 instance (a rank's share of C96 over 8 GPUs: 3 tiles of 48,
+    192 blocks): the oracle at 1e-11 over single-step launches, and a
+    multi-step launch bitwise equal to single steps."""
+    from stsphere.ops.fused import FusedKernel
+    ref, hip = _gpu_pair(N, t, case=case, lim=lim)
+    fk = FusedKernel(hip, B=6)
+    for _ in range(2):
+        ref.step(1)
+        fk.step(1)
+        torch.cuda.synchronize()
+        assert _relerr(ref, hip) < 1e-11
+    from stsphere.ops.native_runtime import NativeStepper
+    _, a = _gpu_pair(N, t, case=case, lim=lim)
+    _, b = _gpu_pair(N, t, case=case, lim=lim)
+    b.dt = a.dt
+    FusedKernel(a, B=6).step(6)
+    fb = FusedKernel(b, B=6)
+    r = NativeStepper(b, use_graph=True, steps_per_graph=6, fused=fb, steps_per_launch=6)
+    r.run(6)
+    torch.cuda.synchronize()
+    fb.check()
+    assert torch.equal(a.tiles_view(), b.tiles_view())
+    r.close()
 
 
 @pytest.mark.gpu
@@ -511,7 +539,7 @@ def test_fused_loopback_plan_equals_one_rank_cpu(N, t, B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,t", [(32, 2), (96, 2)])
+@pytest.mark.parametrize("N,t", [(32, 2), (96, 2), (36, 1)])
 def test_fused_loopback_kernel_equals_one_rank(N, t):
     """The gfx950 fused kernel on a loopback layout (the xGMI ring protocol
     through the rank's own ring, tagged granules every step, one and several
