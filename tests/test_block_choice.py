@@ -34,3 +34,17 @@ def test_ppm_never_gets_a_block_too_small_for_its_window():
 def test_without_device_info_falls_back_to_least_waste():
     assert choose_block(48) == (16, 16)
     assert choose_block(40) in ((16, 16), (32, 8))
+
+
+def test_fused_block_by_rank_share():
+    """ops/fused.py::fused_block: the smallest fused block whose blocks are all
+    resident on the rank's CUs.  C96 (24 tiles of 48) on 1 / 2 / 4 / 8 GPUs of
+    256 CUs: B = 16 (216 blocks), 12 (192), 8 (216), 6 (192,
+    profiles/r5_rehearse/b6); a shared-GPU rehearsal counts its share of the
+    CUs; a grid whose blocks never all fit takes the largest block."""
+    from stsphere.ops.fused import fused_block
+    assert [fused_block(48, 24 // r, 256) for r in (1, 2, 4, 8)] == [16, 12, 8, 6]
+    assert fused_block(48, 3, 32) == 16                  # 8 ranks sharing one GPU
+    assert fused_block(90, 24, 256) == 18                # C180 on one GPU: never resident
+    assert fused_block(96, 1, 256) == 6                  # one panel per rank (6 GPUs): 256 blocks
+    assert fused_block(14, 6, 256) is None
