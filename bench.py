@@ -73,6 +73,11 @@ def parse(argv=None):
                          "kernels (graph-captured; default), IPC copies into the peers' receive slots "
                          "(a copy+signal kernel and a wait kernel, graph-captured) or RCCL grouped send/recv "
                          "(eager)")
+    ap.add_argument("--march3", default="auto", choices=["auto", "on", "off"],
+                    help="native runtime, one rank, streaming-stage grids: the pipelined SSP-RK3 march (one "
+                         "launch per step for the tile interiors + two band launches, ops/march3.py) instead of "
+                         "three streaming-stage launches; auto: where it applies")
+    ap.add_argument("--march3-rows", type=int, default=0, help="pipelined march: stage-3 rows per wave (0 = auto)")
     ap.add_argument("--partition", default="auto")
     ap.add_argument("--dt", type=float, default=None)
     ap.add_argument("--block", default=None, help="stage block shape BXxBY, or the fused runtime's square block size B (default: chosen per grid)")
@@ -358,8 +363,17 @@ def main():
                 ipc = xg = IpcExchange(eng, IpcExchange.slots_for(eng), timeout_s=xg_timeout)   # collective
             elif comm == "rccl":
                 nc = create_nccl_comm(rank, world, local)
+            m3 = None
+            if world == 1 and a.march3 != "off":
+                from stsphere.ops.march3 import March3Step, march3_unsupported, march3_wanted
+                if a.march3 == "on" or march3_wanted(eng):
+                    why = march3_unsupported(eng)
+                    if why:
+                        raise SystemExit(f"[bench] --march3 on: {why}")
+                    m3 = March3Step(eng, rows=a.march3_rows or 32)
+                    info["march3_rows"] = m3.rows
             runner = NativeStepper(eng, nccl_comm=nc, use_graph=True, steps_per_graph=spg,
-                                   xgmi=xg if comm == "xgmi" else None, ipc=ipc)
+                                   xgmi=xg if comm == "xgmi" else None, ipc=ipc, march3=m3)
         elif runtime == "graph":
             runner = GraphStepper(eng, spg)
         return eng, runner, xg
@@ -530,6 +544,7 @@ def main():
                 "block": list((eng.compute.bx, eng.compute.by)) if hasattr(eng.compute, "bx") else None,
                 "steps_per_launch": info["steps_per_launch"],
                 "fused_block": info.get("fused_B"),
+                "march3_rows": info.get("march3_rows"),
                 "graph_replayed_steps": timed.get("graph_steps"),
                 "direct_launch_steps": timed.get("direct_steps"),
                 "kernel_launches": timed.get("launches") if timed.get("direct_steps") else None,

@@ -86,6 +86,7 @@ def main(argv=None):
     s.initialize()
     summary = s.run(nsteps=a.nsteps, days=a.days)
     g = s.gather_global() if a.plot else None     # collective under SPMD
+    s.close()                                     # collective under SPMD (exchange rings)
     if s.rank == 0:
         print(json.dumps(summary, default=float))
         if a.plot:

@@ -132,6 +132,7 @@ class Solver:
         self.runner = None            # NativeStepper (GPU) once stepping starts
         self.fused = None             # ops/fused.py::FusedKernel when the runner steps with it
         self.xgmi = None
+        self._ipc = None
         self._nccl = None
         self.comm = "local"
         self.mode = None
@@ -429,6 +430,17 @@ class Solver:
                       f"{spl} step(s) per launch, " + ("direct launches" if self.mode == "single" else "graph replay"))
             return NativeStepper(e, use_graph=True, steps_per_graph=c.steps_per_graph, fused=fk,
                                  steps_per_launch=spl, direct=self.mode == "single")
+        if self.mode == "single" and c.march3 != "off":
+            from .ops.march3 import March3Step, march3_unsupported, march3_wanted
+            why = march3_unsupported(e)
+            if c.march3 == "on" and why:
+                raise ValueError(f"runtime.march3 = on: {why}")
+            if c.march3 == "on" or march3_wanted(e):
+                m3 = March3Step(e, rows=c.march3_rows)
+                self._log(f"Runtime: pipelined SSP-RK3 march ({m3.ncs} strips x {m3.nrs} segments per tile, "
+                          f"{m3.band.numel()} band blocks), graph replay")
+                self.xgmi = self._ipc = None
+                return NativeStepper(e, use_graph=c.graph, steps_per_graph=c.steps_per_graph, march3=m3)
         xg = nc = ipc = None
         if self.mode == "spmd" and self.comm == "xgmi":
             from .ops.xgmi import XgmiHalo
@@ -444,6 +456,21 @@ class Solver:
         self._ipc = ipc
         return NativeStepper(e, nccl_comm=nc, use_graph=c.graph, steps_per_graph=c.steps_per_graph, xgmi=xg,
                              ipc=ipc)
+
+    def close(self) -> None:
+        """Release the step runner and the exchange rings explicitly.  With
+        several ranks this is collective (every rank calls it, as the run
+        script does at the end): the rings' close joins a group barrier, which
+        a garbage-collection finalizer must not do."""
+        if self.runner is not None:
+            self.runner.close()
+            self.runner = None
+        seen = set()
+        for obj in (self.xgmi, self.fused, getattr(self, "_ipc", None)):
+            if obj is not None and id(obj) not in seen and hasattr(obj, "close"):
+                seen.add(id(obj))
+                obj.close()
+        self.xgmi = self.fused = self._ipc = None
 
     def step(self, nsteps: int = 1) -> None:
         if nsteps <= 0:

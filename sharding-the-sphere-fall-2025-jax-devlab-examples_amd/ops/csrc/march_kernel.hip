@@ -34,31 +34,11 @@
 // tag), and a cell that is another rank's ghost is stored into that rank's
 // ring (push-map entries <= -2); each wave (job) keeps its own stage count.
 // Compared with the fp64 PyTorch oracle in tests/test_march.py.
-#include "stage_common.h"
+#include "march_common.h"
 
 namespace {
 
-constexpr int MW = 64;          // lanes per wave
 constexpr int MO = MW - 4;      // output columns per wave
-constexpr int MWPB = 4;         // independent waves (jobs) per workgroup
-
-// Wave-wide lane shifts.  wave_shr:1: lane i <- lane i-1; wave_shl:1: lane i
-// <- lane i+1 (lanes without a source read 0).  DPP moves are 32-bit, so a
-// double is two moves.
-constexpr int DPP_SHR = 0x138, DPP_SHL = 0x130;
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
-}
-template <int CTRL>
-__device__ __forceinline__ double dpp(double v) {
-  int2 p = __builtin_bit_cast(int2, v);
-  p.x = __builtin_amdgcn_update_dpp(0, p.x, CTRL, 0xf, 0xf, false);
-  p.y = __builtin_amdgcn_update_dpp(0, p.y, CTRL, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, p);
-}
-template <typename T> __device__ __forceinline__ T shr(T v) { return dpp<DPP_SHR>(v); }
-template <typename T> __device__ __forceinline__ T shl(T v) { return dpp<DPP_SHL>(v); }
 
 // panel-local components (e_i, e_j, n) -> Cartesian for a panel whose frame
 // vectors are signed coordinate axes (frame code of ops/fused.py::frame_code)

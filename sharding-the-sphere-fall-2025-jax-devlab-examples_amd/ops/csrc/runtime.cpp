@@ -104,7 +104,7 @@ extern "C" int stsp_device_flags(void) {
 // sizes of the C ABI descriptors, checked against the ctypes mirrors (ops/native.py)
 extern "C" int stsp_desc_size(int which) {
   return which == 0 ? (int)sizeof(StageDesc) : which == 1 ? (int)sizeof(FusedDesc)
-       : which == 2 ? (int)sizeof(StspOp) : -1;
+       : which == 2 ? (int)sizeof(StspOp) : which == 3 ? (int)sizeof(March3Desc) : -1;
 }
 
 extern "C" int stsp_rccl_version(void) {
@@ -278,6 +278,15 @@ int run_op(Runtime* rt, const StspOp& op) {
       const int rc = stsp_fused_launch(op.dtype, static_cast<const FusedDesc*>(op.fused), rt->stream);
       if (rc != 0) {
         rt->err = "fused step launch failed: " + std::to_string(rc);
+        return -3;
+      }
+      return 0;
+    }
+    case STSP_OP_MARCH3: {
+      const int rc = stsp_march3_launch(op.dtype, op.by, &op.stage, static_cast<const March3Desc*>(op.fused),
+                                        rt->stream);
+      if (rc != 0) {
+        rt->err = "pipelined march launch failed: " + std::to_string(rc);
         return -3;
       }
       return 0;
@@ -458,7 +467,7 @@ extern "C" const char* stsp_rt_last_error(void* p) {
 extern "C" int stsp_rt_set_dt(void* p, double dt) {
   auto* rt = static_cast<Runtime*>(p);
   for (StspOp& op : rt->ops) {
-    if (op.type == STSP_OP_STAGE) op.stage.dt = dt;
+    if (op.type == STSP_OP_STAGE || op.type == STSP_OP_MARCH3) op.stage.dt = dt;
     if (op.type == STSP_OP_FUSED && op.fused) static_cast<FusedDesc*>(op.fused)->dt = dt;
   }
   drop_graph(rt);

@@ -7,7 +7,8 @@
 extern "C" {
 
 enum StspOpType { STSP_OP_STAGE = 1, STSP_OP_PACK = 2, STSP_OP_COMM_START = 3, STSP_OP_COMM_WAIT = 4,
-                  STSP_OP_FUSED = 5, STSP_OP_IPC_SEND = 6, STSP_OP_IPC_WAIT = 7 };
+                  STSP_OP_FUSED = 5, STSP_OP_IPC_SEND = 6, STSP_OP_IPC_WAIT = 7,
+                  STSP_OP_MARCH3 = 8 };
 
 #define STSP_MAX_PEERS 32
 
@@ -31,7 +32,10 @@ typedef struct StspOp {
   void* recvbuf;
   int slot_elems;  // elements per slot (= F)
   // FUSED: one whole SSP-RK step (fused_step.hip); the descriptor is owned by
-  // the caller and must outlive the runtime (dt is rewritten by stsp_rt_set_dt)
+  // the caller and must outlive the runtime (dt is rewritten by stsp_rt_set_dt).
+  // MARCH3: the pipelined streaming step (march3_kernel.hip) with `stage`
+  // (step input Q, output out, dt) and `fused` pointing at its March3Desc;
+  // `by` = rows per segment.
   void* fused;
   // IPC copy transport (ops/native_runtime.py::IpcExchange; graph-capturable,
   // no RCCL).  IPC_SEND, in order on the compute stream (on the comm stream

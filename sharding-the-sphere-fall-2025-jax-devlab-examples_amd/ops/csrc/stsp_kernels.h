@@ -78,6 +78,21 @@ typedef struct StageDesc {
 } StageDesc;
 
 int stsp_stage_launch(int phys, int dtype, int bx, int by, const StageDesc* d, hipStream_t stream);
+// Pipelined streaming SSP-RK3 step (march3_kernel.hip): one launch marches all
+// three stages up each strip of a tile (stage s + 1 trails stage s by two rows),
+// reading the step input d->Q once and writing the step output d->out at the
+// cells at least 4 from a tile edge.  Stage s computes out = b0[s] X + b1[s] Q
+// + b2[s] dt L(Q) with X = the step input.  The cells within D of a tile edge of
+// the stage-1 and stage-2 results go to q1 / q2 (stage 1 also pushes its
+// same-rank ghost copies into q1), so that two band launches of the stage kernel
+// finish stages 2 and 3 next to the tile edges (ops/march3.py).
+typedef struct March3Desc {
+  void* q1;
+  void* q2;
+  double b0[3], b1[3], b2[3];
+  int D;
+} March3Desc;
+int stsp_march3_launch(int dtype, int rows, const StageDesc* d, const March3Desc* m, hipStream_t stream);
 int stsp_pack_launch(int dtype, const void* q, int S, int F, const int* idx, int ns, void* send, hipStream_t stream);
 int stsp_copy_index_launch(int dtype, const void* src, const int* sidx, void* dst, const int* didx, int k,
                            int batch, long src_stride, long dst_stride, hipStream_t stream);

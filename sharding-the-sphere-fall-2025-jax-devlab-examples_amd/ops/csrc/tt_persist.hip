@@ -48,7 +48,7 @@ struct TPArgs {
   int lda, ldb, N, r0, ncalls, nsub, periodic, max_rank;
   double c, ih2, eps;
   double* xch;              // [0, 256): R of B; [256, 512): B's core map (k x rn)
-  unsigned* flags;          // [0] R_B ready = step + 1, [1] core ready = step + 1, [2] rn, [3] error
+  unsigned* flags;          // [0] R_B ready = step + 1, [1] core ready (step + 1) << 8 | rn, [3] error
   double* outA;
   double* outB;
   int ldo;
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
   __shared__ double sW[TP_KP][TP_KP + 1];         // core: right singular vectors
   __shared__ double sig[TP_KP];
   __shared__ int s_ord[TP_KP];
-  __shared__ int s_i[4];                          // pivot flag, rotation flag, rank
+  __shared__ int s_i[5];                          // pivot flag, rotation flag, rank, wait failed, core rank
   __shared__ double s_d[2];
   const int side = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int N = a.N;
@@ -311,10 +311,17 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
       __syncthreads();
       if (tid == 0) __hip_atomic_store((tp_gu32*)a.flags, (unsigned)call + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       TP_STAMP(5);
-      if (tid == 0) s_i[3] = tp_wait(a.flags + 1, (unsigned)call + 1u, a.flags + 3, a.timeout_ticks) ? 0 : 1;
+      // flags[1] = (step + 1) << 8 | rn: one single-copy-atomic word, so the rank
+      // can never be read from an older step than the ready count
+      if (tid == 0) {
+        const bool ok = tp_wait(a.flags + 1, ((unsigned)call + 1u) << 8, a.flags + 3, a.timeout_ticks);
+        s_i[3] = ok ? 0 : 1;
+        s_i[4] = ok ? (int)(__hip_atomic_load((tp_gu32*)(a.flags + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+                            255u) : 0;
+      }
       __syncthreads();
       if (s_i[3]) break;
-      rn = (int)__hip_atomic_load((tp_gu32*)(a.flags + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      rn = s_i[4];
       if (rn <= 0 || rn > k) break;
       if (tid < k * rn) sC[tid / rn][tid - (tid / rn) * rn] = ld_wt(a.xch + 256 + tid);
       __syncthreads();
@@ -434,8 +441,8 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        __hip_atomic_store((tp_gu32*)(a.flags + 2), (unsigned)rn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((tp_gu32*)(a.flags + 1), (unsigned)call + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((tp_gu32*)(a.flags + 1), (((unsigned)call + 1u) << 8) | ((unsigned)rn & 255u),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (rn <= 0) break;
       if (tid < k * rn) sC[tid / rn][tid - (tid / rn) * rn] = Tm[tid / rn][tid - (tid / rn) * rn];

@@ -71,6 +71,15 @@ class FusedDesc(ctypes.Structure):
     ]
 
 
+class March3Desc(ctypes.Structure):
+    """Mirror of March3Desc (stsp_kernels.h): the pipelined streaming step."""
+    _fields_ = [
+        ("q1", ctypes.c_void_p), ("q2", ctypes.c_void_p),
+        ("b0", ctypes.c_double * 3), ("b1", ctypes.c_double * 3), ("b2", ctypes.c_double * 3),
+        ("D", ctypes.c_int),
+    ]
+
+
 def lib_path() -> str:
     return _build.lib_for(os.environ.get("STSP_VARIANT", ""))
 
@@ -101,6 +110,8 @@ def load(build_if_missing: bool = True):
         L.stsp_dpp_probe.restype = ci
         L.stsp_fused_launch.argtypes = [ci, ctypes.POINTER(FusedDesc), vp]
         L.stsp_fused_launch.restype = ci
+        L.stsp_march3_launch.argtypes = [ci, ci, ctypes.POINTER(StageDesc), ctypes.POINTER(March3Desc), vp]
+        L.stsp_march3_launch.restype = ci
         L.stsp_fused_limits.argtypes = [ctypes.POINTER(ci), ctypes.POINTER(ci)]
         L.stsp_fused_limits.restype = ci
         _declare_runtime(L)
@@ -111,7 +122,7 @@ def load(build_if_missing: bool = True):
         L.stsp_device_flags.restype = ci
         L.stsp_desc_size.argtypes = [ci]
         L.stsp_desc_size.restype = ci
-        for k, cls in enumerate((StageDesc, FusedDesc)):
+        for k, cls in ((0, StageDesc), (1, FusedDesc), (3, March3Desc)):
             if L.stsp_desc_size(k) != ctypes.sizeof(cls):
                 raise RuntimeError(f"{cls.__name__}: ctypes mirror is {ctypes.sizeof(cls)} bytes, "
                                    f"the library's {L.stsp_desc_size(k)} (stale libstsp.so?)")

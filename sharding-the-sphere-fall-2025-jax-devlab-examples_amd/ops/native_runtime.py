@@ -21,7 +21,7 @@ from . import native
 from .native import StageDesc
 
 MAX_PEERS = 32
-OP_STAGE, OP_PACK, OP_COMM_START, OP_COMM_WAIT, OP_FUSED, OP_IPC_SEND, OP_IPC_WAIT = 1, 2, 3, 4, 5, 6, 7
+OP_STAGE, OP_PACK, OP_COMM_START, OP_COMM_WAIT, OP_FUSED, OP_IPC_SEND, OP_IPC_WAIT, OP_MARCH3 = 1, 2, 3, 4, 5, 6, 7, 8
 
 _I32x = ctypes.c_int * MAX_PEERS
 
@@ -141,10 +141,9 @@ class IpcExchange:
     torch loads, crashed under capture: round 3).
 
     Memory (two allocations per rank, ``xgmi.IpcRing``; peers map both):
-    ``nslots`` receive slots of [max num_recv, F] values in ordinary device
-    memory (read only by the boundary blocks, a kernel launched after the
-    wait), and one flag word per receive peer in an uncached ring (polled
-    inside the wait kernel).  Op j of the step's op list fills / reads slot j, so a
+    ``nslots`` receive slots of [max num_recv, F] values (read only by the
+    boundary blocks, a kernel launched after the wait), and one flag word per
+    receive peer (polled inside the wait kernel), both in uncached rings.  Op j of the step's op list fills / reads slot j, so a
     slot is reused ``nslots`` exchanges later: a peer can be at most one
     exchange ahead (its exchange j + 1 starts after its stage j, which waited
     for our exchange j, and our exchange j + 1 is issued after our stage j has
@@ -172,11 +171,16 @@ class IpcExchange:
         peers = sorted(set(int(q) for q in plan.send_peers) | set(int(q) for q in plan.recv_peers) | {rank})
         if len(plan.send_peers) > MAX_PEERS or len(plan.recv_peers) > 64:
             raise RuntimeError("too many peers for the IPC exchange")
-        # payload slots in ordinary device memory (written by the peers' copies,
-        # read by the boundary blocks, a later kernel than the wait); the flag
-        # words, polled inside the wait kernel, in an uncached ring.  An uncached
-        # payload ran 383 us per C96 step on a shared GPU (the copies into it)
-        self.mem = IpcRing(L, e.device, world, rank, peers, nslots * self.slot_bytes, group, cached=True)
+        # payload slots and flag words in uncached rings.  A peer on ANOTHER GPU
+        # stores into our slot over xGMI, which does not invalidate the lines
+        # our L2 kept from reading the same slot nslots exchanges earlier, and
+        # the wait kernel's relaxed polls are no acquire: a cached slot could be
+        # read stale.  Uncached memory is never held in L2.  Cached
+        # slots (STSP_IPC_CACHED=1) were validated only with the ranks sharing
+        # one GPU (one L2 hierarchy).
+        import os
+        cached = os.environ.get("STSP_IPC_CACHED") == "1"
+        self.mem = IpcRing(L, e.device, world, rank, peers, nslots * self.slot_bytes, group, cached=cached)
         self.fmem = IpcRing(L, e.device, world, rank, peers, flag_bytes, group)
         self.counters = torch.zeros(4 + MAX_PEERS, dtype=torch.int32, device=e.device)   # runtime.cpp ipc kernels
         self.err = torch.zeros(4, dtype=torch.int32, device=e.device)
@@ -221,7 +225,7 @@ class NativeStepper:
 
     def __init__(self, engine, nccl_comm: Optional[int] = None, use_graph: bool = True,
                  steps_per_graph: int = 30, roctx: bool = False, stream: Optional[torch.cuda.Stream] = None,
-                 xgmi=None, fused=None, steps_per_launch: int = 1, direct: bool = False, ipc=None):
+                 xgmi=None, fused=None, steps_per_launch: int = 1, direct: bool = False, ipc=None, march3=None):
         from .hip_compute import HipCompute
         e = engine
         if not isinstance(e.compute, HipCompute):
@@ -239,6 +243,11 @@ class NativeStepper:
             self.remote = False      # remote window cells arrive inside the fused kernel
         if xgmi is not None:
             self.remote = False      # the exchange lives inside the stage kernels
+        # march3: ops/march3.py::March3Step, the pipelined streaming step of one
+        # rank (one march launch + two band launches per step, period 2)
+        self.march3 = march3
+        if march3 is not None and (fused is not None or xgmi is not None or ipc is not None or self.remote):
+            raise RuntimeError("the pipelined march step runs one rank without another step kernel")
         self.ipc = ipc
         if self.remote and not nccl_comm and ipc is None:
             raise RuntimeError("rank has remote neighbours: pass an RCCL communicator (create_nccl_comm) "
@@ -260,6 +269,8 @@ class NativeStepper:
                 raise ValueError("steps_per_launch must be even")
             self.spl = steps_per_launch
         period = (self.spl if self.spl > 1 else 2) if fused is not None else e.integ.period
+        if march3 is not None:
+            period = 2
         self.period = period
         ops: List[StspOp] = []
         pool = list(e.pool)
@@ -272,7 +283,9 @@ class NativeStepper:
             op.dtype = fused.dcode
             op.fused = ctypes.addressof(fd)
             ops.append(op)
-        for _ in range(period if fused is None else 0):
+        if march3 is not None:
+            ops.extend(march3.ops())
+        for _ in range(period if (fused is None and march3 is None) else 0):
             e.pool = pool
             for st in e.integ.stages:
                 if xgmi is not None:

@@ -347,14 +347,19 @@ class XgmiHalo:
         if int(self.err[0].item()) != 0:
             raise RuntimeError("direct xGMI halo: a peer's ghosts did not arrive in time (poll timeout)")
 
-    def close(self) -> None:
+    def close(self, collective: bool = True) -> None:
+        """Explicit close: collective (every rank together, see IpcRing.close).
+        The garbage-collection path passes ``collective=False``."""
         if getattr(self, "mem", None) is not None:
-            self.mem.close()
+            self.mem.close(collective=collective)
         self.base = None
 
     def __del__(self):
+        # a finalizer runs at a different point on every rank (reference
+        # cycles, an exception unwinding on one rank): it must not join a
+        # collective that could pair with an unrelated one (ADVICE r5)
         try:
-            self.close()
+            self.close(collective=False)
         except Exception:
             pass
 
@@ -440,14 +445,18 @@ class IpcRing:
             self.close()
             raise err if err is not None else RuntimeError("xGMI setup failed on another rank")
 
-    def close(self) -> None:
+    def close(self, collective: bool = True) -> None:
         """Collective when distributed (every rank closes its ring together,
-        as every call site does).  Order: this rank's kernels are done (no more
-        stores into peers' rings), its peer mappings are closed, then a group
-        barrier, and only then does the ring go back to the process's pool,
-        where the next ``stsp_xg_alloc`` zeroes and reuses it: without the
+        as every explicit call site does).  Order: this rank's kernels are done
+        (no more stores into peers' rings), its peer mappings are closed, then a
+        group barrier, and only then does the ring go back to the process's
+        pool, where the next ``stsp_xg_alloc`` zeroes and reuses it: without the
         barrier a peer still inside its last launch could store tagged granules
-        into a ring this rank had already handed to a new exchange."""
+        into a ring this rank had already handed to a new exchange.
+
+        ``collective=False`` (finalizers): no barrier, and the
+        allocation is NOT handed back (neither to the pool nor to the driver),
+        since a peer may still store into it; it stays with the process."""
         import torch.distributed as dist
         if getattr(self, "_closed", False):
             return
@@ -458,6 +467,9 @@ class IpcRing:
         for p in self.opened:
             L.stsp_ipc_close(ctypes.c_void_p(p))
         self.opened = []
+        if not collective and self.distributed:
+            self.base = None                     # leaked on purpose: a peer may still store into it
+            return
         if self.distributed and dist.is_initialized():
             dist.barrier(group=self.group)       # every rank, with or without a ring
         if self.base:

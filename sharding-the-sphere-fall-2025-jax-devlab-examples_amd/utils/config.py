@@ -92,6 +92,11 @@ class RuntimeConfig:
     # the shallow-water setup supports it and every block of a rank is resident
     fused: str = "auto"                # auto | on | off
     steps_per_launch: int = 0          # fused multi-step launches; 0 = from the run's chunk length
+    # pipelined streaming step (ops/march3.py: one march launch per step for the
+    # tile interiors + two band launches) on one GPU where the streaming stage
+    # applies (large grids): auto | on | off
+    march3: str = "auto"
+    march3_rows: int = 32
 
 
 @dataclass

@@ -43,7 +43,7 @@ def test_fused_torch_matches_stage_oracle(N, t, B, case, lim):
     assert fe.step_count == 2
 
 
-@pytest.mark.parametrize("B", [8, 12, 16, 18, 20])
+@pytest.mark.parametrize("B", [6, 8, 12, 16, 18, 20])
 def test_pass_schedule_covers_every_pass_once(B):
     """Every face pass of every stage runs on exactly one wave (the kernel's
     per-wave masks), the corner wave and the ghost waves exist in the thread
@@ -85,13 +85,13 @@ def test_pass_schedule_covers_every_pass_once(B):
             assert group_load(new, b, s_) <= group_load(old, b, s_)
 
 
-def test_near_pass_masks_flag_every_near_face():
+@pytest.mark.parametrize("N,B", [(48, 16), (48, 6), (36, 6)])
+def test_near_pass_masks_flag_every_near_face(N, B):
     """A face pass the host does not flag must hold no face within one line
     of a panel-edge line (those faces read neighbour codes and ghost entries;
     an unflagged one would read the raw window), and interior blocks flag
-    nothing."""
+    nothing.  B = 6: the small rank-share blocks."""
     from stsphere.ops.fused import near_pass_masks, stage_face_coords
-    N, B = 48, 16
     L = TileLayout(N, 1, 1, ng=2)
     P = FusedPlan(L, 0, CubedSphereGrid(N), B=B, ns=3)
     flags = np.array([sum(1 << int(r) for r in np.unique(P.reg[b]) if r >= 0) for b in range(P.nb)])
