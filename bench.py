@@ -76,7 +76,8 @@ def parse(argv=None):
     ap.add_argument("--march3", default="auto", choices=["auto", "on", "off"],
                     help="native runtime, one rank, streaming-stage grids: the pipelined SSP-RK3 march (one "
                          "launch per step for the tile interiors + two band launches, ops/march3.py) instead of "
-                         "three streaming-stage launches; auto: where it applies")
+                         "three streaming-stage launches; auto: the measured-faster choice (currently the three "
+                         "launches, profiles/r6_march3)")
     ap.add_argument("--march3-rows", type=int, default=0, help="pipelined march: stage-3 rows per wave (0 = auto)")
     ap.add_argument("--partition", default="auto")
     ap.add_argument("--dt", type=float, default=None)
@@ -151,7 +152,7 @@ def launch_ranks(a) -> int:
            *sys.argv[1:]]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    if share and a.comm != "ipc":
+    if share and a.comm != "ipc" and os.environ.get("STSP_FAIL_XGMI") != "1":
         # several ranks on ONE GPU: one hardware queue per process.  With the
         # default four, three or more processes oversubscribe the queues the
         # scheduler maps at once, it time-slices them, and a multi-step fused
@@ -420,57 +421,67 @@ def main():
         dist.broadcast(d, src=0)
         return float(d.item())
 
+    # transport fallback chain between GPUs: the direct xGMI rings, then the
+    # graph-captured IPC copy transport, then eager RCCL; each attempt is
+    # agreed by every rank (setup, warmup exchange check, bitwise check
+    # against one GPU) and a failed one restarts from a fresh state
+    FALLBACK = {"xgmi": "ipc", "ipc": "rccl"}
+    chain = [comm]
+    while world > 1 and chain[-1] in FALLBACK:
+        chain.append(FALLBACK[chain[-1]])
     eng = runner = xg = None
     fallback_reason = None
-    _phase("build")
-    try:
-        eng, runner, xg = build(comm)
-        ok = True
-    except Exception as exc:   # e.g. no IPC between these GPUs
-        print(f"[bench] rank {rank}: {comm} setup failed: {exc}", file=sys.stderr, flush=True)
-        fallback_reason = f"rank {rank}: {comm} setup failed: {exc}"
-        ok = False
-    if comm == "xgmi" and not agree(ok):
-        close(runner, xg)
-        fallback_reason = fallback_reason or "xgmi setup failed on another rank"
-        comm = "rccl"
-        runtime = "native" if runtime == "fused" else runtime
-        _phase("build_rccl")
-        eng, runner, xg = build(comm)
-    elif not ok:
-        raise SystemExit(1)
-    _phase("warmup")
-    if os.environ.get("STSP_BENCH_HANG_RANK") == str(rank):   # test hook: a rank that never returns
-        while True:
-            time.sleep(1)
-    ok = warm(eng, runner)
-    if not ok:
-        fallback_reason = f"rank {rank}: {comm} exchange timed out in warmup"
     warm_diff = None
     verify = world > 1 and not a.no_verify
-    if verify and ok:
-        _phase("verify")
-        warm_diff = diff_vs_1gpu(eng, a.warmup)
-        ok = warm_diff == 0.0
-        if not ok:
-            fallback_reason = f"{comm}: warmup state differs from one GPU by {warm_diff:.3e}"
-        if not ok and rank == 0:
-            print(f"[bench] {comm}: warmup state differs from one GPU by {warm_diff:.3e}", file=sys.stderr, flush=True)
-    if world > 1 and not agree(ok):
-        if comm != "xgmi":
-            raise SystemExit(f"[bench] rank {rank}: {comm} exchange failed its check")
+
+    def attempt(c):
+        """(engine, runner, exchange, ok, why) of one transport."""
+        e_ = r_ = x_ = None
+        why = None
+        _phase(f"build_{c}")
+        try:
+            e_, r_, x_ = build(c)
+            ok_ = True
+        except Exception as exc:   # e.g. no IPC between these GPUs
+            print(f"[bench] rank {rank}: {c} setup failed: {exc}", file=sys.stderr, flush=True)
+            why = f"rank {rank}: {c} setup failed: {exc}"
+            ok_ = False
+        if world > 1 and not agree(ok_):
+            return e_, r_, x_, False, why or f"{c} setup failed on another rank", None
+        if not ok_:
+            raise SystemExit(1)
+        _phase(f"warmup_{c}")
+        if os.environ.get("STSP_BENCH_HANG_RANK") == str(rank):   # test hook: a rank that never returns
+            while True:
+                time.sleep(1)
+        ok_ = warm(e_, r_)
+        if not ok_:
+            why = f"rank {rank}: {c} exchange timed out in warmup"
+        d_ = None
+        if verify and ok_:
+            _phase(f"verify_{c}")
+            d_ = diff_vs_1gpu(e_, a.warmup)
+            ok_ = d_ == 0.0
+            if not ok_:
+                why = f"{c}: warmup state differs from one GPU by {d_:.3e}"
+                if rank == 0:
+                    print(f"[bench] {why}", file=sys.stderr, flush=True)
+        if world > 1 and not agree(ok_):
+            return e_, r_, x_, False, why or f"{c} check failed on another rank", d_
+        return e_, r_, x_, True, None, d_
+
+    for k, c in enumerate(chain):
+        if k:
+            runtime = "native" if runtime == "fused" else runtime   # the fallbacks are stage-kernel op lists
+        eng, runner, xg, ok, why, warm_diff = attempt(c)
+        if ok:
+            comm = c
+            break
+        fallback_reason = why if fallback_reason is None else f"{fallback_reason}; {why}"
         close(runner, xg)
-        fallback_reason = fallback_reason or f"{comm} check failed on another rank"
-        comm = "rccl"                    # fall back from a fresh state
-        runtime = "native" if runtime == "fused" else runtime
-        _phase("build_rccl")
-        eng, runner, xg = build(comm)
-        if not warm(eng, runner):
-            raise SystemExit(f"[bench] rank {rank}: rccl exchange failed")
-        if verify:
-            warm_diff = diff_vs_1gpu(eng, a.warmup)
-            if warm_diff != 0.0:
-                raise SystemExit(f"[bench] rank {rank}: rccl state differs from one GPU by {warm_diff:.3e}")
+        if k == len(chain) - 1:
+            raise SystemExit(f"[bench] rank {rank}: every transport failed ({fallback_reason})")
+    _phase("timed_prep")
     step = runner.run if runner is not None else eng.step
     stats0 = dict(getattr(runner, "stats", {}))
     _phase("timed")

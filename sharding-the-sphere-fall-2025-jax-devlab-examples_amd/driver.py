@@ -423,13 +423,23 @@ class Solver:
         if use_fused:
             from .ops.fused import FusedKernel, fused_block, rank_cus
             cus = rank_cus(e.device)
-            fk = FusedKernel(e, B=fused_block(e.plan.n, len(e.plan.tiles), cus))   # collective with several ranks
-            self.fused = fk
-            self.xgmi = fk if self.mode == "spmd" else None
-            self._log(f"Runtime: fused SSP-RK3 step, {fk.plan.nb} blocks of {fk.plan.B}x{fk.plan.B}, "
-                      f"{spl} step(s) per launch, " + ("direct launches" if self.mode == "single" else "graph replay"))
-            return NativeStepper(e, use_graph=True, steps_per_graph=c.steps_per_graph, fused=fk,
-                                 steps_per_launch=spl, direct=self.mode == "single")
+            try:
+                fk = FusedKernel(e, B=fused_block(e.plan.n, len(e.plan.tiles), cus))   # collective with several ranks
+            except RuntimeError as exc:
+                if self.mode != "spmd":
+                    raise
+                # the ring setup raised on every rank alike: the stage-kernel op
+                # list with the next transport of the chain
+                self._log(f"Runtime: fused xGMI step unavailable ({exc}); falling back")
+                self.comm = "ipc"
+                fk = None
+            if fk is not None:
+                self.fused = fk
+                self.xgmi = fk if self.mode == "spmd" else None
+                self._log(f"Runtime: fused SSP-RK3 step, {fk.plan.nb} blocks of {fk.plan.B}x{fk.plan.B}, "
+                          f"{spl} step(s) per launch, " + ("direct launches" if self.mode == "single" else "graph replay"))
+                return NativeStepper(e, use_graph=True, steps_per_graph=c.steps_per_graph, fused=fk,
+                                     steps_per_launch=spl, direct=self.mode == "single")
         if self.mode == "single" and c.march3 != "off":
             from .ops.march3 import March3Step, march3_unsupported, march3_wanted
             why = march3_unsupported(e)
@@ -442,16 +452,31 @@ class Solver:
                 self.xgmi = self._ipc = None
                 return NativeStepper(e, use_graph=c.graph, steps_per_graph=c.steps_per_graph, march3=m3)
         xg = nc = ipc = None
-        if self.mode == "spmd" and self.comm == "xgmi":
-            from .ops.xgmi import XgmiHalo
-            xg = XgmiHalo(e)
-        elif self.mode == "spmd" and self.comm == "rccl":
-            if self._nccl is None:
-                self._nccl = create_nccl_comm(self.rank, self.world, self.device.index or 0)
-            nc = self._nccl
-        elif self.mode == "spmd" and self.comm == "ipc":
-            from .ops.native_runtime import IpcExchange
-            ipc = IpcExchange(e, IpcExchange.slots_for(e))        # collective (IPC handles)
+        if self.mode == "spmd":
+            # transport chain between GPUs: direct xGMI rings -> IPC copy kernel
+            # (graph-captured) -> RCCL (eager).  A setup that fails raises on
+            # every rank alike (IpcRing agrees on every step), so all ranks
+            # move down the chain together.
+            order = ["xgmi", "ipc", "rccl"]
+            chain = order[order.index(self.comm):] if self.comm in order else [self.comm]
+            for k, cm in enumerate(chain):
+                try:
+                    if cm == "xgmi":
+                        from .ops.xgmi import XgmiHalo
+                        xg = XgmiHalo(e)
+                    elif cm == "ipc":
+                        from .ops.native_runtime import IpcExchange
+                        ipc = IpcExchange(e, IpcExchange.slots_for(e))        # collective (IPC handles)
+                    elif cm == "rccl":
+                        if self._nccl is None:
+                            self._nccl = create_nccl_comm(self.rank, self.world, self.device.index or 0)
+                        nc = self._nccl
+                    self.comm = cm
+                    break
+                except RuntimeError as exc:
+                    if k == len(chain) - 1:
+                        raise
+                    self._log(f"Runtime: {cm} exchange unavailable ({exc}); falling back to {chain[k + 1]}")
         self.xgmi = xg
         self._ipc = ipc
         return NativeStepper(e, nccl_comm=nc, use_graph=c.graph, steps_per_graph=c.steps_per_graph, xgmi=xg,

@@ -44,9 +44,8 @@
 #include <type_traits>
 
 
-// Timing-only probe builds (ops/build.py variants fp_alledge / fp_nogwait):
-// every block runs the panel-edge face body (numerics unchanged), or near
-// faces skip the wait for the ghost pass (numerics wrong: timing only)
+// Timing-only probe build (ops/build.py variant fp_alledge): every block runs
+// the panel-edge face body (numerics unchanged; profiles/r5_fused)
 #ifndef STSP_FPROBE_ALLEDGE
 #define STSP_FPROBE_ALLEDGE 0
 #endif
@@ -55,9 +54,6 @@
 // of the IPC-mapped rings from a protocol one (multi-rank shared-GPU runs)
 #ifndef STSP_XG_FENCE
 #define STSP_XG_FENCE 0
-#endif
-#ifndef STSP_FPROBE_NOGWAIT
-#define STSP_FPROBE_NOGWAIT 0
 #endif
 
 namespace {
@@ -652,7 +648,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         near = (unsigned)(k - e0 + 1) <= 2u || (unsigned)(k - e1 + 1) <= 2u;
         wnear = __builtin_amdgcn_ballot_w64(near) != 0;
       }
-      if (wnear && !STSP_FPROBE_NOGWAIT) gwait();          // this wave reads ghost entries
+      if (wnear) gwait();          // this wave reads ghost entries
       if (near) {
         const int sm = ax ? 2 : 0;                         // side index of -axis; +axis = sm + 1
         const int ci = fv * CS + fu, cj = ci - (ax ? CS : 1);  // code indices of b and a

@@ -58,9 +58,16 @@ template <typename T>
 struct P3 {
   T* q1;
   T* q2;
-  T b0[3], b1[3], b2[3];
   int D, ncs, nrs, njobs;
 };
+
+// SSP-RK3 (models/integrators.py::ssp_rk3): stage s computes
+// b0 X + b1 Q + b2 dt L(Q).  Compile-time constants, the same values the stage
+// kernel receives as (T) of the host doubles (the host checks the integrator).
+template <typename T, int S> struct RK3;
+template <typename T> struct RK3<T, 1> { static constexpr T b0 = T(0.0), b1 = T(1.0), b2 = T(1.0); };
+template <typename T> struct RK3<T, 2> { static constexpr T b0 = T(0.75), b1 = T(0.25), b2 = T(0.25); };
+template <typename T> struct RK3<T, 3> { static constexpr T b0 = T(1.0 / 3.0), b1 = T(2.0 / 3.0), b2 = T(2.0 / 3.0); };
 
 // rolling rows of one interior march stage: primitives (h, v, sqrt(g h)) of
 // rows j and j + 1, the half slope of row j, the flux through the face below j
@@ -103,11 +110,12 @@ __device__ __forceinline__ void xfaces(const T (&c)[5], const T (&mxc)[3], T Lw,
 
 // divergence, sources, RK combination and tangent projection of one cell, as
 // the streaming stage (rec = 1/A, centre xyz, grad b xyz, 0)
-template <typename T>
+template <typename T, int STG>
 __device__ __forceinline__ void update_cell(const T (&Fw)[4], const T (&Fe)[4], const T (&Gs)[4], const T (&Gn)[4],
                                             const T (&rec)[8], const T (&qo)[4], const T (&xs)[4], const T (&mxc)[3],
                                             const T (&mxe)[3], const T (&mn)[3], const T (&ms)[3], T Lw, T Le, T Ln,
-                                            T Ls, T g, T omega2, T c0, T c1, T c2, T dt, T (&o)[4]) {
+                                            T Ls, T g, T omega2, T dt, T (&o)[4]) {
+  constexpr T c0 = RK3<T, STG>::b0, c1 = RK3<T, STG>::b1, c2 = RK3<T, STG>::b2;
   const T iA = rec[0];
   const T r0 = rec[1], r1 = rec[2], r2 = rec[3];
   T dq[4];
@@ -126,8 +134,8 @@ __device__ __forceinline__ void update_cell(const T (&Fw)[4], const T (&Fe)[4], 
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
     T base = T(0);
-    if (c1 != T(0)) base = c1 * qo[f];
-    if (c0 != T(0)) base += c0 * xs[f];
+    if constexpr (c1 != T(0)) base = c1 * qo[f];
+    if constexpr (c0 != T(0)) base += c0 * xs[f];
     o[f] = c2 * dt * dq[f] + base;
   }
   const T d = o[1] * r0 + o[2] * r1 + o[3] * r2;
@@ -144,7 +152,8 @@ struct RowGeo {
 template <typename T, int LIM, int R>
 __global__ __launch_bounds__(MW * MWPB) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 8 ? STSP_M3_WPE64 : STSP_M3_WPE32)))
 void march3_kernel(Args<T> a, P3<T> m) {
-  pin_args(a);
+  // (no pin_args: a long-running march needs few of the arguments, and pinned
+  // SGPRs spilled into VGPR lanes inside the loop)
   // per wave: the stage-1 and stage-2 results [row % 3], and the raw step
   // input rows j - 4 .. j + 2 [row % 7] (stage 1's own cell, the RK base of
   // stages 2 and 3): read once from memory, never again
@@ -275,42 +284,43 @@ void march3_kernel(Args<T> a, P3<T> m) {
 #pragma unroll
     for (int f = 0; f < 4; ++f) v[f] = qg[((y % 7) * 4 + f) * MW + lane];
   };
-  auto mrow = [&](int j, T (&v)[3]) {
+  auto mrow = [&](int jp, T (&v)[3]) {               // face-line normals of y-face jp (clamped)
+    const int jc = jp < 0 ? 0 : (jp > n ? n : jp);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) v[k] = myt[k * (n + 1) + j];
+    for (int k = 0; k < 3; ++k) v[k] = myt[k * (n + 1) + jc];
   };
 
-  // one consumed row r of interior stage s (2 or 3): slope of row r - 1, flux
+  // one consumed row r of interior stage STG (2 or 3): slope of row r - 1, flux
   // through the face below it (k = rows consumed before r), then, from the
   // fifth row on, the update of row r - 2 into o (returns true when it did).
-  // G: geometry of row r - 2 (its Ln is the face r - 1)
-  auto stage_row = [&](MRows<T>& st, const T (&C)[5], int r, int k, int s, const RowGeo<T>& G, T (&o)[4]) -> bool {
+  // G: geometry of row r - 2 (its Ln is the face r - 1); mn / ms: normals of
+  // the faces above / below row r - 2
+  auto stage_row = [&](auto stg, MRows<T>& st, const T (&C)[5], int r, int k, const RowGeo<T>& G,
+                       const T (&mn)[3], const T (&ms)[3], T (&o)[4]) -> bool {
+    constexpr int STG = decltype(stg)::value;
     T hsB[4], Gn[4] = {T(0), T(0), T(0), T(0)};
 #pragma unroll
     for (int f = 0; f < 4; ++f) hsB[f] = half_slope<LIM>(st.cB[f] - st.cA[f], C[f] - st.cB[f]);
     if (k >= 3) {
-      T wl[4], wr[4], mf[3];
-      mrow(r - 1, mf);
+      T wl[4], wr[4];
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
         wl[f] = st.cA[f] + st.hsA[f];
         wr[f] = st.cB[f] - hsB[f];
       }
-      swe_flux<T>(wl, wr, st.cA, st.cB, mf[0], mf[1], mf[2], G.Ln, g, Gn);
+      swe_flux<T>(wl, wr, st.cA, st.cB, mn[0], mn[1], mn[2], G.Ln, g, Gn);
     }
     bool out = false;
     if (k >= 4) {
       const int j = r - 2;
-      T xs[4], qo[4], mn[3], ms[3];
+      T xs[4], qo[4];
       qring_ld(j, xs);
-      ring_ld(s - 2, j, qo);
-      mrow(j + 1, mn);
-      mrow(j, ms);
+      ring_ld(STG - 2, j, qo);
       T Fw[4], Fe[4];
       xfaces<T, LIM>(st.cA, mxc, G.Lw, g, Fw, Fe);
       const T Le = shl(G.Lw);
-      update_cell<T>(Fw, Fe, st.Gs, Gn, G.rec, qo, xs, mxc, mxe, mn, ms, G.Lw, Le, G.Ln, G.Ls, g, a.omega2,
-                     m.b0[s - 1], m.b1[s - 1], m.b2[s - 1], a.dt, o);
+      update_cell<T, STG>(Fw, Fe, st.Gs, Gn, G.rec, qo, xs, mxc, mxe, mn, ms, G.Lw, Le, G.Ln, G.Ls, g, a.omega2,
+                          a.dt, o);
       out = true;
     }
 #pragma unroll
@@ -325,7 +335,8 @@ void march3_kernel(Args<T> a, P3<T> m) {
   for (int f = 0; f < 5; ++f) st2.cA[f] = st2.cB[f] = st3.cA[f] = st3.cB[f] = T(0);
 #pragma unroll
   for (int f = 0; f < 4; ++f) st2.hsA[f] = st2.Gs[f] = st3.hsA[f] = st3.Gs[f] = T(0);
-  // geometry of each stage's row in the first iteration
+  // geometry of each stage's row in the first iteration; afterwards each
+  // stage loads its next row's geometry right after using the current one
   RowGeo<T> G1, G2, G3;
   ld_geo(y0, G1);
   ld_geo(y0 - 2, G2);
@@ -355,6 +366,12 @@ void march3_kernel(Args<T> a, P3<T> m) {
     mrow(y0, mf);
     swe_flux<T>(wl, wr, cm1, cA, mf[0], mf[1], mf[2], G1.Ls, g, Gs);
   }
+  // normals of the face below each stage's row (the face above it is the next
+  // row's face below: one load of three values per stage and row)
+  T ms1[3], ms2[3], ms3[3];
+  mrow(y0, ms1);
+  mrow(y0 - 2, ms2);
+  mrow(y0 - 4, ms3);
   T qn[4];                                           // raw row j + 2, loaded one step ahead
   ldq(xc, y0 + 2, qn);
 
@@ -363,10 +380,9 @@ void march3_kernel(Args<T> a, P3<T> m) {
     prim(qn, cC);
     qring_st(j + 2, qn);
     if (j + 1 < y1) ldq(xc, j + 3, qn);              // prefetch (row j + 3 <= n + 1)
-    T qo[4], mn[3], ms[3];
+    T qo[4], mn[3];
     qring_ld(j, qo);
     mrow(j + 1, mn);
-    mrow(j, ms);
 
     // ---- stage 1, y: slope of row j + 1, flux through the face above row j ---
     T hsB[4], Gn[4];
@@ -447,9 +463,11 @@ void march3_kernel(Args<T> a, P3<T> m) {
     {
       const T xz[4] = {T(0), T(0), T(0), T(0)};
       const T Le = shl(G1.Lw);
-      update_cell<T>(Fw, Fe, Gs, Gn, G1.rec, qo, xz, mxc, mxe, mn, ms, G1.Lw, Le, G1.Ln, G1.Ls, g, a.omega2,
-                     m.b0[0], m.b1[0], m.b2[0], a.dt, o1);
+      update_cell<T, 1>(Fw, Fe, Gs, Gn, G1.rec, qo, xz, mxc, mxe, mn, ms1, G1.Lw, Le, G1.Ln, G1.Ls, g, a.omega2,
+                        a.dt, o1);
     }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ms1[k] = mn[k];
     ld_geo(j + 1, G1);                               // stage 1's next row, an iteration ahead
     ring_st(0, j, o1);
     if (own & (j >= rlo) & (j < rhi)) {
@@ -482,7 +500,11 @@ void march3_kernel(Args<T> a, P3<T> m) {
     {
       T C2[5], o2[4];
       prim(o1, C2);
-      const bool out2 = stage_row(st2, C2, j, j - y0, 2, G2, o2);
+      T mn2[3];
+      mrow(j - 1, mn2);
+      const bool out2 = stage_row(std::integral_constant<int, 2>(), st2, C2, j, j - y0, G2, mn2, ms2, o2);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) ms2[k] = mn2[k];
       ld_geo(j - 1, G2);
       if (out2) {
         const int j2 = j - 2;
@@ -494,7 +516,11 @@ void march3_kernel(Args<T> a, P3<T> m) {
         }
         T C3[5], o3[4];
         prim(o2, C3);
-        const bool out3 = stage_row(st3, C3, j2, j2 - (ys - 2), 3, G3, o3);
+        T mn3[3];
+        mrow(j - 3, mn3);
+        const bool out3 = stage_row(std::integral_constant<int, 3>(), st3, C3, j2, j2 - (ys - 2), G3, mn3, ms3, o3);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ms3[k] = mn3[k];
         if (out3) {
           const int j3 = j2 - 2;
           if (own & (x >= 4) & (x < n - 4)) {
@@ -521,11 +547,10 @@ int march3_l(const StageDesc* d, const March3Desc* md, hipStream_t s) {
   P3<T> m;
   m.q1 = (T*)md->q1;
   m.q2 = (T*)md->q2;
-  for (int k = 0; k < 3; ++k) {
-    m.b0[k] = (T)md->b0[k];
-    m.b1[k] = (T)md->b1[k];
-    m.b2[k] = (T)md->b2[k];
-  }
+  // the kernel's SSP-RK3 coefficients are compile-time (RK3<T, s>): refuse others
+  const double b[3][3] = {{0.0, 1.0, 1.0}, {0.75, 0.25, 0.25}, {1.0 / 3.0, 2.0 / 3.0, 2.0 / 3.0}};
+  for (int k = 0; k < 3; ++k)
+    if (md->b0[k] != b[k][0] || md->b1[k] != b[k][1] || md->b2[k] != b[k][2]) return -14;
   m.D = md->D;
   m.ncs = (d->n - 8 + M3O - 1) / M3O;
   m.nrs = (d->n - 8 + R - 1) / R;

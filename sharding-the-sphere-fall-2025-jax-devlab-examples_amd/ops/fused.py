@@ -1255,7 +1255,8 @@ class FusedKernel:
             self.prime()
 
     def _setup_exchange(self, X, timeout_s: float) -> None:
-        from .xgmi import IpcRing, _declare
+        from .xgmi import IpcRing, _declare, refuse_if_forced
+        refuse_if_forced()
         e = self.e
         L = _declare(self.lib)
         if int(L.stsp_xg_protocol()) != 1:

@@ -88,11 +88,18 @@ def march3_unsupported(engine) -> Optional[str]:
     return None
 
 
+# The automatic runtime choice keeps the three-launch streaming stage: the
+# pipelined step measured even with it at C720 on one MI355X (fp64 405 vs 394
+# us/step, fp32 207 vs 181-188: profiles/r6_march3/README.md), so `auto` leaves
+# it off and `on` selects it.
+MARCH3_AUTO = False
+
+
 def march3_wanted(engine) -> bool:
     """The size rule of the streaming stage (HipCompute.march_wanted) on a rank
-    the pipelined step applies to."""
+    the pipelined step applies to, when the automatic choice takes it."""
     hc = getattr(engine, "compute", None)
-    return bool(getattr(hc, "march_wanted", False)) and march3_unsupported(engine) is None
+    return MARCH3_AUTO and bool(getattr(hc, "march_wanted", False)) and march3_unsupported(engine) is None
 
 
 class March3Step:

@@ -217,6 +217,15 @@ class XgmiPlan:
             self.nprod[p] = len(np.unique(blk))
 
 
+def refuse_if_forced() -> None:
+    """Test hook of the transport fallback chain (xgmi -> ipc -> rccl):
+    ``STSP_FAIL_XGMI=1`` makes every direct-ring setup raise on every rank
+    alike, as a node without peer IPC would."""
+    import os
+    if os.environ.get("STSP_FAIL_XGMI") == "1":
+        raise RuntimeError("direct xGMI ring setup refused (STSP_FAIL_XGMI=1 test hook)")
+
+
 class XgmiHalo:
     """Memory, IPC mappings and initial delivery of the direct exchange for
     one ``Engine(backend='hip')``; ``fill(desc)`` turns a stage descriptor into
@@ -224,6 +233,7 @@ class XgmiHalo:
 
     def __init__(self, engine, group=None, timeout_s: float = 2.0):
         from . import native
+        refuse_if_forced()
         from .hip_compute import HipCompute
         e = engine
         if not isinstance(e.compute, HipCompute):

@@ -46,21 +46,23 @@ def test_single_gpu_solver_matches_cpu(limiter, tmp_path):
     assert type(g.runner).__name__ == "NativeStepper"
 
 
-def _spmd_worker(rank, world, port, t, outdir, comm, fused="auto"):
+def _spmd_worker(rank, world, port, t, outdir, comm, fused="auto", fail_xgmi=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), STSP_SHARE_GPU="1")
+    if fail_xgmi:
+        os.environ["STSP_FAIL_XGMI"] = "1"     # every ring setup raises: the chain lands on ipc
     import torch.distributed as dist
     try:
-        c = _cfg(world, t, out=os.path.join(outdir, "run"), comm=comm)
+        c = _cfg(world, t, out=os.path.join(outdir, "run"), comm="xgmi" if fail_xgmi else comm)
         c["runtime"]["fused"] = fused
         s = Solver(c, verbose=False)
         s.initialize()
-        assert s.comm == comm
         s.run(nsteps=6)
+        assert s.comm == comm, s.comm
         # the default SPMD runtime is the fused step with the xGMI ring inside
         # it (every block of the rank's share resident); "off", or another
         # exchange: stage kernels (ipc: graph-replayed IPC copies)
-        assert (s.fused is not None) == (fused != "off" and comm == "xgmi"), s.fused
+        assert (s.fused is not None) == (fused != "off" and comm == "xgmi" and not fail_xgmi), s.fused
         if comm == "ipc":
             assert s.runner.use_graph and s.runner.stats["graph_steps"] > 0, s.runner.stats
         s.save_checkpoint()
@@ -101,6 +103,24 @@ def test_spmd_xgmi_solver_matches_single_and_restarts(world, t, fused, comm, tmp
     b = np.load(os.path.join(out, "b.npy"))
     assert np.array_equal(a, r)      # same kernels, same order: bitwise
     assert np.array_equal(b, r)      # restart from step 6 re-delivers the remote ghosts
+
+
+@pytest.mark.parametrize("fused", ["auto", "off"])
+def test_spmd_solver_falls_back_to_ipc_when_the_rings_fail(fused, tmp_path):
+    """Transport chain xgmi -> ipc -> rccl: with every direct-ring setup
+    refused (STSP_FAIL_XGMI=1, as on a node without peer IPC) the Solver lands
+    on the graph-captured IPC copy transport on every rank, bitwise equal to
+    one GPU running the stage kernels."""
+    out = str(tmp_path)
+    mp.spawn(_spmd_worker, args=(2, _free_port(), 1, out, "ipc", fused, True), nprocs=2, join=True)
+    c = _cfg(1, 1, out=str(tmp_path / "ref"))
+    c["runtime"]["fused"] = "off"
+    ref = Solver(c, verbose=False)
+    ref.initialize()
+    ref.run(nsteps=10)
+    r = ref.gather_global()
+    assert np.array_equal(np.load(os.path.join(out, "a.npy")), r)
+    assert np.array_equal(np.load(os.path.join(out, "b.npy")), r)
 
 
 def test_tc1_norms_on_the_hip_path_match_reference_and_converge():
