@@ -52,9 +52,26 @@ bool rccl_sym(void* h, const char* name, F& out) {
 const RcclApi* rccl_api() {
   if (g_rccl_done) return g_rccl.version ? &g_rccl : nullptr;
   g_rccl_done = true;
-  // the copy already in the process (PyTorch's), else the one on the search path
-  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-  g_rccl.path = "librccl.so.1 (already loaded)";
+  // STSP_RCCL_LIB=<path>: that RCCL (e.g. ROCm's /opt/rocm/lib/librccl.so.1.0.70200)
+  // beside PyTorch's copy, its own symbols bound first (RTLD_DEEPBIND, local);
+  // its HIP runtime dependency resolves to the one already loaded (same
+  // soname), so torch streams stay usable.  Else the copy already in the
+  // process (PyTorch's), else the one on the search path.
+  void* h = nullptr;
+  static std::string alt_path;
+  if (const char* alt = std::getenv("STSP_RCCL_LIB")) {
+    h = dlopen(alt, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
+    if (!h) {
+      g_rccl_err = std::string("cannot load STSP_RCCL_LIB=") + alt + ": " + dlerror();
+      return nullptr;
+    }
+    alt_path = std::string(alt) + " (STSP_RCCL_LIB, deepbind)";
+    g_rccl.path = alt_path.c_str();
+  }
+  if (!h) {
+    h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    g_rccl.path = "librccl.so.1 (already loaded)";
+  }
   if (!h) {
     h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
     g_rccl.path = "librccl.so.1 (dlopen)";
@@ -113,6 +130,12 @@ extern "C" int stsp_rccl_version(void) {
 }
 
 extern "C" const char* stsp_rccl_error(void) { return g_rccl_err.c_str(); }
+
+// which librccl the runtime resolved (after stsp_rccl_version() succeeded)
+extern "C" const char* stsp_rccl_path(void) {
+  const RcclApi* r = rccl_api();
+  return r && r->path ? r->path : "";
+}
 
 namespace {
 

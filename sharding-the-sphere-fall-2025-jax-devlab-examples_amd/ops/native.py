@@ -152,6 +152,8 @@ def _declare_runtime(L):
     L.stsp_rccl_version.restype = ci
     L.stsp_rccl_error.argtypes = []
     L.stsp_rccl_error.restype = ctypes.c_char_p
+    L.stsp_rccl_path.argtypes = []
+    L.stsp_rccl_path.restype = ctypes.c_char_p
     L.stsp_roctx_push.argtypes = [ctypes.c_char_p]
     L.stsp_roctx_push.restype = ci
     L.stsp_roctx_pop.argtypes = []

@@ -10,6 +10,9 @@ bitwise equality with the single-rank engine, graph replay counts, and eager /
 replayed us per step.
 
     STSP_GRAPH_COMM=1 NCCL_GRAPH_MIXING_SUPPORT=0 python tools/rccl_capture_probe.py
+    STSP_RCCL_LIB=/opt/rocm/lib/librccl.so.1.0.70200 STSP_GRAPH_COMM=1 python tools/rccl_capture_probe.py
+
+(STSP_RCCL_LIB: ROCm 7.2's RCCL 2.27.7 beside torch's 2.26.6, ops/csrc/runtime.cpp.)
 """
 import argparse
 import json
@@ -27,6 +30,8 @@ def main():
     ap.add_argument("--N", type=int, default=24)
     ap.add_argument("--steps", type=int, default=60)
     a = ap.parse_args()
+    import faulthandler
+    faulthandler.enable()        # a crash inside capture / replay names its Python frame
     import torch
     import torch.distributed as dist
     from stsphere.engine import Engine
@@ -43,6 +48,7 @@ def main():
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     comm = nr.create_nccl_comm(0, 1, 0)
     out = {"rccl_version": nr.rccl_version() if hasattr(nr, "rccl_version") else None,
+           "rccl_path": nr.lib().stsp_rccl_path().decode(),
            "env": {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_", "STSP_GRAPH"))}}
     g = CubedSphereGrid(a.N)
     ref = Engine(ShallowWater("tc5"), TileLayout(a.N, 2, 1, ng=2), grid=g, device="cuda", backend="hip")
@@ -57,6 +63,8 @@ def main():
     e = make()
     ns = nr.NativeStepper(e, nccl_comm=comm, use_graph=True, steps_per_graph=3)
     out["graph_capture_enabled"] = bool(ns.use_graph)
+    print(f"[probe] {out['rccl_path']} v{out['rccl_version']}: stepper built, running 6 steps", file=sys.stderr,
+          flush=True)
     ref.step(6)
     ns.run(6)
     torch.cuda.synchronize()
