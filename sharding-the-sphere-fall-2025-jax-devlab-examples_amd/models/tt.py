@@ -715,9 +715,19 @@ class CubedSphereLowRankDiffusion:
         return U6 + c * lap
 
 
+def _setup_svd(M: torch.Tensor):
+    """Thin SVD for setup (coefficient / initial-field factors): large device
+    matrices go through the host LAPACK in fp64 (rocSOLVER's gesvd takes
+    seconds per 1024^2 panel), the factors come back to M's device."""
+    if M.device.type == "cuda" and M.numel() > 65536:
+        u, s, vh = torch.linalg.svd(M.detach().to(device="cpu", dtype=torch.float64), full_matrices=False)
+        return (x.to(device=M.device, dtype=M.dtype) for x in (u, s, vh))
+    return torch.linalg.svd(M, full_matrices=False)
+
+
 def lowrank_coefficients(M: torch.Tensor, eps: float):
     """Factor a fixed coefficient field M [n, m] as C D^T to relative accuracy eps."""
-    u, s, vh = torch.linalg.svd(M, full_matrices=False)
+    u, s, vh = _setup_svd(M)
     r = _trunc_rank(s, eps * float(torch.linalg.norm(s)), None)
     return (u[:, :r] * s[:r]).contiguous(), vh[:r].T.contiguous()
 
@@ -859,6 +869,13 @@ class CubedSphereLowRankAdvection:
         return torch.stack([f.dense() for f in F])
 
 
+# columns per native rounding call of the six-panel SWE's "hip" backend: the
+# device core (tt_core_kernel) takes k <= 32; wider cores go through the host
+# Jacobi SVD (~1.7 ms per call at k = 64 measured at N = 256,
+# profiles/r6_tt/README.md)
+ROUND_CAP = 32
+
+
 class CubedSphereLowRankShallowWater:
     """Linearised rotating shallow water on the six panels of the cubed
     sphere, carried entirely in factored form U_p = A_p B_p^T: the six-panel
@@ -888,14 +905,31 @@ class CubedSphereLowRankShallowWater:
     the same two cells from both sides, so the total mass sum(A h) is
     conserved to round-off and truncation.  ``dense_step`` is the N x N
     six-panel reference of the same discrete operator
-    (tests/test_tt_and_models.py: factored vs dense to 1e-10)."""
+    (tests/test_tt_and_models.py: factored vs dense to 1e-10).
+
+    ``backend``: "torch" rounds every product with Householder QR + SVD
+    (``recompress``); "hip" (CUDA tensors) rounds every product of at most 64
+    columns (and no more columns than rows) in ONE native call,
+    ``ops/tt_ops.recompress`` = stsp_tt_recompress: CholeskyQR3 of both
+    factors on the MFMA Gram / Cholesky / product kernels, the k x k core on
+    the device, one 4-byte read-back.  Wider products (a coefficient of rank
+    rc times a field of rank rf has rc rf columns) are rounded chunk by chunk
+    through the same call (``_round_native``); only a product whose rank
+    fills min(32, N / 2) columns stays on the library QR (rocSOLVER) and SVD.
+    ``stats`` counts native calls and library roundings
+    (tests/test_tt_kernels.py, tools/tt_sphere_bench.py)."""
 
     FIELDS = ("h", "vx", "vy", "vz")
 
     def __init__(self, N: int, H: float = 1000.0, g: float = 9.80616, omega: float = 7.292e-5,
                  eps: float = 1e-13, max_rank: Optional[int] = None, coef_eps: float = 1e-15,
-                 dtype=torch.float64, device="cpu"):
+                 dtype=torch.float64, device="cpu", backend: str = "torch"):
         from .geometry import CubedSphereGrid
+        if backend not in ("torch", "hip"):
+            raise ValueError(f"backend must be 'torch' or 'hip', got {backend!r}")
+        if backend == "hip" and torch.device(device).type != "cuda":
+            raise ValueError("backend 'hip' needs a CUDA device")
+        self.backend = backend
         self.N, self.H, self.g, self.omega = N, H, g, omega
         self.eps, self.max_rank = eps, max_rank
         self.dtype, self.device = dtype, torch.device(device)
@@ -927,7 +961,7 @@ class CubedSphereLowRankShallowWater:
         self._e = e
         c = math.sqrt(g * H)
         self.dt_max = 0.5 * grid.min_spacing() / (c + 1e-300)
-        self.stats = {"recompressions": 0, "max_k": 0}
+        self.stats = {"recompressions": 0, "max_k": 0, "native": 0, "library": 0}
 
     def coefficient_ranks(self) -> dict:
         rk = lambda L: max(int(C.shape[1]) for C, _ in L)
@@ -938,8 +972,44 @@ class CubedSphereLowRankShallowWater:
     # ---- factored operator ----------------------------------------------------
     def _trunc(self, A, B) -> LowRankField:
         self.stats["recompressions"] += 1
-        self.stats["max_k"] = max(self.stats["max_k"], int(A.shape[1]))
+        k = int(A.shape[1])
+        self.stats["max_k"] = max(self.stats["max_k"], k)
+        if self.backend == "hip":
+            out = self._round_native(A, B)
+            if out is not None:
+                return out
+        self.stats["library"] += 1
         return recompress(A, B, self.eps, self.max_rank)
+
+    def _round_native(self, A, B, cap: Optional[int] = None) -> Optional[LowRankField]:
+        """Round A B^T with native calls of at most cap = min(ROUND_CAP,
+        rows / 2) columns (the k x k core runs on the device up to 32 columns;
+        a factor at least twice as tall as wide keeps CholeskyQR well posed):
+        the first cap columns, then the running result concatenated
+        with the next cap - rank columns, and so on (A B^T is the sum of its
+        column chunks' products; each rounding is relative to its partial sum,
+        max_rank applies to the last).  A Khatri-Rao product of rc rf columns
+        thus costs ~rc (r + rf)^2 N instead of (rc rf)^2 N.  None (library path)
+        when the running rank fills the cap."""
+        from ..ops import tt_ops
+        k = int(A.shape[1])
+        if cap is None:
+            cap = min(ROUND_CAP, int(A.shape[0]) // 2, int(B.shape[0]) // 2)
+        if k <= cap:
+            self.stats["native"] += 1
+            return LowRankField(*tt_ops.recompress(A, B, self.eps, self.max_rank))
+        a, b = tt_ops.recompress(A[:, :cap], B[:, :cap], self.eps)
+        calls, o = 1, cap
+        while o < k:
+            c = cap - int(a.shape[1])
+            if c < 1:
+                return None
+            last = o + c >= k
+            a, b = tt_ops.recompress(torch.cat([a, A[:, o:o + c]], 1), torch.cat([b, B[:, o:o + c]], 1), self.eps,
+                                     self.max_rank if last else None)
+            calls, o = calls + 1, o + c
+        self.stats["native"] += calls
+        return LowRankField(a, b)
 
     def _avg_x(self, X: LowRankField, g: torch.Tensor):
         """Face values of x-faces [N, N+1] with the W / E ghost strips."""

@@ -467,7 +467,8 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       // another rank's cell: spin on its granules in ring slot xe % SLOTS until
       // every tag carries this step (xe + 1); a timeout sets err and falls through
       constexpr int G = sizeof(T) / 4;
-      const gu64* rp = (const gu64*)(a.recv) + (long)(xe_ % STSP_XG_SLOTS) * a.ring + (long)(-2 - src) * (4 * G);
+      const gu64* rp = (const gu64*)(a.recv) + (long)(xe_ % STSP_XG_SLOTS) * a.ring;
+      const int nrec = a.ring / (4 * G), rec = -2 - src;
       const unsigned want = (unsigned)xe_ + 1u;
       unsigned long long gr[4 * G];
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -475,7 +476,8 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         bool ok = true;
         if (STSP_XG_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 #pragma unroll
-        for (int k = 0; k < 4 * G; ++k) gr[k] = __hip_atomic_load(rp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int k = 0; k < 4 * G; ++k)
+          gr[k] = __hip_atomic_load(rp + ring_word(nrec, 4 * G, rec, k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const unsigned er = __hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int k = 0; k < 4 * G; ++k) ok &= (unsigned)(gr[k] >> 32) == want;
@@ -1010,18 +1012,20 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       for (int k = 0; k < a.K; ++k) {
         const int code = xp[k];
         if (code < 0) break;
-        gu64* dst = ((gu64*)(a.peer_ring[code >> 24])) + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring +
-                    (long)(code & 0xFFFFFF) * (4 * G);
+        gu64* dst = ((gu64*)(a.peer_ring[code >> 24])) + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring;
+        const int nrec = a.ring / (4 * G), rec = code & 0xFFFFFF;
         const unsigned long long tag = (unsigned long long)((unsigned)xe + 2u) << 32;
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
           if constexpr (G == 2) {
             const unsigned long long b = __builtin_bit_cast(unsigned long long, Q[f]);
-            __hip_atomic_store(dst + 2 * f, tag | (b & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(dst + 2 * f + 1, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          } else {
-            __hip_atomic_store(dst + f, tag | __builtin_bit_cast(unsigned, Q[f]), __ATOMIC_RELAXED,
+            __hip_atomic_store(dst + ring_word(nrec, 8, rec, 2 * f), tag | (b & 0xFFFFFFFFull), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(dst + ring_word(nrec, 8, rec, 2 * f + 1), tag | (b >> 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+          } else {
+            __hip_atomic_store(dst + ring_word(nrec, 4, rec, f), tag | __builtin_bit_cast(unsigned, Q[f]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           }
         }
       }

@@ -120,7 +120,8 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
         }
         if (m < 0) {                               // remote slot -1 - m: spin on its granules
           constexpr int G = sizeof(T) / 4;
-          const gu64* rp = ((const gu64*)(a.recv)) + (long)(xe % STSP_XG_SLOTS) * a.ring + (long)(-1 - m) * (4 * G);
+          const gu64* rp = ((const gu64*)(a.recv)) + (long)(xe % STSP_XG_SLOTS) * a.ring;
+          const int nrec = a.ring / (4 * G), rec = -1 - m;
           const unsigned want = (unsigned)xe + 1u;
           unsigned long long gr[4 * G];
           const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -128,7 +129,7 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
             bool ok = true;
 #pragma unroll
             for (int k = 0; k < 4 * G; ++k) {
-              gr[k] = __hip_atomic_load(rp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              gr[k] = __hip_atomic_load(rp + ring_word(nrec, 4 * G, rec, k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
               ok &= (unsigned)(gr[k] >> 32) == want;
             }
             if (ok) break;
@@ -482,18 +483,20 @@ void march_kernel(Args<T> a, int ncs, int nrs, int njobs) {
           // another rank's ghost: its ring slot (xe + 1) % SLOTS, tag xe + 2
           constexpr int G = sizeof(T) / 4;
           const int code = -2 - pt[k];
-          gu64* dst = ((gu64*)(a.peer_ring[code >> 24])) + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring +
-                      (long)(code & 0xFFFFFF) * (4 * G);
+          gu64* dst = ((gu64*)(a.peer_ring[code >> 24])) + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring;
+          const int nrec = a.ring / (4 * G), rec = code & 0xFFFFFF;
           const unsigned long long tag = (unsigned long long)((unsigned)xe + 2u) << 32;
 #pragma unroll
           for (int f = 0; f < 4; ++f) {
             if constexpr (G == 2) {
               const unsigned long long bits = __builtin_bit_cast(unsigned long long, o[f]);
-              __hip_atomic_store(dst + 2 * f, tag | (bits & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              __hip_atomic_store(dst + 2 * f + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            } else {
-              __hip_atomic_store(dst + f, tag | __builtin_bit_cast(unsigned, o[f]), __ATOMIC_RELAXED,
+              __hip_atomic_store(dst + ring_word(nrec, 8, rec, 2 * f), tag | (bits & 0xFFFFFFFFull), __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(dst + ring_word(nrec, 8, rec, 2 * f + 1), tag | (bits >> 32), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+              __hip_atomic_store(dst + ring_word(nrec, 4, rec, f), tag | __builtin_bit_cast(unsigned, o[f]),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
           }
         }

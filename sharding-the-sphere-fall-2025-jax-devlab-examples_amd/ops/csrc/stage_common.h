@@ -34,6 +34,20 @@
 // 2 or 3: S = 4 (three slots left a window where a peer two stages ahead
 // overwrote the slot a slow block of ours was still reading).
 #define STSP_XG_SLOTS 4
+// Ring record layout.  A slot holds nrec = ring / NW records of NW words (NW =
+// F G tagged 8-byte granules, or F values under STSP_XG_TAG=0).
+// STSP_XG_SOA=1 (default): word-major, word w of record r at w nrec + r.  The
+// host numbers a consumer's records by owner rank, then cell id (row order),
+// so the lanes of one store or poll instruction touch consecutive 8-byte words
+// (up to 512 contiguous bytes per wave) instead of words NW x 8 bytes apart
+// (record-major, r NW + w: STSP_XG_SOA=0, the round-5 layout, kept for the A/B
+// in profiles/r6_ring).
+#ifndef STSP_XG_SOA
+#define STSP_XG_SOA 1
+#endif
+__device__ __forceinline__ long ring_word(int nrec, int nw, int rec, int w) {
+  return STSP_XG_SOA ? (long)w * nrec + rec : (long)rec * nw + w;
+}
 // Own-cell waves: 1 = the first waves not on SIMD 0, 0 = waves 0 .. n-1.
 #ifndef STSP_OWN_SKIP0
 #define STSP_OWN_SKIP0 1

@@ -416,8 +416,8 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
             if constexpr (XG && STSP_XG_TAG) {
               // spin on this cell's granules until all carry this stage's tag
               constexpr int G = sizeof(T) / 4;
-              const gu64* rp = ((const gu64*)(a.recv)) + (long)(xe % STSP_XG_SLOTS) * a.ring +
-                               (long)(-1 - m) * (F * G);
+              const gu64* rp = ((const gu64*)(a.recv)) + (long)(xe % STSP_XG_SLOTS) * a.ring;
+              const int nrec = a.ring / (F * G), rec = -1 - m;
               const unsigned want = (unsigned)xe + 1u;
               unsigned long long gr[F * G];
               const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -425,7 +425,8 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
                 bool ok = true;
 #pragma unroll
                 for (int k = 0; k < F * G; ++k) {
-                  gr[k] = __hip_atomic_load(rp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                  gr[k] = __hip_atomic_load(rp + ring_word(nrec, F * G, rec, k), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_SYSTEM);
                   ok &= (unsigned)(gr[k] >> 32) == want;
                 }
                 if (ok) break;
@@ -444,9 +445,9 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
                   v[f] = __builtin_bit_cast(T, (unsigned)gr[f]);
               }
             } else if constexpr (XG) {
-              const T* rp = rring + (long)(-1 - m) * F;
+              const int nrec = a.ring / F;
 #pragma unroll
-              for (int f = 0; f < F; ++f) v[f] = ld_sys(rp + f);
+              for (int f = 0; f < F; ++f) v[f] = ld_sys(rring + ring_word(nrec, F, -1 - m, f));
             } else {
               const T* rp = rring + (long)(-1 - m) * F;
 #pragma unroll
@@ -837,24 +838,27 @@ __device__ __forceinline__ void stage_body(const Args<T>& a, const int bid) {
           const int code = -2 - pt[k];
           if constexpr (STSP_XG_TAG) {
             constexpr int G = sizeof(T) / 4;
-            gu64* dst = ((gu64*)(a.peer_ring[code >> 24])) + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring +
-                        (long)(code & 0xFFFFFF) * (F * G);
+            gu64* dst = ((gu64*)(a.peer_ring[code >> 24])) + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring;
+            const int nrec = a.ring / (F * G), rec = code & 0xFFFFFF;
             const unsigned long long tag = (unsigned long long)((unsigned)xe + 2u) << 32;
 #pragma unroll
             for (int f = 0; f < F; ++f) {
               if constexpr (G == 2) {
                 const unsigned long long b = __builtin_bit_cast(unsigned long long, o[f]);
-                __hip_atomic_store(dst + 2 * f, tag | (b & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(dst + 2 * f + 1, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              } else {
-                __hip_atomic_store(dst + f, tag | __builtin_bit_cast(unsigned, o[f]), __ATOMIC_RELAXED,
+                __hip_atomic_store(dst + ring_word(nrec, F * G, rec, 2 * f), tag | (b & 0xFFFFFFFFull),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(dst + ring_word(nrec, F * G, rec, 2 * f + 1), tag | (b >> 32), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
+              } else {
+                __hip_atomic_store(dst + ring_word(nrec, F, rec, f), tag | __builtin_bit_cast(unsigned, o[f]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
               }
             }
           } else {
-            T* dst = a.peer_ring[code >> 24] + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring + (long)(code & 0xFFFFFF) * F;
+            T* dst = a.peer_ring[code >> 24] + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring;
+            const int nrec = a.ring / F, rec = code & 0xFFFFFF;
 #pragma unroll
-            for (int f = 0; f < F; ++f) st_sys(dst + f, o[f]);
+            for (int f = 0; f < F; ++f) st_sys(dst + ring_word(nrec, F, rec, f), o[f]);
           }
         }
       }
@@ -987,22 +991,26 @@ __global__ __launch_bounds__(256) void xg_prime_kernel(const T* __restrict__ q, 
     const int c = code[i];
     if constexpr (STSP_XG_TAG) {
       constexpr int G = sizeof(T) / 4;
-      gu64* dst = ((gu64*)(peer_ring[c >> 24])) + (long)slot * ring + (long)(c & 0xFFFFFF) * F * G;
+      gu64* dst = ((gu64*)(peer_ring[c >> 24])) + (long)slot * ring;
+      const int nrec = ring / (F * G), rec = c & 0xFFFFFF;
       const unsigned long long tag = (unsigned long long)((unsigned)epoch + 1u) << 32;
       for (int f = 0; f < F; ++f) {
         const T v = q[(long)f * S + src[i]];
         if constexpr (G == 2) {
           const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-          __hip_atomic_store(dst + 2 * f, tag | (b & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(dst + 2 * f + 1, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(dst + ring_word(nrec, F * G, rec, 2 * f), tag | (b & 0xFFFFFFFFull), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(dst + ring_word(nrec, F * G, rec, 2 * f + 1), tag | (b >> 32), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
         } else {
-          __hip_atomic_store(dst + f, tag | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
+          __hip_atomic_store(dst + ring_word(nrec, F, rec, f), tag | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_SYSTEM);
         }
       }
     } else {
-      T* dst = peer_ring[c >> 24] + (long)slot * ring + (long)(c & 0xFFFFFF) * F;
-      for (int f = 0; f < F; ++f) st_sys(dst + f, q[(long)f * S + src[i]]);
+      T* dst = peer_ring[c >> 24] + (long)slot * ring;
+      const int nrec = ring / F, rec = c & 0xFFFFFF;
+      for (int f = 0; f < F; ++f) st_sys(dst + ring_word(nrec, F, rec, f), q[(long)f * S + src[i]]);
     }
   }
   __threadfence_system();

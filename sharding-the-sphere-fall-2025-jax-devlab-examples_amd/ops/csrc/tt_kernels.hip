@@ -489,6 +489,25 @@ __global__ __launch_bounds__(64) void chol_inv_kernel(const T* __restrict__ G, i
   // factor is well conditioned, defined when it is rank deficient)
   const bool adaptive = shift_c < 0;
   const T sc = T(adaptive ? -shift_c : shift_c);
+  // an exactly zero factor (G = 0: a field at rest times a coefficient) is
+  // X = Q R with Q = X, R = 0: R^-1 := I, no failure; its core is zero and the
+  // recompression reports the zero product (-22) for the caller to map to the
+  // rank-1 zero field
+  if (t == 0) {
+    T s = T(0);
+    for (int i = 0; i < k; ++i) s += G[(long)i * ldg + i];
+    tr = s;
+  }
+  __syncthreads();
+  if (tr == T(0)) {
+    if (t < k)
+      for (int i = 0; i < k; ++i) {
+        R[(long)i * ldr + t] = T(0);
+        Ri[(long)i * ldr + t] = i == t ? T(1) : T(0);
+      }
+    if (t == 0) info[b] = 0;
+    return;
+  }
   int bad = 0;
   for (int attempt = adaptive ? 0 : 1; attempt < 2; ++attempt) {
     if (t < k)
@@ -864,9 +883,135 @@ size_t stsp_tt_step_workspace3(int N, int r, int nsub) {
          (size_t)12 * k * k + 16;
 }
 
-// 1 (default): stsp_tt_lr_step3 forms the k x k core on the device when k <= 32
-// (tt_core_kernel); 0: on the host (jacobi_svd), for comparison
+// stsp_tt_set_core: 1 (default) forms the k x k core of stsp_tt_lr_step3 /
+// stsp_tt_recompress on the device when k <= 32 (tt_core_kernel); 0: on the
+// host (jacobi_svd), for comparison.
+
+// CholeskyQR3 of one factor X [N][k] (row stride ldx) on the device (models/
+// tt.py::cholqr3): pass p = {MFMA Gram, shifted Cholesky + inverse, MFMA
+// product}; passes write s0, s1, s0 (row stride k), so Q ends in s0 and s1 may
+// alias X.  Rs: [pass][R, Ri] k x k, dinfo[pass]: pivot flags.
+static int cholqr3_dev(int dtype, const void* X, int ldx, int N, int k, void* s0, void* s1, void* part, void* G,
+                       char* Rs, int* dinfo, hipStream_t st) {
+  const size_t es = dtype == 1 ? 8 : 4;
+  // shift coefficient 11 (N k + k (k + 1)) u (models/tt.py::cholqr3_shift)
+  const double u = dtype == 1 ? 1.1102230246251565e-16 : 5.960464477539063e-08;
+  const double shc = 11.0 * ((double)N * k + (double)k * (k + 1)) * u;
+  const int P = stsp_tt_gram_blocks(N);
+  const void* in = X;
+  int ldin = ldx;
+  void* outs[3] = {s0, s1, s0};
+  int rc;
+  for (int pass = 0; pass < 3; ++pass) {
+    char* R = Rs + es * (size_t)(pass * 2) * k * k;
+    char* Ri = R + es * (size_t)k * k;
+    if ((rc = stsp_tt_gram(dtype, in, ldin, in, ldin, N, k, k, part, P, G, k, 1.0, st))) return rc;
+    if ((rc = stsp_tt_chol_inv(dtype, G, k, 0, R, Ri, k, 0, k, 1, pass == 0 ? shc : -shc, dinfo + pass, st)))
+      return rc;
+    if ((rc = stsp_tt_mm(dtype, in, ldin, Ri, k, outs[pass], k, N, k, k, 1.0, 0.0, st))) return rc;
+    in = outs[pass];
+    ldin = k;
+  }
+  return 0;
+}
+
+// The k x k core of a recompression after CholeskyQR3 of both factors (Rs:
+// [side][pass][R, Ri], dinfo[side * 3 + pass], Q[side] with row stride k) and
+// the two final MFMA products Aout = QA (U S)_rn, Bout = QB W_rn.  k <= 32 and
+// tt_core_mode: tt_core_kernel on the device, one 4-byte read-back (the rank
+// sizes the products); else the six R factors to the host, jacobi_svd there,
+// the maps back.  dX: 2 k^2 elements; dinfo needs 9 ints.  Returns rn or < 0.
 static int tt_core_mode = 1;
+static int core_and_products(int dtype, void* const Q[2], const int Nq[2], int k, double eps, int max_rank, char* Rs,
+                             int* dinfo, void* dX, double* hbuf, void* Aout, int ldao, void* Bout, int ldbo,
+                             hipStream_t st) {
+  const size_t es = dtype == 1 ? 8 : 4;
+  auto Rp = [&](int side, int pass) { return (void*)(Rs + es * (size_t)((side * 3 + pass) * 2) * k * k); };
+  double* hR = hbuf;                 // [side][pass] k x k
+  int* hinfo = (int*)(hbuf + 6 * k * k);
+  double* hX = hbuf + 6 * k * k + 8;
+  int rc, rn;
+  if (k <= CORE_K && tt_core_mode != 0) {
+    int* drn = dinfo + 8;
+    if (dtype == 1)
+      hipLaunchKernelGGL(tt_core_kernel<double>, dim3(1), dim3(256), 0, st, (const double*)Rs, dinfo, k, eps,
+                         max_rank, (double*)dX, drn);
+    else
+      hipLaunchKernelGGL(tt_core_kernel<float>, dim3(1), dim3(256), 0, st, (const float*)Rs, dinfo, k, eps,
+                         max_rank, (float*)dX, drn);
+    if (hipGetLastError() != hipSuccess) return -25;
+    if (hipMemcpyAsync(hinfo, drn, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess) return -20;
+    if (hipStreamSynchronize(st) != hipSuccess) return -21;
+    rn = hinfo[0];
+    if (rn <= 0) return rn;
+  } else {
+    for (int side = 0; side < 2; ++side)
+      for (int pass = 0; pass < 3; ++pass)
+        if (hipMemcpyAsync((char*)hR + es * (size_t)(side * 3 + pass) * k * k, Rp(side, pass), es * (size_t)k * k,
+                           hipMemcpyDeviceToHost, st) != hipSuccess)
+          return -20;
+    if (hipMemcpyAsync(hinfo, dinfo, sizeof(int) * 6, hipMemcpyDeviceToHost, st) != hipSuccess) return -20;
+    if (hipStreamSynchronize(st) != hipSuccess) return -21;
+    for (int i = 0; i < 6; ++i)
+      if (hinfo[i] != 0) return -24;
+    if (dtype == 0) {
+      const float* f = (const float*)hR;
+      for (int i = 6 * k * k - 1; i >= 0; --i) hR[i] = (double)f[i];
+    }
+    // R = R3 R2 R1 per side, core C = Ra Rb^T
+    std::vector<double> Rt[2], tmp(k * k), C(k * k), sig(k), W(k * k);
+    for (int side = 0; side < 2; ++side) {
+      Rt[side].assign(hR + (size_t)(side * 3) * k * k, hR + (size_t)(side * 3 + 1) * k * k);
+      for (int pass = 1; pass < 3; ++pass) {
+        const double* Rk = hR + (size_t)(side * 3 + pass) * k * k;
+        for (int i = 0; i < k; ++i)
+          for (int j = 0; j < k; ++j) {
+            double acc = 0;
+            for (int l = i; l < k; ++l) acc += Rk[i * k + l] * Rt[side][l * k + j];   // Rk upper triangular
+            tmp[i * k + j] = acc;
+          }
+        Rt[side] = tmp;
+      }
+    }
+    for (int i = 0; i < k; ++i)
+      for (int j = 0; j < k; ++j) {
+        double acc = 0;
+        for (int l = 0; l < k; ++l) acc += Rt[0][i * k + l] * Rt[1][j * k + l];
+        C[i * k + j] = acc;
+      }
+    jacobi_svd(k, k, C.data(), sig.data(), W.data());       // C = (U S) W^T, U S in C's columns
+    std::vector<int> ord(k);
+    for (int j = 0; j < k; ++j) ord[j] = j;
+    std::sort(ord.begin(), ord.end(), [&](int a, int b) { return sig[a] > sig[b]; });
+    double tot = 0;
+    for (int j = 0; j < k; ++j) tot += sig[j] * sig[j];
+    rn = k;
+    double tail = 0;
+    for (int jj = k - 1; jj >= 1; --jj) {
+      tail += sig[ord[jj]] * sig[ord[jj]];
+      if (tail <= eps * eps * tot) rn = jj;
+      else break;
+    }
+    if (max_rank > 0) rn = std::min(rn, max_rank);
+    rn = std::max(rn, 1);
+    if (!(tot > 0)) return -22;
+    for (int i = 0; i < k; ++i)
+      for (int jj = 0; jj < rn; ++jj) {
+        const int j = ord[jj];
+        hX[i * 2 * k + jj] = C[i * k + j];
+        hX[i * 2 * k + rn + jj] = W[i * k + j];
+      }
+    if (dtype == 0) {
+      float* f = (float*)hX;
+      for (int i = 0; i < 2 * k * k; ++i) f[i] = (float)hX[i];
+    }
+    if (hipMemcpyAsync(dX, hX, es * 2 * k * k, hipMemcpyHostToDevice, st) != hipSuccess) return -23;
+  }
+  if ((rc = stsp_tt_mm(dtype, Q[0], k, dX, 2 * k, Aout, ldao, Nq[0], k, rn, 1.0, 0.0, st))) return rc;
+  if ((rc = stsp_tt_mm(dtype, Q[1], k, (char*)dX + es * rn, 2 * k, Bout, ldbo, Nq[1], k, rn, 1.0, 0.0, st))) return rc;
+  return rn;
+}
+
 int stsp_tt_set_core(int mode) {
   const int old = tt_core_mode;
   tt_core_mode = mode;
@@ -889,7 +1034,6 @@ int stsp_tt_lr_step3(int dtype, const void* A, int lda, const void* B, int ldb, 
   void* dX = (char*)part + es * (size_t)P * kp * kp;
   char* Rs = (char*)dX + es * (size_t)2 * k * k;          // [side][pass][R, Ri] k x k
   int* dinfo = (int*)(Rs + es * (size_t)12 * k * k);       // [side][pass]
-  auto Rp = [&](int side, int pass, int inv) { return (void*)(Rs + es * (size_t)((side * 3 + pass) * 2 + inv) * k * k); };
   int rc;
   const void* srcA = A;
   const void* srcB = B;
@@ -904,112 +1048,56 @@ int stsp_tt_lr_step3(int dtype, const void* A, int lda, const void* B, int ldb, 
     sa = sb = 2 * rr;
     cur ^= 1;
   }
-  // shift coefficient 11 (N k + k (k + 1)) u (models/tt.py::cholqr3_shift)
-  const double u = dtype == 1 ? 1.1102230246251565e-16 : 5.960464477539063e-08;
-  const double shc = 11.0 * ((double)N * k + (double)k * (k + 1)) * u;
-  void* Q[2] = {(void*)srcA, (void*)srcB};
-  int qb = cur;     // the free buffer set
+  // CholeskyQR3 per factor: scratch = the free buffer and the expansion output
+  // itself (no longer read after pass 1's Gram + product)
+  const void* src[2] = {srcA, srcB};
+  void* Q[2];
   for (int side = 0; side < 2; ++side) {
-    int qcur = qb;
-    for (int pass = 0; pass < 3; ++pass) {
-      if ((rc = stsp_tt_gram(dtype, Q[side], k, Q[side], k, N, k, k, part, P, G, k, 1.0, st))) return rc;
-      if ((rc = stsp_tt_chol_inv(dtype, G, k, 0, Rp(side, pass, 0), Rp(side, pass, 1), k, 0, k, 1,
-                                 pass == 0 ? shc : -shc, dinfo + side * 3 + pass, st)))
-        return rc;
-      void* dst = buf[qcur][side];
-      if ((rc = stsp_tt_mm(dtype, Q[side], k, Rp(side, pass, 1), k, dst, k, N, k, k, 1.0, 0.0, st))) return rc;
-      // the next pass reads dst; its own output goes to the buffer Q held
-      void* old = Q[side];
-      Q[side] = dst;
-      buf[qcur][side] = old;
-    }
+    if ((rc = cholqr3_dev(dtype, src[side], k, N, k, buf[cur][side], (void*)src[side], part, G,
+                          Rs + es * (size_t)side * 6 * k * k, dinfo + side * 3, st)))
+      return rc;
+    Q[side] = buf[cur][side];
   }
-  // R factors (not the inverses) and flags to the host in one copy each
-  double* hR = hbuf;                 // [side][pass] k x k
-  int* hinfo = (int*)(hbuf + 6 * k * k);
-  double* hX = hbuf + 6 * k * k + 8;
-  if (k <= CORE_K && tt_core_mode != 0) {
-    // the core on the device: one 4-byte read-back (the rank sizes the final products)
-    int* drn = dinfo + 8;
-    if (dtype == 1)
-      hipLaunchKernelGGL(tt_core_kernel<double>, dim3(1), dim3(256), 0, st, (const double*)Rs, dinfo, k, eps,
-                         max_rank, (double*)dX, drn);
-    else
-      hipLaunchKernelGGL(tt_core_kernel<float>, dim3(1), dim3(256), 0, st, (const float*)Rs, dinfo, k, eps,
-                         max_rank, (float*)dX, drn);
-    if (hipGetLastError() != hipSuccess) return -25;
-    if (hipMemcpyAsync(hinfo, drn, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess) return -20;
-    if (hipStreamSynchronize(st) != hipSuccess) return -21;
-    const int rn = hinfo[0];
-    if (rn <= 0) return rn;
-    if ((rc = stsp_tt_mm(dtype, Q[0], k, dX, 2 * k, Aout, ldo, N, k, rn, 1.0, 0.0, st))) return rc;
-    if ((rc = stsp_tt_mm(dtype, Q[1], k, (char*)dX + es * rn, 2 * k, Bout, ldo, N, k, rn, 1.0, 0.0, st))) return rc;
-    return rn;
-  }
-  for (int side = 0; side < 2; ++side)
-    for (int pass = 0; pass < 3; ++pass)
-      if (hipMemcpyAsync((char*)hR + es * (size_t)(side * 3 + pass) * k * k, Rp(side, pass, 0), es * (size_t)k * k,
-                         hipMemcpyDeviceToHost, st) != hipSuccess)
-        return -20;
-  if (hipMemcpyAsync(hinfo, dinfo, sizeof(int) * 6, hipMemcpyDeviceToHost, st) != hipSuccess) return -20;
-  if (hipStreamSynchronize(st) != hipSuccess) return -21;
-  for (int i = 0; i < 6; ++i)
-    if (hinfo[i] != 0) return -24;
-  if (dtype == 0) {
-    const float* f = (const float*)hR;
-    for (int i = 6 * k * k - 1; i >= 0; --i) hR[i] = (double)f[i];
-  }
-  // R = R3 R2 R1 per side, core C = Ra Rb^T
-  std::vector<double> Rt[2], tmp(k * k), C(k * k), sig(k), W(k * k);
-  for (int side = 0; side < 2; ++side) {
-    Rt[side].assign(hR + (size_t)(side * 3) * k * k, hR + (size_t)(side * 3 + 1) * k * k);
-    for (int pass = 1; pass < 3; ++pass) {
-      const double* Rk = hR + (size_t)(side * 3 + pass) * k * k;
-      for (int i = 0; i < k; ++i)
-        for (int j = 0; j < k; ++j) {
-          double acc = 0;
-          for (int l = i; l < k; ++l) acc += Rk[i * k + l] * Rt[side][l * k + j];   // Rk upper triangular
-          tmp[i * k + j] = acc;
-        }
-      Rt[side] = tmp;
-    }
-  }
-  for (int i = 0; i < k; ++i)
-    for (int j = 0; j < k; ++j) {
-      double acc = 0;
-      for (int l = 0; l < k; ++l) acc += Rt[0][i * k + l] * Rt[1][j * k + l];
-      C[i * k + j] = acc;
-    }
-  jacobi_svd(k, k, C.data(), sig.data(), W.data());       // C = (U S) W^T, U S in C's columns
-  std::vector<int> ord(k);
-  for (int j = 0; j < k; ++j) ord[j] = j;
-  std::sort(ord.begin(), ord.end(), [&](int a, int b) { return sig[a] > sig[b]; });
-  double tot = 0;
-  for (int j = 0; j < k; ++j) tot += sig[j] * sig[j];
-  int rn = k;
-  double tail = 0;
-  for (int jj = k - 1; jj >= 1; --jj) {
-    tail += sig[ord[jj]] * sig[ord[jj]];
-    if (tail <= eps * eps * tot) rn = jj;
-    else break;
-  }
-  if (max_rank > 0) rn = std::min(rn, max_rank);
-  rn = std::max(rn, 1);
-  if (!(tot > 0)) return -22;
-  for (int i = 0; i < k; ++i)
-    for (int jj = 0; jj < rn; ++jj) {
-      const int j = ord[jj];
-      hX[i * 2 * k + jj] = C[i * k + j];
-      hX[i * 2 * k + rn + jj] = W[i * k + j];
-    }
-  if (dtype == 0) {
-    float* f = (float*)hX;
-    for (int i = 0; i < 2 * k * k; ++i) f[i] = (float)hX[i];
-  }
-  if (hipMemcpyAsync(dX, hX, es * 2 * k * k, hipMemcpyHostToDevice, st) != hipSuccess) return -23;
-  if ((rc = stsp_tt_mm(dtype, Q[0], k, dX, 2 * k, Aout, ldo, N, k, rn, 1.0, 0.0, st))) return rc;
-  if ((rc = stsp_tt_mm(dtype, Q[1], k, (char*)dX + es * rn, 2 * k, Bout, ldo, N, k, rn, 1.0, 0.0, st))) return rc;
-  return rn;
+  const int Nq[2] = {N, N};
+  return core_and_products(dtype, Q, Nq, k, eps, max_rank, Rs, dinfo, dX, hbuf, Aout, ldo, Bout, ldo, st);
+}
+
+// Rounding of one product A B^T (A [NA][k], B [NB][k], k <= 64) to the rank
+// rn <= max_rank of relative accuracy eps, in one native call: CholeskyQR3 of
+// both factors on the device (MFMA Gram + shifted Cholesky + MFMA product, x 3),
+// the k x k core (device when k <= 32, else host), Aout = QA (U S)_rn,
+// Bout = QB W_rn.  The inputs are not written.  The recompression that every
+// operation of the six-panel factored SWE ends with (models/tt.py::
+// CubedSphereLowRankShallowWater, backend "hip").  ws: stsp_tt_recompress_
+// workspace elements; hbuf: 8 k^2 + 8 doubles (pinned).  Returns rn or < 0.
+size_t stsp_tt_recompress_workspace(int NA, int NB, int k) {
+  const int kp = (k + 15) / 16 * 16;
+  return (size_t)2 * ((size_t)NA + NB) * k + (size_t)k * k +
+         (size_t)stsp_tt_gram_blocks(NA > NB ? NA : NB) * kp * kp + (size_t)2 * k * k + (size_t)12 * k * k + 16;
+}
+
+int stsp_tt_recompress(int dtype, const void* A, int lda, int NA, const void* B, int ldb, int NB, int k, double eps,
+                       int max_rank, void* ws, double* hbuf, void* Aout, int ldao, void* Bout, int ldbo,
+                       hipStream_t st) {
+  if (NA < 1 || NB < 1 || k < 1 || k > 64 || lda < k || ldb < k) return -1;
+  if (dtype != 0 && dtype != 1) return -4;
+  const size_t es = dtype == 1 ? 8 : 4;
+  const int kp = (k + 15) / 16 * 16;
+  char* w = (char*)ws;
+  void* sA[2] = {w, w + es * (size_t)NA * k};
+  void* sB[2] = {w + es * 2 * (size_t)NA * k, w + es * (2 * (size_t)NA * k + (size_t)NB * k)};
+  void* G = w + es * 2 * ((size_t)NA + NB) * k;
+  void* part = (char*)G + es * (size_t)k * k;
+  void* dX = (char*)part + es * (size_t)stsp_tt_gram_blocks(NA > NB ? NA : NB) * kp * kp;
+  char* Rs = (char*)dX + es * (size_t)2 * k * k;
+  int* dinfo = (int*)(Rs + es * (size_t)12 * k * k);
+  int rc;
+  if ((rc = cholqr3_dev(dtype, A, lda, NA, k, sA[0], sA[1], part, G, Rs, dinfo, st))) return rc;
+  if ((rc = cholqr3_dev(dtype, B, ldb, NB, k, sB[0], sB[1], part, G, Rs + es * (size_t)6 * k * k, dinfo + 3, st)))
+    return rc;
+  void* Q[2] = {sA[0], sB[0]};
+  const int Nq[2] = {NA, NB};
+  return core_and_products(dtype, Q, Nq, k, eps, max_rank, Rs, dinfo, dX, hbuf, Aout, ldao, Bout, ldbo, st);
 }
 
 int stsp_tt_lr_step(int dtype, const void* A, int lda, const void* B, int ldb, int N, int r, double c, double ih2,

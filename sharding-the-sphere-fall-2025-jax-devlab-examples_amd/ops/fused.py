@@ -1586,7 +1586,8 @@ class FusedExchangePlan:
     blocks), so all ranks derive the same enumeration with no messages:
 
     * consumer p: the remote cells its blocks need (``need[0]``), ordered by
-      owner rank then global id, are the slots of its receive ring; window cells
+      owner rank, tile, producing block and cell, are the slots of its receive
+      ring; window cells
       read them as ``src = -2 - slot``;
     * producer r: for each of its cells needed by p, the code
       ``p << 24 | slot``; the fused kernel stores the cell's new value there at
@@ -1616,8 +1617,13 @@ class FusedExchangePlan:
         for p, P in enumerate(self.plans):
             m = P.need[:, 0] & (P.src == -2)
             g = np.unique(P.gid[m])
-            tid, _, _ = L.locate(g)
-            order = np.lexsort((g, owner[tid]))
+            tid, i, j = L.locate(g)
+            # producer order: owner rank, tile, block row, block column, then
+            # the block's cells in row order (the producing wave's lane order),
+            # so the word-major ring (stage_common.h, STSP_XG_SOA) takes a
+            # wave's pushes to one peer as runs of consecutive 8-byte words
+            # (tools/ring_model.py)
+            order = np.lexsort((i % B, j % B, i // B, j // B, tid, owner[tid]))
             self.need_remote.append(g[order])
         self.ring_slots = max(1, max(len(x) for x in self.need_remote))
         if self.ring_slots >= (1 << XG_SLOT_BITS):

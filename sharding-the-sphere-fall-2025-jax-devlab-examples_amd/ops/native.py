@@ -190,6 +190,10 @@ def _declare_tt(L):
     L.stsp_tt_lr_step3.restype = ci
     L.stsp_tt_step_workspace3.argtypes = [ci, ci, ci]
     L.stsp_tt_step_workspace3.restype = ctypes.c_size_t
+    L.stsp_tt_recompress_workspace.argtypes = [ci, ci, ci]
+    L.stsp_tt_recompress_workspace.restype = ctypes.c_size_t
+    L.stsp_tt_recompress.argtypes = [ci, vp, ci, ci, vp, ci, ci, ci, cd, ci, vp, vp, vp, ci, vp, ci, vp]
+    L.stsp_tt_recompress.restype = ci
     # persistent factored step (tt_persist.hip)
     L.stsp_tt_persist.argtypes = [vp, ci, vp, ci, ci, ci, ci, ci, cd, cd, ci, cd, ci, vp, vp, vp, vp, ci, vp, vp,
                                   cd, vp]

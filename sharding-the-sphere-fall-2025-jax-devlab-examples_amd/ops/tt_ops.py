@@ -4,6 +4,8 @@
 * ``tsmm(A, X, out=...)``   A X (+ beta out) for A [N, k], X [k, m], MFMA
 * ``expand(X, ...)``        [x0 X + x1 D X, y0 X + y1 D X] with D the 1-D second difference
 * ``dense_diffusion(U, c)`` U + c * (5-point Laplacian of U), zero Dirichlet
+* ``recompress(A, B, eps)`` A B^T (k <= 64 columns) rounded to rank <= max_rank:
+  CholeskyQR3 of both factors + k x k core + two products, ONE native call
 
 All of them run on torch's current stream.  Operands must be CUDA tensors of
 one dtype (float64 or float32) whose rows are contiguous (stride(1) == 1); row
@@ -133,3 +135,52 @@ def dense_diffusion(U: torch.Tensor, c: float, out: torch.Tensor = None) -> torc
                                    native.current_stream_handle())
     native.check(rc, "tt_dense_diffusion")
     return out
+
+
+class _RecompressBuffers:
+    """Device workspace and pinned host buffer of ``recompress``, grown to the
+    largest (rows, k) seen and reused (pinning host memory costs milliseconds,
+    a recompression tens of microseconds)."""
+
+    def __init__(self):
+        self.ws = None
+        self.hbuf = None
+
+    def get(self, L, NA: int, NB: int, k: int, dtype, device):
+        need = L.stsp_tt_recompress_workspace(NA, NB, k)
+        if self.ws is None or self.ws.numel() < need or self.ws.dtype != dtype or self.ws.device != device:
+            self.ws = torch.empty(need, dtype=dtype, device=device)
+        if self.hbuf is None:
+            self.hbuf = torch.empty(8 * 64 * 64 + 8, dtype=torch.float64).pin_memory()
+        return self.ws, self.hbuf
+
+
+_RBUF = _RecompressBuffers()
+
+
+def recompress(A: torch.Tensor, B: torch.Tensor, eps: float, max_rank: int = None):
+    """A [NA, k] B[NB, k]^T -> (A', B') of rank rn <= max_rank with
+    ||A B^T - A' B'^T|| <= eps ||A B^T|| (k <= 64; stsp_tt_recompress in
+    ops/csrc/tt_kernels.hip): CholeskyQR3 of each factor on the MFMA Gram /
+    Cholesky / product kernels, the k x k core on the device (k <= 32; host
+    Jacobi above), two MFMA products.  One 4-byte read-back (the rank sizes
+    the outputs).  The inputs are not written; the outputs are column slices
+    of one [NA + NB, kmax] buffer with contiguous rows."""
+    L = native.require_native()
+    code = _check(A, B)
+    NA, k = A.shape
+    NB, k2 = B.shape
+    if k2 != k or not 1 <= k <= 64:
+        raise ValueError(f"recompress: shapes {tuple(A.shape)} / {tuple(B.shape)}")
+    ws, hbuf = _RBUF.get(L, NA, NB, k, A.dtype, A.device)
+    rmax = k if not max_rank else min(k, int(max_rank))
+    out = torch.empty((NA + NB, rmax), dtype=A.dtype, device=A.device)
+    rn = L.stsp_tt_recompress(code, native.ptr(A), A.stride(0), NA, native.ptr(B), B.stride(0), NB, k, float(eps),
+                              int(max_rank or 0), native.ptr(ws), native.ptr(hbuf), native.ptr(out), rmax,
+                              native.ptr(out[NA:]), rmax, native.current_stream_handle())
+    if rn == -22:           # the product is exactly zero: the rank-1 zero field
+        z = out[:, :1].zero_()
+        return z[:NA], z[NA:]
+    if rn <= 0:
+        raise RuntimeError(f"stsp_tt_recompress failed ({rn})")
+    return out[:NA, :rn], out[NA:, :rn]

@@ -57,8 +57,9 @@ def test_bench_deadline_kills_hung_rank_cpu():
     assert len(lines) == 1, r.stdout + r.stderr
     out = json.loads(lines[0])
     assert out["status"] == "timeout" and out["value"] is None
-    assert out["phases"]["1"]["phase"] == "warmup"
-    assert out["phases"]["0"]["phase"] in ("warmup", "verify")
+    # phases carry the transport being tried (warmup_<comm>, verify_<comm>)
+    assert out["phases"]["1"]["phase"].startswith("warmup")
+    assert out["phases"]["0"]["phase"].split("_")[0] in ("warmup", "verify")
 
 
 def test_bench_preflight_refuses_missing_gpus():

@@ -314,3 +314,32 @@ def test_cube_lowrank_shallow_water_curvature_sum_kills_constant_gradient():
     F = sw.to_factored(W)
     Rf = sw.to_dense(sw.rhs(F))
     assert float(Rf.abs().max()) < 1e-9
+
+
+def test_cube_lowrank_shallow_water_chunked_rounding_cpu(monkeypatch):
+    """The hip backend's chunk-by-chunk rounding of wide products
+    (``_round_native``: <= min(ROUND_CAP, N / 2) columns per native call, the
+    running result carried into the next chunk), with the native call replaced
+    by the QR + SVD rounding of the same columns: still the dense operator to
+    1e-10."""
+    from stsphere.ops import tt_ops
+
+    def fake(A, B, eps, max_rank=None):
+        assert A.shape[1] <= min(tt.ROUND_CAP, A.shape[0] // 2, B.shape[0] // 2)
+        f = tt.recompress(A, B, eps, max_rank)
+        return f.A, f.B
+
+    monkeypatch.setattr(tt_ops, "recompress", fake)
+    N = 40
+    sw = tt.CubedSphereLowRankShallowWater(N, eps=1e-13)
+    sw.backend = "hip"
+    W = sw.gaussian_hill()
+    F = sw.to_factored(W)
+    Wd = W.clone()
+    for _ in range(2):
+        F = sw.step(F, sw.dt_max)
+        Wd = sw.dense_step(Wd, sw.dt_max)
+    D = sw.to_dense(F)
+    assert float((D - Wd).abs().amax() / Wd.abs().amax()) < 1e-10
+    st = sw.stats
+    assert st["native"] > st["recompressions"] - st["library"] > 0
