@@ -716,10 +716,11 @@ class CubedSphereLowRankDiffusion:
 
 
 def _setup_svd(M: torch.Tensor):
-    """Thin SVD for setup (coefficient / initial-field factors): large device
-    matrices go through the host LAPACK in fp64 (rocSOLVER's gesvd takes
-    seconds per 1024^2 panel), the factors come back to M's device."""
-    if M.device.type == "cuda" and M.numel() > 65536:
+    """Thin SVD for setup (coefficient factors): device matrices go through
+    the host LAPACK in fp64 and the factors come back to M's device.
+    rocSOLVER's device SVD takes seconds per 1024^2 panel and left ~1e-9
+    relative errors in small factors (profiles/r6_tt/README.md)."""
+    if M.device.type == "cuda":
         u, s, vh = torch.linalg.svd(M.detach().to(device="cpu", dtype=torch.float64), full_matrices=False)
         return (x.to(device=M.device, dtype=M.dtype) for x in (u, s, vh))
     return torch.linalg.svd(M, full_matrices=False)
@@ -978,8 +979,30 @@ class CubedSphereLowRankShallowWater:
             out = self._round_native(A, B)
             if out is not None:
                 return out
+            self.stats["library"] += 1
+            return self._round_library(A, B)
         self.stats["library"] += 1
         return recompress(A, B, self.eps, self.max_rank)
+
+    def _round_library(self, A, B) -> LowRankField:
+        """The hip backend's rounding of a product too wide for the native
+        call: Householder QR of both factors on the device (rocSOLVER geqrf),
+        the core's SVD on the host in fp64 (LAPACK).  The device SVD of the
+        core (rocSOLVER's Jacobi-based gesvd path) left relative errors up to
+        4e-9 per rounding where this route and the native call stay near
+        1e-12 (profiles/r6_tt/README.md)."""
+        qa, ra = torch.linalg.qr(A)
+        qb, rb = torch.linalg.qr(B)
+        C = (ra @ rb.T).to(device="cpu", dtype=torch.float64).numpy()
+        u, sv, vt = np.linalg.svd(C)
+        tail = np.cumsum((sv * sv)[::-1])[::-1]
+        ok = np.nonzero(tail <= (self.eps * self.eps) * max(tail[0], 1e-300))[0]
+        r = max(1, int(ok[0]) if ok.size else len(sv))
+        if self.max_rank is not None:
+            r = min(r, self.max_rank)
+        Xa = torch.as_tensor(np.ascontiguousarray(u[:, :r] * sv[:r]), dtype=A.dtype, device=A.device)
+        Xb = torch.as_tensor(np.ascontiguousarray(vt[:r].T), dtype=B.dtype, device=B.device)
+        return LowRankField(qa @ Xa, qb @ Xb)
 
     def _round_native(self, A, B, cap: Optional[int] = None) -> Optional[LowRankField]:
         """Round A B^T with native calls of at most cap = min(ROUND_CAP,
@@ -1110,8 +1133,16 @@ class CubedSphereLowRankShallowWater:
 
     # ---- conversions / diagnostics --------------------------------------------
     def to_factored(self, W: torch.Tensor):
-        return [[LowRankField.from_dense(W[q, p].to(device=self.device, dtype=self.dtype), min(self.eps, 1e-14),
-                                         self.max_rank) for p in range(6)] for q in range(4)]
+        """Factor a dense state (setup): the SVDs run on the host in fp64
+        (LAPACK); rocSOLVER's device SVD left ~1e-9 relative errors in the
+        initial factors, more than the whole factored run adds
+        (profiles/r6_tt/README.md)."""
+        def fac(U):
+            f = LowRankField.from_dense(U.detach().to(device="cpu", dtype=torch.float64), min(self.eps, 1e-14),
+                                        self.max_rank)
+            return LowRankField(f.A.to(device=self.device, dtype=self.dtype),
+                                f.B.to(device=self.device, dtype=self.dtype))
+        return [[fac(W[q, p]) for p in range(6)] for q in range(4)]
 
     @staticmethod
     def to_dense(F) -> torch.Tensor:

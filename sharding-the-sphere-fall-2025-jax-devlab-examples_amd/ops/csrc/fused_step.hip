@@ -186,6 +186,13 @@ struct FArgs {
   const unsigned* sched;  // [nb][3 stages][17]: per wave (16) bit p = the wave runs face pass p (faces 64 p ..
                           // 64 p + 63); word 16 bit p = pass p holds a face next to a panel-edge line
   const T* nrmf;          // [nb][3][NFL] per-face normals of panel-edge blocks (PFN builds)
+  // tagged in-launch hand-off (one rank, several steps per launch; null = the
+  // epoch hand-off): [2 slots][4 G words][S] u64, word-major.  At the end of
+  // step e every block stores its cells as 4 G tagged granules {tag = e + 2,
+  // 32-bit payload} into slot (e + 1) & 1; a reader of step e + 1 re-reads its
+  // window cell's granules until every tag matches.  The data is the flag: no
+  // drain, no barrier, no epoch store and no separate poll round trip.
+  unsigned long long* hx;
 };
 
 // The launch's first failure, for the host's message (err[0..5]): the code
@@ -357,6 +364,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   int xe = 0;                                            // steps this block has completed
   const int nsteps = MULTI ? a.nsteps : 1;
   const bool epoch_on = XG || MULTI;
+  const bool tagh = MULTI && !XG && a.hx != nullptr;     // block-uniform
   if (epoch_on) xe = a.epoch[bid];
   const int n = a.n;
   // a window cell's panel and panel-local index (cube topology) and its
@@ -507,6 +515,36 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       for (int f = 0; f < 4; ++f) Q[f] = T(0);
     }
   };
+  // a window cell of another block at step xe_ > launch start, tagged hand-off
+  auto load_tagged = [&](int src_, T (&q)[4], int xe_) {
+    constexpr int G = sizeof(T) / 4;
+    const unsigned S = (unsigned)a.S;
+    const gu64* hp = (const gu64*)a.hx + (size_t)(xe_ & 1) * (4 * G) * S + (unsigned)src_;
+    const unsigned want = (unsigned)xe_ + 1u;
+    unsigned long long gr[4 * G];
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < 4 * G; ++k) gr[k] = __hip_atomic_load(hp + (size_t)k * S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < 4 * G; ++k) ok &= (unsigned)(gr[k] >> 32) == want;
+      if (ok) break;
+      if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
+        fused_fail(a.err, 2u, bid, xe_, src_, (int)(gr[0] >> 32));
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      if constexpr (G == 2)
+        q[f] = __builtin_bit_cast(T, (gr[2 * f + 1] << 32) | (gr[2 * f] & 0xFFFFFFFFull));
+      else
+        q[f] = __builtin_bit_cast(T, (unsigned)gr[f]);
+    }
+  };
   auto load_state = [&](const T* Qin, int xe_) { load_state_of(src, Q, Qin, xe_); };
   T* const buf[2] = {const_cast<T*>(a.Q), a.out};
   load_state(buf[0], xe);
@@ -608,6 +646,18 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
 #pragma unroll
     for (int k = 0; k < TPT; ++k)
       if (tl_wi[k] >= 0) load_state_of(tl_src[k], tq[k], Qin, xe_);
+  };
+  auto tail_load_tagged = [&](int xe_, T (&tq)[TPT][4]) {
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+      if (tl_wi[k] >= 0) {
+        if (tl_src[k] >= 0) load_tagged(tl_src[k], tq[k], xe_);
+        else {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) tq[k][f] = T(0);
+        }
+      }
+    }
   };
   auto tail_put = [&](const T (&tq)[TPT][4]) {
 #pragma unroll
@@ -754,7 +804,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     enter_cell();
   }
   __syncthreads();
-  if (wait && tid < 64) {
+  if (wait && !tagh && tid < 64) {
     // wait for the producers' previous step (wave 0 polls) ...
     const int p = tid < a.PM ? a.prod[(long)bid * a.PM + tid] : -1;
     const int pa = p >= 0 ? p : bid;
@@ -778,8 +828,10 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       __builtin_amdgcn_s_sleep(1);
     }
   } else {
-    // ... while the other waves compute the inner stage-1 faces
-    const int t0 = wait ? tid - 64 : tid, dt_ = wait ? NT - 64 : NT;
+    // ... while the other waves compute the inner stage-1 faces (tagged
+    // hand-off: every wave; the ring loads below are the wait)
+    const bool w0 = wait && !tagh;
+    const int t0 = w0 ? tid - 64 : tid, dt_ = w0 ? NT - 64 : NT;
     for (int t = t0; t < NI; t += dt_) inner_face(t);
   }
   FSTAMP(1);
@@ -788,10 +840,22 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     // this step's ring (the own cells' new state is still in Q), tail cells
     // issued first
     T tq[TPT][4];
-    tail_load(buf[it & 1], xe, tq);
-    if (tid >= B * B) {
-      load_state(buf[it & 1], xe);
-      enter_cell();
+    if (tagh) {
+      tail_load_tagged(xe, tq);
+      if (tid >= B * B) {
+        if (src >= 0) load_tagged(src, Q, xe);
+        else {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) Q[f] = T(0);
+        }
+        enter_cell();
+      }
+    } else {
+      tail_load(buf[it & 1], xe, tq);
+      if (tid >= B * B) {
+        load_state(buf[it & 1], xe);
+        enter_cell();
+      }
     }
     tail_put(tq);
     __syncthreads();
@@ -969,7 +1033,24 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     const unsigned S = (unsigned)a.S;
     unsigned so = (unsigned)src;
     asm volatile("" : "+v"(so));
-    if (MULTI) {             // write-through: the next step's readers may sit on another XCD
+    if (tagh && !last) {     // tagged granules for the next step's readers (word-major)
+      constexpr int G = sizeof(T) / 4;
+      gu64* hp = (gu64*)a.hx + (size_t)((xe + 1) & 1) * (4 * G) * S + so;
+      const unsigned long long tag = (unsigned long long)((unsigned)xe + 2u) << 32;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        if constexpr (G == 2) {
+          const unsigned long long b = __builtin_bit_cast(unsigned long long, Q[f]);
+          __hip_atomic_store(hp + (size_t)(2 * f) * S, tag | (b & 0xFFFFFFFFull), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(hp + (size_t)(2 * f + 1) * S, tag | (b >> 32), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          __hip_atomic_store(hp + (size_t)f * S, tag | __builtin_bit_cast(unsigned, Q[f]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    } else if (MULTI) {      // write-through: the next step's readers may sit on another XCD
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
         T* p = o32(Out, so + f * S);
@@ -1037,7 +1118,11 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   }
   if (epoch_on) {
     // every storing wave drains its stores, then one lane publishes the step
-    if (MULTI) {
+    // (tagged hand-off: the step count only at the end of the launch, for the
+    // next launch)
+    if (tagh) {
+      if (last && tid == 0) a.epoch[bid] = xe + 1;
+    } else if (MULTI) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) __hip_atomic_store(a.epoch + bid, xe + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1081,6 +1166,7 @@ int launch_fused(const FusedDesc* d, hipStream_t s) {
   a.PM = d->PM;
   a.sched = (const unsigned*)d->sched;
   a.nrmf = (const T*)d->nrmf;
+  a.hx = (unsigned long long*)d->hx;
   if (!a.sched || !a.nrmf) return -4;
   if (a.nsteps > 1 && (!a.prod || a.PM <= 0 || a.PM > 64 || !d->epoch || !d->err)) return -7;
   a.mdiv_n = magic_div((unsigned)d->n, (unsigned long long)d->N + 1);

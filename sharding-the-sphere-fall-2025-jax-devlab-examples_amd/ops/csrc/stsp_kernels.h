@@ -165,6 +165,9 @@ typedef struct FusedDesc {
   // word 16 bit p = pass p holds a face next to a panel-edge line
   const unsigned* sched;
   const void* nrmf;     // [nb][3][2 H1 (H1+1)] per-face normals of panel-edge blocks (component-major)
+  // tagged in-launch hand-off of a one-rank multi-step launch, [2][4 G][S] u64
+  // zero-initialised and kept with the epoch array; null = epoch hand-off
+  void* hx;
 } FusedDesc;
 int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stream);
 int stsp_fused_limits(int* gmax, int* cmax);

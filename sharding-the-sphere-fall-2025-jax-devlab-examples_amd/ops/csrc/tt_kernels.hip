@@ -467,38 +467,86 @@ int lr_core(int k, const double* Ga, const double* Gb, double eps, int max_rank,
 // Q's near-null directions carry no weight in the product, so the truncation
 // bound of the core SVD is unchanged.
 //
-// This kernel is the k x k part of one pass: one 64-thread workgroup per
-// matrix (batch = blockIdx.x), G in LDS, right-looking Cholesky (thread c owns
-// column c), then R^-1 by back substitution (thread c owns column c of the
-// inverse).  info[b] = j + 1 if pivot j was not positive (left for the host to
-// report; the factor is then unusable).
-template <typename T>
-__global__ __launch_bounds__(64) void chol_inv_kernel(const T* __restrict__ G, int ldg, long sg, T* __restrict__ R,
-                                                      T* __restrict__ Ri, int ldr, long sr, int k, double shift_c,
-                                                      int* __restrict__ info) {
-  __shared__ T a[64][65];
-  __shared__ T xi[64][65];
-  __shared__ T tr;
-  __shared__ int piv;
-  const int b = blockIdx.x, t = threadIdx.x;
-  G += b * sg;
-  R += b * sr;
-  Ri += b * sr;
+// This kernel is the k x k part of one pass: one wave per matrix (batch =
+// blockIdx.x).  Lane c holds column c of G in registers (padded to KP = 16,
+// 32 or 64 with an identity block, R = diag(R_k, I), so every loop has static
+// bounds); the right-looking Cholesky and then R^-1 by back substitution take
+// the other columns' entries by lane shuffles (ds_bpermute), no LDS round
+// trip and no barrier per column.  The round-5 form (thread per column through
+// LDS, three barriers per column) took 54 us per k ~ 30 matrix in the six-panel
+// SWE's roundings (profiles/r6_tt).  info[b] = j + 1 if pivot j was not
+// positive (left for the host to report; the factor is then unusable).
+template <typename T, int KP>
+__device__ __forceinline__ void chol_inv_wave(const T* __restrict__ G, int ldg, T* __restrict__ R,
+                                              T* __restrict__ Ri, int ldr, int k, double shift_c, T tr,
+                                              int* __restrict__ info) {
+  const int lane = threadIdx.x;
   // shift_c < 0: try the plain Cholesky first and shift (by |shift_c|) only
   // if a pivot fails (CholeskyQR passes 2 and 3: orthonormal to eps when the
   // factor is well conditioned, defined when it is rank deficient)
   const bool adaptive = shift_c < 0;
   const T sc = T(adaptive ? -shift_c : shift_c);
+  T g[KP];
+  int fail = 0;
+  for (int attempt = adaptive ? 0 : 1; attempt < 2; ++attempt) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      g[i] = (i < k && lane < k) ? G[(long)i * ldg + lane] : (i == lane ? T(1) : T(0));
+      if (attempt == 1 && i == lane && lane < k) g[i] += sc * tr;
+    }
+    fail = 0;
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      T d = __shfl(g[j], j);
+      if (!(d > T(0))) { if (!fail) fail = j + 1; d = T(1); }
+      const T sq = sqrt(d);
+      if (lane == j) g[j] = sq;
+      if (lane > j) g[j] /= sq;
+      const T rt = g[j];
+#pragma unroll
+      for (int i = j + 1; i < KP; ++i) {
+        const T rji = __shfl(g[j], i);             // R[j][i]: lane i's column
+        if (i <= lane) g[i] -= rji * rt;
+      }
+    }
+    if (!fail) break;
+  }
+  // column c of R^-1: x[c][c] = 1 / R[c][c], x[i][c] = -(sum_{i<l<=c} R[i][l] x[l][c]) / R[i][i]
+  T ri[KP];
+#pragma unroll
+  for (int i = KP - 1; i >= 0; --i) {
+    const T rii = __shfl(g[i], i);
+    T sum = T(0);
+#pragma unroll
+    for (int l = i + 1; l < KP; ++l) sum += __shfl(g[i], l) * ri[l];
+    ri[i] = i == lane ? T(1) / rii : (i < lane ? -sum / rii : T(0));
+  }
+  if (lane < k) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i)
+      if (i < k) {
+        R[(long)i * ldr + lane] = i <= lane ? g[i] : T(0);
+        Ri[(long)i * ldr + lane] = ri[i];
+      }
+  }
+  if (lane == 0) info[blockIdx.x] = fail;
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void chol_inv_kernel(const T* __restrict__ G, int ldg, long sg, T* __restrict__ R,
+                                                      T* __restrict__ Ri, int ldr, long sr, int k, double shift_c,
+                                                      int* __restrict__ info) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  G += b * sg;
+  R += b * sr;
+  Ri += b * sr;
+  T tr = t < k ? G[(long)t * ldg + t] : T(0);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) tr += __shfl_xor(tr, o);
   // an exactly zero factor (G = 0: a field at rest times a coefficient) is
   // X = Q R with Q = X, R = 0: R^-1 := I, no failure; its core is zero and the
   // recompression reports the zero product (-22) for the caller to map to the
   // rank-1 zero field
-  if (t == 0) {
-    T s = T(0);
-    for (int i = 0; i < k; ++i) s += G[(long)i * ldg + i];
-    tr = s;
-  }
-  __syncthreads();
   if (tr == T(0)) {
     if (t < k)
       for (int i = 0; i < k; ++i) {
@@ -508,53 +556,9 @@ __global__ __launch_bounds__(64) void chol_inv_kernel(const T* __restrict__ G, i
     if (t == 0) info[b] = 0;
     return;
   }
-  int bad = 0;
-  for (int attempt = adaptive ? 0 : 1; attempt < 2; ++attempt) {
-    if (t < k)
-      for (int i = 0; i < k; ++i) a[i][t] = G[(long)i * ldg + t];
-    __syncthreads();
-    if (t == 0) {
-      T s = T(0);
-      for (int i = 0; i < k; ++i) s += a[i][i];
-      tr = s;
-      piv = 0;
-    }
-    __syncthreads();
-    if (attempt == 1 && t < k) a[t][t] += sc * tr;
-    __syncthreads();
-    for (int j = 0; j < k; ++j) {
-      if (t == 0) {
-        T d = a[j][j];
-        if (!(d > T(0))) { if (!piv) piv = j + 1; d = T(1); }
-        a[j][j] = sqrt(d);
-      }
-      __syncthreads();
-      if (t > j && t < k) a[j][t] /= a[j][j];
-      __syncthreads();
-      if (t > j && t < k) {
-        const T rt = a[j][t];
-        for (int i = j + 1; i <= t; ++i) a[i][t] -= a[j][i] * rt;
-      }
-      __syncthreads();
-    }
-    bad = piv;
-    __syncthreads();
-    if (!bad) break;
-  }
-  // column c of R^-1: x[c][c] = 1 / R[c][c], x[i][c] = -(sum_{i<l<=c} R[i][l] x[l][c]) / R[i][i]
-  if (t < k) {
-    xi[t][t] = T(1) / a[t][t];
-    for (int i = t - 1; i >= 0; --i) {
-      T s = T(0);
-      for (int l = i + 1; l <= t; ++l) s += a[i][l] * xi[l][t];
-      xi[i][t] = -s / a[i][i];
-    }
-    for (int i = 0; i < k; ++i) {
-      R[(long)i * ldr + t] = i <= t ? a[i][t] : T(0);
-      Ri[(long)i * ldr + t] = i <= t ? xi[i][t] : T(0);
-    }
-  }
-  if (t == 0) info[b] = bad;
+  if (k <= 16) chol_inv_wave<T, 16>(G, ldg, R, Ri, ldr, k, shift_c, tr, info);
+  else if (k <= 32) chol_inv_wave<T, 32>(G, ldg, R, Ri, ldr, k, shift_c, tr, info);
+  else chol_inv_wave<T, 64>(G, ldg, R, Ri, ldr, k, shift_c, tr, info);
 }
 
 
@@ -620,11 +624,17 @@ __global__ __launch_bounds__(256) void tt_core_kernel(const T* __restrict__ Rs, 
     sW[i * KS + j] = i == j ? 1.0 : 0.0;
   }
   __syncthreads();
-  if (tid == 0) {
+  {   // ||C||_F^2: strided partial sums, wave reduction, one add per wave
     double t = 0;
-    for (int i = 0; i < k; ++i)
-      for (int j = 0; j < k; ++j) t += sC[i * KS + j] * sC[i * KS + j];
-    s_tot = t;
+    for (int e = tid; e < kk; e += blockDim.x) {
+      const double x = sC[(e / k) * KS + e % k];
+      t += x * x;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+    if ((tid & 63) == 0) sig[tid >> 6] = t;     // sig[] is free until the sweeps end
+    __syncthreads();
+    if (tid == 0) s_tot = (sig[0] + sig[1]) + (sig[2] + sig[3]);   // fixed order: reproducible
   }
   __syncthreads();
   const double tiny = 1e-30 * s_tot;
@@ -683,14 +693,14 @@ __global__ __launch_bounds__(256) void tt_core_kernel(const T* __restrict__ Rs, 
     sig[tid] = sqrt(s2);
   }
   __syncthreads();
+  if (tid < k) {   // descending order by rank (ties by index): thread j places column j
+    const double v = sig[tid];
+    int r = 0;
+    for (int i = 0; i < k; ++i) r += sig[i] > v || (sig[i] == v && i < tid);
+    s_ord[r] = tid;
+  }
+  __syncthreads();
   if (tid == 0) {
-    for (int j = 0; j < k; ++j) s_ord[j] = j;
-    for (int a = 1; a < k; ++a) {              // insertion sort, descending
-      const int v = s_ord[a];
-      int b = a - 1;
-      while (b >= 0 && sig[s_ord[b]] < sig[v]) { s_ord[b + 1] = s_ord[b]; --b; }
-      s_ord[b + 1] = v;
-    }
     double tot = 0;
     for (int j = 0; j < k; ++j) tot += sig[j] * sig[j];
     int rn = k;

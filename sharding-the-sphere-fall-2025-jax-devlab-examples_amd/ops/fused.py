@@ -39,6 +39,7 @@ Stage ``s`` (1-based) updates the square ``[lo_s, hi_s)`` with
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -1234,6 +1235,13 @@ class FusedKernel:
         self.mem = None
         # per-block step counters (xGMI tags; waits inside a multi-step launch)
         self.tens["epoch"] = torch.zeros(nb, dtype=torch.int32, device=dev)
+        # tagged in-launch hand-off (one rank): [2 slots][4 G words][S] u64,
+        # zero tags; lives with the epoch array, whose counts only grow, so a
+        # tag a reader waits for was written in the same launch
+        self.handoff = handoff_mode() if X is None else "epoch"
+        if self.handoff == "tag":
+            words = 4 * (torch.tensor([], dtype=e.dtype).element_size() // 4)
+            self.tens["hx"] = torch.zeros(2 * words * e.plan.S, dtype=torch.int64, device=dev)
         self.tens["err"] = torch.zeros(8, dtype=torch.int32, device=dev)   # code, block, step, what, seen
         self.tens["prod"] = torch.as_tensor(producer_table(P), dtype=torch.int32, device=dev).contiguous()
         # face passes per wave, balanced over the SIMDs (pass_schedule)
@@ -1318,6 +1326,7 @@ class FusedKernel:
         d.PM = int(tn["prod"].shape[1])
         d.sched = p(tn["sched"])
         d.nrmf = p(tn["nrmf"])
+        d.hx = p(tn["hx"]) if self.handoff == "tag" else 0
         if self.mem is not None:
             d.xg = 1
             d.ring = self.ring
@@ -1574,6 +1583,20 @@ def ctypes_limits(L) -> Tuple[int, int]:
 # ---------------------------------------------------------------------------
 # Several ranks: remote window cells through the direct xGMI ring
 # ---------------------------------------------------------------------------
+
+def handoff_mode() -> str:
+    """In-launch hand-off of a one-rank multi-step fused launch:
+    ``STSP_FUSED_HANDOFF`` = "tag" (tagged granules, the data is the flag) or
+    "epoch" (write-through state, drained per-block step counter, producer
+    poll; profiles/r6_handoff)."""
+    m = os.environ.get("STSP_FUSED_HANDOFF", HANDOFF_DEFAULT)
+    if m not in ("tag", "epoch"):
+        raise ValueError(f"STSP_FUSED_HANDOFF must be 'tag' or 'epoch', got {m!r}")
+    return m
+
+
+HANDOFF_DEFAULT = "epoch"
+
 
 XG_SLOT_BITS = 24
 
