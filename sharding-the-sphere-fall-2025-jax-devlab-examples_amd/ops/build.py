@@ -29,13 +29,15 @@ ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
 # march waves per SIMD) and the timing-only fused-step probe fp_alledge;
 # xgfence: system-scope fences around the fused step's xGMI ring (multi-rank
 # visibility diagnostic); xgaos: the record-major ring layout of round 5
-# (STSP_XG_SOA=0), the A/B of profiles/r6_ring
+# (STSP_XG_SOA=0), the A/B of profiles/r6_ring; ftag: the fused step's tagged
+# in-launch hand-off (STSP_FUSED_HANDOFF=tag, profiles/r6_handoff)
 VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgc": ["-DSTSP_XG_TAG=0"],
                  "unfused": ["-DSTSP_FUSE_FACES=0"], "pe0": ["-DSTSP_PE_WAVE=0"],
                  "ownw0": ["-DSTSP_OWN_SKIP0=0"], "w9": ["-DSTSP_W10=0"], "swsqrt": ["-DSTSP_HW_SQRT=0"],
                  "selslope": ["-DSTSP_SIGN_SLOPE=0"], "wpe6": ["-DSTSP_WPE=6"], "wpe7": ["-DSTSP_WPE=7"],
                  "fp_alledge": ["-DSTSP_FPROBE_ALLEDGE=1"],
-                 "xgfence": ["-DSTSP_XG_FENCE=1"], "xgaos": ["-DSTSP_XG_SOA=0"]}
+                 "xgfence": ["-DSTSP_XG_FENCE=1"], "xgaos": ["-DSTSP_XG_SOA=0"],
+                 "ftag": ["-DSTSP_FUSED_TAGH=1"]}
 
 
 def lib_for(variant: str = "") -> str:

@@ -55,6 +55,12 @@
 #ifndef STSP_XG_FENCE
 #define STSP_XG_FENCE 0
 #endif
+// Tagged in-launch hand-off (FArgs::hx, STSP_FUSED_HANDOFF=tag on the host):
+// compiled in only by the ftag variant, so the production epoch path carries
+// none of its code (profiles/r6_handoff: slower at B = 16, faster at B = 6)
+#ifndef STSP_FUSED_TAGH
+#define STSP_FUSED_TAGH 0
+#endif
 
 namespace {
 
@@ -364,7 +370,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   int xe = 0;                                            // steps this block has completed
   const int nsteps = MULTI ? a.nsteps : 1;
   const bool epoch_on = XG || MULTI;
-  const bool tagh = MULTI && !XG && a.hx != nullptr;     // block-uniform
+  const bool tagh = STSP_FUSED_TAGH && MULTI && !XG && a.hx != nullptr;     // block-uniform
   if (epoch_on) xe = a.epoch[bid];
   const int n = a.n;
   // a window cell's panel and panel-local index (cube topology) and its
@@ -1260,6 +1266,9 @@ extern "C" int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stre
 }
 
 // Compile-time sizes of the fused kernel (host checks): ghost entries and corner faces per block.
+// 1 if this library carries the tagged in-launch hand-off (ftag variant)
+extern "C" int stsp_fused_tagh(void) { return STSP_FUSED_TAGH; }
+
 extern "C" int stsp_fused_limits(int* gmax, int* cmax) {
   *gmax = FD<3, 16>::GMAX;
   *cmax = FD<3, 16>::CMAX;

@@ -171,6 +171,7 @@ typedef struct FusedDesc {
 } FusedDesc;
 int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stream);
 int stsp_fused_limits(int* gmax, int* cmax);
+int stsp_fused_tagh(void);
 // Direct xGMI halo build constants: protocol (0 counters, 1 tagged granules), ring slots.
 int stsp_xg_protocol(void);
 int stsp_xg_slots(void);

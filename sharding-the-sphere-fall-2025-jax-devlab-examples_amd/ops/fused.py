@@ -1239,6 +1239,8 @@ class FusedKernel:
         # zero tags; lives with the epoch array, whose counts only grow, so a
         # tag a reader waits for was written in the same launch
         self.handoff = handoff_mode() if X is None else "epoch"
+        if self.handoff == "tag" and not int(self.lib.stsp_fused_tagh()):
+            raise RuntimeError("STSP_FUSED_HANDOFF=tag needs the ftag library (STSP_VARIANT=ftag)")
         if self.handoff == "tag":
             words = 4 * (torch.tensor([], dtype=e.dtype).element_size() // 4)
             self.tens["hx"] = torch.zeros(2 * words * e.plan.S, dtype=torch.int64, device=dev)
@@ -1586,9 +1588,9 @@ def ctypes_limits(L) -> Tuple[int, int]:
 
 def handoff_mode() -> str:
     """In-launch hand-off of a one-rank multi-step fused launch:
-    ``STSP_FUSED_HANDOFF`` = "tag" (tagged granules, the data is the flag) or
-    "epoch" (write-through state, drained per-block step counter, producer
-    poll; profiles/r6_handoff)."""
+    ``STSP_FUSED_HANDOFF`` = "tag" (tagged granules, the data is the flag;
+    needs the ``ftag`` library, STSP_VARIANT=ftag) or "epoch" (write-through
+    state, drained per-block step counter, producer poll; profiles/r6_handoff)."""
     m = os.environ.get("STSP_FUSED_HANDOFF", HANDOFF_DEFAULT)
     if m not in ("tag", "epoch"):
         raise ValueError(f"STSP_FUSED_HANDOFF must be 'tag' or 'epoch', got {m!r}")

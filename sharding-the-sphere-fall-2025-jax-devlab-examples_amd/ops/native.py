@@ -115,6 +115,8 @@ def load(build_if_missing: bool = True):
         L.stsp_march3_launch.restype = ci
         L.stsp_fused_limits.argtypes = [ctypes.POINTER(ci), ctypes.POINTER(ci)]
         L.stsp_fused_limits.restype = ci
+        L.stsp_fused_tagh.argtypes = []
+        L.stsp_fused_tagh.restype = ci
         _declare_runtime(L)
         _declare_tt(L)
         L.stsp_schedule_spin.argtypes = [ci]

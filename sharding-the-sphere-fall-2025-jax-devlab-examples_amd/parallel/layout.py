@@ -206,16 +206,17 @@ class TileLayout:
         return out
 
     def needs(self, rank: int, peer: int) -> np.ndarray:
-        """Ordered unique global cells owned by `peer` that `rank` reads as
-        ghosts (first-occurrence order of rank's ghost enumeration: the edge
-        strips, then the carried corner ghosts)."""
+        """Unique global cells owned by `peer` that `rank` reads as ghosts
+        (edge strips and carried corner ghosts), in global-id order: the
+        producer's row order, so a wave's pushes of one row land in
+        consecutive receive slots of the word-major xGMI ring
+        (tools/ring_model.py).  Every transport (ring slots, RCCL pack / unpack,
+        IPC copies) numbers slots from this one list."""
         cs = self.corner_sources(rank)
         src = np.concatenate([self.ghost_sources(rank).reshape(-1), cs[cs >= 0]])
         tid, _, _ = self.locate(src)
         own = np.asarray(self.owner)[tid]
-        sel = src[own == peer]
-        _, first = np.unique(sel, return_index=True)
-        return sel[np.sort(first)]
+        return np.unique(src[own == peer])
 
     def local_flat(self, gflat: np.ndarray) -> np.ndarray:
         """global flat -> padded offset in the owning rank's storage."""
