@@ -19,7 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libstsp.so")
 SOURCES = ["stage_kernel.hip", "march_kernel.hip", "march3_kernel.hip", "fused_step.hip", "tt_kernels.hip", "tt_persist.hip", "runtime.cpp"]
-HEADERS = ["stsp_kernels.h", "stage_common.h", "march_common.h", "runtime.h", "rccl_abi.h"]
+HEADERS = ["stsp_kernels.h", "stage_common.h", "march_common.h", "tt_common.h", "runtime.h", "rccl_abi.h"]
 ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
 # library variants: "" = production; "diag" = in-kernel phase stamps of the
 # stage kernel (-DSTSP_STAMPS); "xgc" = the arrival-counter hand-off of the
@@ -29,15 +29,13 @@ ARCH = os.environ.get("STSP_OFFLOAD_ARCH", "gfx950")
 # march waves per SIMD) and the timing-only fused-step probe fp_alledge;
 # xgfence: system-scope fences around the fused step's xGMI ring (multi-rank
 # visibility diagnostic); xgaos: the record-major ring layout of round 5
-# (STSP_XG_SOA=0), the A/B of profiles/r6_ring; ftag: the fused step's tagged
-# in-launch hand-off (STSP_FUSED_HANDOFF=tag, profiles/r6_handoff)
+# (STSP_XG_SOA=0), the A/B of profiles/r6_ring
 VARIANT_FLAGS = {"": [], "diag": ["-DSTSP_STAMPS"], "xgc": ["-DSTSP_XG_TAG=0"],
                  "unfused": ["-DSTSP_FUSE_FACES=0"], "pe0": ["-DSTSP_PE_WAVE=0"],
                  "ownw0": ["-DSTSP_OWN_SKIP0=0"], "w9": ["-DSTSP_W10=0"], "swsqrt": ["-DSTSP_HW_SQRT=0"],
                  "selslope": ["-DSTSP_SIGN_SLOPE=0"], "wpe6": ["-DSTSP_WPE=6"], "wpe7": ["-DSTSP_WPE=7"],
                  "fp_alledge": ["-DSTSP_FPROBE_ALLEDGE=1"],
-                 "xgfence": ["-DSTSP_XG_FENCE=1"], "xgaos": ["-DSTSP_XG_SOA=0"],
-                 "ftag": ["-DSTSP_FUSED_TAGH=1"]}
+                 "xgfence": ["-DSTSP_XG_FENCE=1"], "xgaos": ["-DSTSP_XG_SOA=0"]}
 
 
 def lib_for(variant: str = "") -> str:

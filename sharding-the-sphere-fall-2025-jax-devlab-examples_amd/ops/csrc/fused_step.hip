@@ -55,11 +55,13 @@
 #ifndef STSP_XG_FENCE
 #define STSP_XG_FENCE 0
 #endif
-// Tagged in-launch hand-off (FArgs::hx, STSP_FUSED_HANDOFF=tag on the host):
-// compiled in only by the ftag variant, so the production epoch path carries
-// none of its code (profiles/r6_handoff: slower at B = 16, faster at B = 6)
+// Tagged in-launch hand-off (FArgs::hx; the host picks it for blocks of at
+// most 8 cells, ops/fused.py::handoff_mode: faster at B = 6, slower at B = 16,
+// profiles/r6_handoff).  Its block-uniform branches cost the epoch path
+// nothing measurable (same box: 11.7-12.2 us/step with or without them);
+// STSP_FUSED_TAGH=0 compiles it out.
 #ifndef STSP_FUSED_TAGH
-#define STSP_FUSED_TAGH 0
+#define STSP_FUSED_TAGH 1
 #endif
 
 namespace {
@@ -1266,7 +1268,7 @@ extern "C" int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stre
 }
 
 // Compile-time sizes of the fused kernel (host checks): ghost entries and corner faces per block.
-// 1 if this library carries the tagged in-launch hand-off (ftag variant)
+// 1 if this library carries the tagged in-launch hand-off
 extern "C" int stsp_fused_tagh(void) { return STSP_FUSED_TAGH; }
 
 extern "C" int stsp_fused_limits(int* gmax, int* cmax) {

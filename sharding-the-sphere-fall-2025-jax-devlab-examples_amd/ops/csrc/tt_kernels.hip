@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tt_common.h"
+
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -479,7 +481,7 @@ int lr_core(int k, const double* Ga, const double* Gb, double eps, int max_rank,
 template <typename T, int KP>
 __device__ __forceinline__ void chol_inv_wave(const T* __restrict__ G, int ldg, T* __restrict__ R,
                                               T* __restrict__ Ri, int ldr, int k, double shift_c, T tr,
-                                              int* __restrict__ info) {
+                                              int* __restrict__ info, int istride) {
   const int lane = threadIdx.x;
   // shift_c < 0: try the plain Cholesky first and shift (by |shift_c|) only
   // if a pivot fails (CholeskyQR passes 2 and 3: orthonormal to eps when the
@@ -497,7 +499,7 @@ __device__ __forceinline__ void chol_inv_wave(const T* __restrict__ G, int ldg, 
     fail = 0;
 #pragma unroll
     for (int j = 0; j < KP; ++j) {
-      T d = __shfl(g[j], j);
+      T d = tt::lane_bcast(g[j], j);
       if (!(d > T(0))) { if (!fail) fail = j + 1; d = T(1); }
       const T sq = sqrt(d);
       if (lane == j) g[j] = sq;
@@ -505,7 +507,7 @@ __device__ __forceinline__ void chol_inv_wave(const T* __restrict__ G, int ldg, 
       const T rt = g[j];
 #pragma unroll
       for (int i = j + 1; i < KP; ++i) {
-        const T rji = __shfl(g[j], i);             // R[j][i]: lane i's column
+        const T rji = tt::lane_bcast(g[j], i);     // R[j][i]: lane i's column
         if (i <= lane) g[i] -= rji * rt;
       }
     }
@@ -515,10 +517,10 @@ __device__ __forceinline__ void chol_inv_wave(const T* __restrict__ G, int ldg, 
   T ri[KP];
 #pragma unroll
   for (int i = KP - 1; i >= 0; --i) {
-    const T rii = __shfl(g[i], i);
+    const T rii = tt::lane_bcast(g[i], i);
     T sum = T(0);
 #pragma unroll
-    for (int l = i + 1; l < KP; ++l) sum += __shfl(g[i], l) * ri[l];
+    for (int l = i + 1; l < KP; ++l) sum += tt::lane_bcast(g[i], l) * ri[l];
     ri[i] = i == lane ? T(1) / rii : (i < lane ? -sum / rii : T(0));
   }
   if (lane < k) {
@@ -529,13 +531,13 @@ __device__ __forceinline__ void chol_inv_wave(const T* __restrict__ G, int ldg, 
         Ri[(long)i * ldr + lane] = ri[i];
       }
   }
-  if (lane == 0) info[blockIdx.x] = fail;
+  if (lane == 0) info[blockIdx.x * istride] = fail;
 }
 
 template <typename T>
 __global__ __launch_bounds__(64) void chol_inv_kernel(const T* __restrict__ G, int ldg, long sg, T* __restrict__ R,
                                                       T* __restrict__ Ri, int ldr, long sr, int k, double shift_c,
-                                                      int* __restrict__ info) {
+                                                      int* __restrict__ info, int istride) {
   const int b = blockIdx.x, t = threadIdx.x;
   G += b * sg;
   R += b * sr;
@@ -553,12 +555,12 @@ __global__ __launch_bounds__(64) void chol_inv_kernel(const T* __restrict__ G, i
         R[(long)i * ldr + t] = T(0);
         Ri[(long)i * ldr + t] = i == t ? T(1) : T(0);
       }
-    if (t == 0) info[b] = 0;
+    if (t == 0) info[b * istride] = 0;
     return;
   }
-  if (k <= 16) chol_inv_wave<T, 16>(G, ldg, R, Ri, ldr, k, shift_c, tr, info);
-  else if (k <= 32) chol_inv_wave<T, 32>(G, ldg, R, Ri, ldr, k, shift_c, tr, info);
-  else chol_inv_wave<T, 64>(G, ldg, R, Ri, ldr, k, shift_c, tr, info);
+  if (k <= 16) chol_inv_wave<T, 16>(G, ldg, R, Ri, ldr, k, shift_c, tr, info, istride);
+  else if (k <= 32) chol_inv_wave<T, 32>(G, ldg, R, Ri, ldr, k, shift_c, tr, info, istride);
+  else chol_inv_wave<T, 64>(G, ldg, R, Ri, ldr, k, shift_c, tr, info, istride);
 }
 
 
@@ -637,6 +639,11 @@ __global__ __launch_bounds__(256) void tt_core_kernel(const T* __restrict__ Rs, 
     if (tid == 0) s_tot = (sig[0] + sig[1]) + (sig[2] + sig[3]);   // fixed order: reproducible
   }
   __syncthreads();
+  // only rounding noise (below 1e-15 of ||C||) is left unrotated.  Skipping
+  // every column below 1 % of the truncation tolerance saved ~20 % of the
+  // sweeps on the six-panel SWE's fp64 cores but changed the rank of an fp32
+  // core (eps 1e-6: 3 vs the host's 7; tests/test_tt_kernels.py): a column
+  // small early in the sweeps can still gain weight from a large one
   const double tiny = 1e-30 * s_tot;
   // round-robin: m = k rounded up to even, position 0 fixed, the rest rotate;
   // pair p joins positions p and m - 1 - p (index k: the dummy of odd k)
@@ -659,12 +666,12 @@ __global__ __launch_bounds__(256) void tt_core_kernel(const T* __restrict__ Rs, 
             be += y * y;
             ga += x * y;
           }
-#pragma unroll
-          for (int o = 8; o >= 1; o >>= 1) {
-            al += __shfl_xor(al, o, 16);
-            be += __shfl_xor(be, o, 16);
-            ga += __shfl_xor(ga, o, 16);
-          }
+          // 16-lane sums through DPP; every lane of the wave runs them (the
+          // pair guard above is lane-group uniform and DPP needs no exec gaps
+          // inside a row)
+          al = tt::sum16(al);
+          be = tt::sum16(be);
+          ga = tt::sum16(ga);
           if (!(al <= tiny || be <= tiny || fabs(ga) <= 1e-15 * sqrt(al * be))) {
             const double ze = (be - al) / (2.0 * ga);
             const double t = (ze >= 0 ? 1.0 : -1.0) / (fabs(ze) + sqrt(1.0 + ze * ze));
@@ -751,18 +758,23 @@ int stsp_tt_gram(int dtype, const void* A, int lda, const void* B, int ldb, int 
 // G_b + shift_c trace(G_b) I = R_b^T R_b, Ri_b = R_b^-1 (k <= 64, row-major;
 // shift_c < 0: unshifted unless a pivot fails, then shifted by |shift_c|,
 // batch strides sg / sr in elements), info[b] = 0 or the failing pivot + 1.
-int stsp_tt_chol_inv(int dtype, const void* G, int ldg, long sg, void* R, void* Ri, int ldr, long sr, int k,
-                     int batch, double shift_c, int* info, hipStream_t stream) {
+static int chol_inv_launch(int dtype, const void* G, int ldg, long sg, void* R, void* Ri, int ldr, long sr, int k,
+                           int batch, double shift_c, int* info, int istride, hipStream_t stream) {
   if (k < 1 || k > 64 || batch < 1) return -1;
   if (dtype == 1)
     hipLaunchKernelGGL(chol_inv_kernel<double>, dim3(batch), dim3(64), 0, stream, (const double*)G, ldg, sg,
-                       (double*)R, (double*)Ri, ldr, sr, k, shift_c, info);
+                       (double*)R, (double*)Ri, ldr, sr, k, shift_c, info, istride);
   else if (dtype == 0)
     hipLaunchKernelGGL(chol_inv_kernel<float>, dim3(batch), dim3(64), 0, stream, (const float*)G, ldg, sg, (float*)R,
-                       (float*)Ri, ldr, sr, k, shift_c, info);
+                       (float*)Ri, ldr, sr, k, shift_c, info, istride);
   else
     return -4;
   return (int)hipGetLastError();
+}
+
+int stsp_tt_chol_inv(int dtype, const void* G, int ldg, long sg, void* R, void* Ri, int ldr, long sr, int k,
+                     int batch, double shift_c, int* info, hipStream_t stream) {
+  return chol_inv_launch(dtype, G, ldg, sg, R, Ri, ldr, sr, k, batch, shift_c, info, 1, stream);
 }
 
 // C[N][m] (ldc) = alpha * A X + beta * C,  A [N][k] (lda), X [k][m] (ldx), k, m <= 64.
@@ -897,30 +909,41 @@ size_t stsp_tt_step_workspace3(int N, int r, int nsub) {
 // stsp_tt_recompress on the device when k <= 32 (tt_core_kernel); 0: on the
 // host (jacobi_svd), for comparison.
 
-// CholeskyQR3 of one factor X [N][k] (row stride ldx) on the device (models/
-// tt.py::cholqr3): pass p = {MFMA Gram, shifted Cholesky + inverse, MFMA
-// product}; passes write s0, s1, s0 (row stride k), so Q ends in s0 and s1 may
-// alias X.  Rs: [pass][R, Ri] k x k, dinfo[pass]: pivot flags.
-static int cholqr3_dev(int dtype, const void* X, int ldx, int N, int k, void* s0, void* s1, void* part, void* G,
-                       char* Rs, int* dinfo, hipStream_t st) {
+// CholeskyQR3 of the two factors X[side] [N[side]][k] (row stride ldx[side])
+// side by side on the device (models/tt.py::cholqr3): per pass one MFMA Gram
+// per factor, ONE batched shifted Cholesky + inverse for both (two waves in
+// parallel: the single-wave latency chain is paid once per pass, not twice),
+// one MFMA product per factor.  Passes write s0, s1, s0 (row stride k), so Q
+// ends in s0[side] and s1[side] may alias X[side].  G: 2 k^2; Rs: [side][pass]
+// [R, Ri] k x k; dinfo[side * 3 + pass].  The shift uses the taller factor.
+static int cholqr3_pair(int dtype, const void* const X[2], const int ldx[2], const int N[2], int k,
+                        void* const s0[2], void* const s1[2], void* part, void* G, char* Rs, int* dinfo,
+                        hipStream_t st) {
   const size_t es = dtype == 1 ? 8 : 4;
+  const size_t kk = (size_t)k * k;
   // shift coefficient 11 (N k + k (k + 1)) u (models/tt.py::cholqr3_shift)
   const double u = dtype == 1 ? 1.1102230246251565e-16 : 5.960464477539063e-08;
-  const double shc = 11.0 * ((double)N * k + (double)k * (k + 1)) * u;
-  const int P = stsp_tt_gram_blocks(N);
-  const void* in = X;
-  int ldin = ldx;
-  void* outs[3] = {s0, s1, s0};
+  const int Nmax = N[0] > N[1] ? N[0] : N[1];
+  const double shc = 11.0 * ((double)Nmax * k + (double)k * (k + 1)) * u;
+  const void* in[2] = {X[0], X[1]};
+  int ldin[2] = {ldx[0], ldx[1]};
   int rc;
   for (int pass = 0; pass < 3; ++pass) {
-    char* R = Rs + es * (size_t)(pass * 2) * k * k;
-    char* Ri = R + es * (size_t)k * k;
-    if ((rc = stsp_tt_gram(dtype, in, ldin, in, ldin, N, k, k, part, P, G, k, 1.0, st))) return rc;
-    if ((rc = stsp_tt_chol_inv(dtype, G, k, 0, R, Ri, k, 0, k, 1, pass == 0 ? shc : -shc, dinfo + pass, st)))
+    for (int side = 0; side < 2; ++side)
+      if ((rc = stsp_tt_gram(dtype, in[side], ldin[side], in[side], ldin[side], N[side], k, k, part,
+                             stsp_tt_gram_blocks(N[side]), (char*)G + es * side * kk, k, 1.0, st)))
+        return rc;
+    char* R0 = Rs + es * (size_t)(pass * 2) * kk;          // side 0's R of this pass; side 1 at + 6 k^2
+    if ((rc = chol_inv_launch(dtype, G, k, (long)kk, R0, R0 + es * kk, k, (long)(6 * kk), k, 2,
+                              pass == 0 ? shc : -shc, dinfo + pass, 3, st)))
       return rc;
-    if ((rc = stsp_tt_mm(dtype, in, ldin, Ri, k, outs[pass], k, N, k, k, 1.0, 0.0, st))) return rc;
-    in = outs[pass];
-    ldin = k;
+    for (int side = 0; side < 2; ++side) {
+      void* out = pass == 1 ? s1[side] : s0[side];
+      const char* Ri = R0 + es * (size_t)side * 6 * kk + es * kk;
+      if ((rc = stsp_tt_mm(dtype, in[side], ldin[side], Ri, k, out, k, N[side], k, k, 1.0, 0.0, st))) return rc;
+      in[side] = out;
+      ldin[side] = k;
+    }
   }
   return 0;
 }
@@ -1061,14 +1084,11 @@ int stsp_tt_lr_step3(int dtype, const void* A, int lda, const void* B, int ldb, 
   // CholeskyQR3 per factor: scratch = the free buffer and the expansion output
   // itself (no longer read after pass 1's Gram + product)
   const void* src[2] = {srcA, srcB};
-  void* Q[2];
-  for (int side = 0; side < 2; ++side) {
-    if ((rc = cholqr3_dev(dtype, src[side], k, N, k, buf[cur][side], (void*)src[side], part, G,
-                          Rs + es * (size_t)side * 6 * k * k, dinfo + side * 3, st)))
-      return rc;
-    Q[side] = buf[cur][side];
-  }
-  const int Nq[2] = {N, N};
+  const int lds[2] = {k, k}, Nq[2] = {N, N};
+  void* const s0[2] = {buf[cur][0], buf[cur][1]};
+  void* const s1[2] = {(void*)srcA, (void*)srcB};
+  if ((rc = cholqr3_pair(dtype, src, lds, Nq, k, s0, s1, part, G, Rs, dinfo, st))) return rc;
+  void* Q[2] = {s0[0], s0[1]};
   return core_and_products(dtype, Q, Nq, k, eps, max_rank, Rs, dinfo, dX, hbuf, Aout, ldo, Bout, ldo, st);
 }
 
@@ -1082,7 +1102,7 @@ int stsp_tt_lr_step3(int dtype, const void* A, int lda, const void* B, int ldb, 
 // workspace elements; hbuf: 8 k^2 + 8 doubles (pinned).  Returns rn or < 0.
 size_t stsp_tt_recompress_workspace(int NA, int NB, int k) {
   const int kp = (k + 15) / 16 * 16;
-  return (size_t)2 * ((size_t)NA + NB) * k + (size_t)k * k +
+  return (size_t)2 * ((size_t)NA + NB) * k + (size_t)2 * k * k +
          (size_t)stsp_tt_gram_blocks(NA > NB ? NA : NB) * kp * kp + (size_t)2 * k * k + (size_t)12 * k * k + 16;
 }
 
@@ -1097,16 +1117,17 @@ int stsp_tt_recompress(int dtype, const void* A, int lda, int NA, const void* B,
   void* sA[2] = {w, w + es * (size_t)NA * k};
   void* sB[2] = {w + es * 2 * (size_t)NA * k, w + es * (2 * (size_t)NA * k + (size_t)NB * k)};
   void* G = w + es * 2 * ((size_t)NA + NB) * k;
-  void* part = (char*)G + es * (size_t)k * k;
+  void* part = (char*)G + es * (size_t)2 * k * k;
   void* dX = (char*)part + es * (size_t)stsp_tt_gram_blocks(NA > NB ? NA : NB) * kp * kp;
   char* Rs = (char*)dX + es * (size_t)2 * k * k;
   int* dinfo = (int*)(Rs + es * (size_t)12 * k * k);
   int rc;
-  if ((rc = cholqr3_dev(dtype, A, lda, NA, k, sA[0], sA[1], part, G, Rs, dinfo, st))) return rc;
-  if ((rc = cholqr3_dev(dtype, B, ldb, NB, k, sB[0], sB[1], part, G, Rs + es * (size_t)6 * k * k, dinfo + 3, st)))
-    return rc;
+  const void* X[2] = {A, B};
+  const int ldx[2] = {lda, ldb}, Nq[2] = {NA, NB};
+  void* const s0[2] = {sA[0], sB[0]};
+  void* const s1[2] = {sA[1], sB[1]};
+  if ((rc = cholqr3_pair(dtype, X, ldx, Nq, k, s0, s1, part, G, Rs, dinfo, st))) return rc;
   void* Q[2] = {sA[0], sB[0]};
-  const int Nq[2] = {NA, NB};
   return core_and_products(dtype, Q, Nq, k, eps, max_rank, Rs, dinfo, dX, hbuf, Aout, ldao, Bout, ldbo, st);
 }
 

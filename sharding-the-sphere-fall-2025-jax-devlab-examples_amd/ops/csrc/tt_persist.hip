@@ -32,6 +32,8 @@
 
 #include <cstdint>
 
+#include "tt_common.h"
+
 namespace {
 
 // 512 threads (8 waves, 2 per SIMD): a 256-VGPR budget, so the k x k
@@ -255,7 +257,7 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
           fail = 0;
 #pragma unroll
           for (int j = 0; j < TP_KP; ++j) {
-            double d = __shfl(g[j], j);
+            double d = tt::lane_bcast(g[j], j);
             if (!(d > 0.0)) { if (!fail) fail = j + 1; d = 1.0; }
             const double sq = sqrt(d);
             if (lane == j) g[j] = sq;
@@ -263,7 +265,7 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
             const double rt = g[j];
 #pragma unroll
             for (int i = j + 1; i < TP_KP; ++i) {
-              const double rji = __shfl(g[j], i);             // R[j][i]: lane i's column
+              const double rji = tt::lane_bcast(g[j], i);     // R[j][i]: lane i's column
               if (i <= lane) g[i] -= rji * rt;
             }
           }
@@ -272,10 +274,10 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
         double ri[TP_KP];
 #pragma unroll
         for (int i = TP_KP - 1; i >= 0; --i) {
-          const double rii = __shfl(g[i], i);
+          const double rii = tt::lane_bcast(g[i], i);
           double sum = 0.0;
 #pragma unroll
-          for (int l = i + 1; l < TP_KP; ++l) sum += __shfl(g[i], l) * ri[l];
+          for (int l = i + 1; l < TP_KP; ++l) sum += tt::lane_bcast(g[i], l) * ri[l];
           ri[i] = i == lane ? 1.0 / rii : (i < lane ? -sum / rii : 0.0);
         }
         if (lane < k) {
@@ -373,12 +375,9 @@ __global__ __launch_bounds__(TP_T) void tt_persist_kernel(TPArgs a) {
                   be += y * y;
                   ga += x * y;
                 }
-#pragma unroll
-                for (int o = 4; o >= 1; o >>= 1) {
-                  al += __shfl_xor(al, o, 8);
-                  be += __shfl_xor(be, o, 8);
-                  ga += __shfl_xor(ga, o, 8);
-                }
+                al = tt::sum8(al);        // 8-lane sums through DPP
+                be = tt::sum8(be);
+                ga = tt::sum8(ga);
                 if (!(al <= tiny || be <= tiny || fabs(ga) <= 1e-15 * sqrt(al * be))) {
                   const double ze = (be - al) / (2.0 * ga);
                   const double t = (ze >= 0 ? 1.0 : -1.0) / (fabs(ze) + sqrt(1.0 + ze * ze));

@@ -1238,9 +1238,11 @@ class FusedKernel:
         # tagged in-launch hand-off (one rank): [2 slots][4 G words][S] u64,
         # zero tags; lives with the epoch array, whose counts only grow, so a
         # tag a reader waits for was written in the same launch
-        self.handoff = handoff_mode() if X is None else "epoch"
+        self.handoff = handoff_mode(B) if X is None else "epoch"
         if self.handoff == "tag" and not int(self.lib.stsp_fused_tagh()):
-            raise RuntimeError("STSP_FUSED_HANDOFF=tag needs the ftag library (STSP_VARIANT=ftag)")
+            if os.environ.get("STSP_FUSED_HANDOFF") == "tag":
+                raise RuntimeError("STSP_FUSED_HANDOFF=tag needs a library built with STSP_FUSED_TAGH=1")
+            self.handoff = "epoch"
         if self.handoff == "tag":
             words = 4 * (torch.tensor([], dtype=e.dtype).element_size() // 4)
             self.tens["hx"] = torch.zeros(2 * words * e.plan.S, dtype=torch.int64, device=dev)
@@ -1586,18 +1588,23 @@ def ctypes_limits(L) -> Tuple[int, int]:
 # Several ranks: remote window cells through the direct xGMI ring
 # ---------------------------------------------------------------------------
 
-def handoff_mode() -> str:
-    """In-launch hand-off of a one-rank multi-step fused launch:
-    ``STSP_FUSED_HANDOFF`` = "tag" (tagged granules, the data is the flag;
-    needs the ``ftag`` library, STSP_VARIANT=ftag) or "epoch" (write-through
-    state, drained per-block step counter, producer poll; profiles/r6_handoff)."""
-    m = os.environ.get("STSP_FUSED_HANDOFF", HANDOFF_DEFAULT)
-    if m not in ("tag", "epoch"):
-        raise ValueError(f"STSP_FUSED_HANDOFF must be 'tag' or 'epoch', got {m!r}")
+def handoff_mode(B: int) -> str:
+    """In-launch hand-off of a one-rank multi-step fused launch with B x B
+    blocks: "tag" (tagged granules, the data is the flag) or "epoch"
+    (write-through state, drained per-block step counter, producer poll).
+    ``STSP_FUSED_HANDOFF`` = tag / epoch / auto (default): auto takes the
+    tagged form for B <= 8, where it measured 2-3 % faster (C36 B = 6), and
+    the epoch form above, where the tagged form's doubled hand-off bytes cost
+    2-5 % (C96 B = 16; profiles/r6_handoff)."""
+    m = os.environ.get("STSP_FUSED_HANDOFF", "auto")
+    if m not in ("tag", "epoch", "auto"):
+        raise ValueError(f"STSP_FUSED_HANDOFF must be 'tag', 'epoch' or 'auto', got {m!r}")
+    if m == "auto":
+        return "tag" if B <= HANDOFF_TAG_MAX_B else "epoch"
     return m
 
 
-HANDOFF_DEFAULT = "epoch"
+HANDOFF_TAG_MAX_B = 8
 
 
 XG_SLOT_BITS = 24

@@ -9,14 +9,14 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/${TAG:-r6_handoff}
 mkdir -p $OUT
 cd $ROOT
-STSP_VARIANT=ftag STSP_FUSED_HANDOFF=tag timeout -k 10 400 python -u -m pytest tests/test_fused.py tests/test_long_run.py -m gpu -x -q \
+STSP_FUSED_HANDOFF=tag timeout -k 10 400 python -u -m pytest tests/test_fused.py tests/test_long_run.py -m gpu -x -q \
   --timeout 300 --timeout-method thread > $OUT/pytest_tag.log 2>&1 || { tail -30 $OUT/pytest_tag.log; exit 1; }
 tail -2 $OUT/pytest_tag.log
 for rep in 1 2 3; do
   for m in epoch tag; do
-    V=$([ $m = tag ] && echo ftag || echo ""); STSP_VARIANT=$V STSP_FUSED_HANDOFF=$m timeout -k 10 120 python -u tools/fused_probe.py --N 96 --t 2 > $OUT/probe_C96_${m}_$rep.json 2> $OUT/probe_C96_${m}_$rep.err || exit $?
-    STSP_VARIANT=$V STSP_FUSED_HANDOFF=$m timeout -k 10 120 python -u tools/fused_probe.py --N 36 --t 1 --B 6 > $OUT/probe_C36B6_${m}_$rep.json 2> $OUT/probe_C36B6_${m}_$rep.err || exit $?
-    STSP_VARIANT=$V STSP_FUSED_HANDOFF=$m timeout -k 10 180 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_${m}_$rep.json 2> $OUT/bench_${m}_$rep.err || exit $?
+    STSP_FUSED_HANDOFF=$m timeout -k 10 120 python -u tools/fused_probe.py --N 96 --t 2 > $OUT/probe_C96_${m}_$rep.json 2> $OUT/probe_C96_${m}_$rep.err || exit $?
+    STSP_FUSED_HANDOFF=$m timeout -k 10 120 python -u tools/fused_probe.py --N 36 --t 1 --B 6 > $OUT/probe_C36B6_${m}_$rep.json 2> $OUT/probe_C36B6_${m}_$rep.err || exit $?
+    STSP_FUSED_HANDOFF=$m timeout -k 10 180 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_${m}_$rep.json 2> $OUT/bench_${m}_$rep.err || exit $?
     python - $OUT $m $rep <<'PY'
 import json, sys
 out, m, rep = sys.argv[1:]
