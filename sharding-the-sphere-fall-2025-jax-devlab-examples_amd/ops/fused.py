@@ -1239,6 +1239,10 @@ class FusedKernel:
         # zero tags; lives with the epoch array, whose counts only grow, so a
         # tag a reader waits for was written in the same launch
         self.handoff = handoff_mode(B) if X is None else "epoch"
+        if self.handoff == "tag" and not read_relation_symmetric(P):
+            if os.environ.get("STSP_FUSED_HANDOFF") == "tag":
+                raise RuntimeError("tagged hand-off needs a symmetric block read relation")
+            self.handoff = "epoch"
         if self.handoff == "tag" and not int(self.lib.stsp_fused_tagh()):
             if os.environ.get("STSP_FUSED_HANDOFF") == "tag":
                 raise RuntimeError("STSP_FUSED_HANDOFF=tag needs a library built with STSP_FUSED_TAGH=1")
@@ -1550,11 +1554,20 @@ def corner_tables(P: "FusedPlan", code: np.ndarray, gpair: np.ndarray) -> Tuple[
     return ct, cg
 
 
-def producer_table(P: "FusedPlan") -> np.ndarray:
+def read_relation_symmetric(P: "FusedPlan") -> bool:
+    """True if every block whose window reads a cell of block c is itself read
+    by c (in-rank producers).  The tagged hand-off waits only for the cells a
+    block reads; with a symmetric relation that also keeps every producer at
+    most one step ahead of its readers, which its two slots need."""
+    return producer_table(P, symmetric=False)[1]
+
+
+def producer_table(P: "FusedPlan", symmetric: bool = True):
     """[nb, PM] int32: the blocks of this rank whose cells each block's window
     loads (its producers for a step inside a multi-step launch), made
     symmetric so the same wait also guarantees that every reader of a block's
-    previous state is done before the block overwrites it; -1 padded."""
+    previous state is done before the block overwrites it; -1 padded.
+    symmetric=False: (None, whether the read relation already is symmetric)."""
     L = P.layout
     pos = {int(t): k for k, t in enumerate(P.tiles)}
     sets = [set() for _ in range(P.nb)]
@@ -1567,6 +1580,8 @@ def producer_table(P: "FusedPlan") -> np.ndarray:
         li = np.array([pos[int(t)] for t in tid])
         blk = (li * P.nby + j // P.B) * P.nbx + i // P.B
         sets[b].update(int(x) for x in np.unique(blk) if int(x) != b)
+    if not symmetric:
+        return None, all(b in sets[c] for b in range(P.nb) for c in sets[b])
     for b in range(P.nb):
         for c in list(sets[b]):
             sets[c].add(b)

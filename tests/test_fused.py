@@ -560,3 +560,15 @@ def test_fused_loopback_kernel_equals_one_rank(N, t):
     fb.check()
     assert torch.equal(a.tiles_view(), b.tiles_view())
     fb.close()
+
+
+@pytest.mark.parametrize("N,t,B", [(96, 2, 16), (48, 1, 8), (36, 1, 6), (48, 2, 8), (180, 3, 20)])
+def test_block_read_relation_is_symmetric(N, t, B):
+    """The tagged in-launch hand-off (two slots, no producer poll) needs every
+    reader of a block to be read by it as well, so no producer runs two steps
+    ahead of a reader; FusedKernel falls back to the epoch hand-off otherwise."""
+    from stsphere.models.geometry import CubedSphereGrid
+    from stsphere.ops.fused import FusedPlan, read_relation_symmetric
+    P = FusedPlan(TileLayout(N, t, 1, ng=2), 0, CubedSphereGrid(N), B=B, ns=3)
+    P.src[~P.need[:, 0]] = -1
+    assert read_relation_symmetric(P)
