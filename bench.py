@@ -393,9 +393,16 @@ def main():
             runner.prepare(a.steps)
         step = runner.run if runner is not None else eng.step
         step(a.warmup)
+        # one rank: no sync here.  The host work between warm-up and timing
+        # (phase marks, counters) overlaps the last warm-up launches, and the
+        # synchronize in front of the timed region waits for them, so the GPU
+        # idles ~10 us before the timed launch instead of ~50 (a GPU idle for
+        # tens of us starts the launch cold: ~0.5 us/step slower over 20
+        # steps, profiles/r5_fused/ramp_probe.json).  The exchange check is the
+        # post-timing one (runner.check() below).
+        if world == 1 and os.environ.get("STSP_BENCH_WARM_SYNC") != "1":   # =1: the A/B of round 6
+            return True
         sync()
-        # one rank: the exchange check is the post-timing one (runner.check() below);
-        # a device read here only lengthens the GPU's idle gap before the timed region
         if hasattr(runner, "check") and world > 1:
             try:
                 runner.check()

@@ -201,6 +201,7 @@ struct FArgs {
   // window cell's granules until every tag matches.  The data is the flag: no
   // drain, no barrier, no epoch store and no separate poll round trip.
   unsigned long long* hx;
+  const signed char* pidx;   // [nb][W*W] per-cell producer index (FusedDesc::pidx), or null
 };
 
 // The launch's first failure, for the host's message (err[0..5]): the code
@@ -373,6 +374,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   const int nsteps = MULTI ? a.nsteps : 1;
   const bool epoch_on = XG || MULTI;
   const bool tagh = STSP_FUSED_TAGH && MULTI && !XG && a.hx != nullptr;     // block-uniform
+  const bool pcell = MULTI && !XG && !tagh && a.pidx != nullptr;            // block-uniform
   if (epoch_on) xe = a.epoch[bid];
   const int n = a.n;
   // a window cell's panel and panel-local index (cube topology) and its
@@ -812,7 +814,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     enter_cell();
   }
   __syncthreads();
-  if (wait && !tagh && tid < 64) {
+  if (wait && !tagh && !pcell && tid < 64) {
     // wait for the producers' previous step (wave 0 polls) ...
     const int p = tid < a.PM ? a.prod[(long)bid * a.PM + tid] : -1;
     const int pa = p >= 0 ? p : bid;
@@ -838,12 +840,15 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   } else {
     // ... while the other waves compute the inner stage-1 faces (tagged
     // hand-off: every wave; the ring loads below are the wait)
-    const bool w0 = wait && !tagh;
+    const bool w0 = wait && !tagh && !pcell;
     const int t0 = w0 ? tid - 64 : tid, dt_ = w0 ? NT - 64 : NT;
     for (int t = t0; t < NI; t += dt_) inner_face(t);
   }
   FSTAMP(1);
-  __syncthreads();
+  // the ring loads below write only ring cells of the window and the threads'
+  // own s_x slots, the inner faces read only the block's cells: with no wave
+  // polling for the block (tagged hand-off, per-cell polls) no barrier between
+  if (!(wait && (tagh || pcell))) __syncthreads();
   if (wait) {
     // this step's ring (the own cells' new state is still in Q), tail cells
     // issued first
@@ -859,6 +864,30 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         enter_cell();
       }
     } else {
+      if (pcell) {
+        // this thread's window cells: wait for each one's producer to have
+        // completed the previous step (a wave's lanes share a few producers)
+        auto poll_prod = [&](int cu, int cv) {
+          const int k = a.pidx[(long)bid * W * W + cv * W + cu];
+          if (k < 0) return;
+          const int p = a.prod[(long)bid * a.PM + k];
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          for (;;) {
+            const int e = __hip_atomic_load(a.epoch + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (e >= xe) break;
+            if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+            if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
+              fused_fail(a.err, 2u, bid, xe, p, e);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        };
+        if (tid >= B * B && owner) poll_prod(u, v);
+#pragma unroll
+        for (int k = 0; k < TPT; ++k)
+          if (tl_wi[k] >= 0) poll_prod(tl_wi[k] % WS, tl_wi[k] / WS);
+      }
       tail_load(buf[it & 1], xe, tq);
       if (tid >= B * B) {
         load_state(buf[it & 1], xe);
@@ -1175,6 +1204,7 @@ int launch_fused(const FusedDesc* d, hipStream_t s) {
   a.sched = (const unsigned*)d->sched;
   a.nrmf = (const T*)d->nrmf;
   a.hx = (unsigned long long*)d->hx;
+  a.pidx = d->pidx;
   if (!a.sched || !a.nrmf) return -4;
   if (a.nsteps > 1 && (!a.prod || a.PM <= 0 || a.PM > 64 || !d->epoch || !d->err)) return -7;
   a.mdiv_n = magic_div((unsigned)d->n, (unsigned long long)d->N + 1);

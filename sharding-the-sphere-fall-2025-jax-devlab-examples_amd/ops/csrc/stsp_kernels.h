@@ -168,6 +168,10 @@ typedef struct FusedDesc {
   // tagged in-launch hand-off of a one-rank multi-step launch, [2][4 G][S] u64
   // zero-initialised and kept with the epoch array; null = epoch hand-off
   void* hx;
+  // per-cell producer polls of a one-rank epoch hand-off: [nb][W*W] int8
+  // index into prod[b] of the producer of each window cell (-1: none); null =
+  // wave 0 polls every producer before a barrier
+  const signed char* pidx;
 } FusedDesc;
 int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stream);
 int stsp_fused_limits(int* gmax, int* cmax);

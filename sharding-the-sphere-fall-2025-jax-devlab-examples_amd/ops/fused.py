@@ -1251,7 +1251,15 @@ class FusedKernel:
             words = 4 * (torch.tensor([], dtype=e.dtype).element_size() // 4)
             self.tens["hx"] = torch.zeros(2 * words * e.plan.S, dtype=torch.int64, device=dev)
         self.tens["err"] = torch.zeros(8, dtype=torch.int32, device=dev)   # code, block, step, what, seen
-        self.tens["prod"] = torch.as_tensor(producer_table(P), dtype=torch.int32, device=dev).contiguous()
+        prod = producer_table(P)
+        self.tens["prod"] = torch.as_tensor(prod, dtype=torch.int32, device=dev).contiguous()
+        # per-cell producer polls (epoch hand-off, one rank): every ring thread
+        # waits for the producer of its own window cell, then loads it, instead
+        # of wave 0 polling every producer before a barrier (profiles/r6_handoff)
+        self.poll = poll_mode() if (X is None and self.handoff == "epoch" and read_relation_symmetric(P)) \
+            else "block"
+        if self.poll == "cell":
+            self.tens["pidx"] = torch.as_tensor(cell_producer_index(P, prod), device=dev).contiguous()
         # face passes per wave, balanced over the SIMDs (pass_schedule)
         edge_b = np.array([any(int(x) > 0 for x in np.unique(P.reg[b])) for b in range(nb)])
         sched = pass_schedule(B, np.asarray(P.ccnt), edge_b, G)
@@ -1335,6 +1343,7 @@ class FusedKernel:
         d.sched = p(tn["sched"])
         d.nrmf = p(tn["nrmf"])
         d.hx = p(tn["hx"]) if self.handoff == "tag" else 0
+        d.pidx = p(tn["pidx"]) if self.poll == "cell" else 0
         if self.mem is not None:
             d.xg = 1
             d.ring = self.ring
@@ -1552,6 +1561,40 @@ def corner_tables(P: "FusedPlan", code: np.ndarray, gpair: np.ndarray) -> Tuple[
             ct[b, j, 10], ct[b, j, 11], ct[b, j, 12] = fc, fd, flags
             cg[b, j, :4] = P.cgeo[b, j]
     return ct, cg
+
+
+def poll_mode() -> str:
+    """``STSP_FUSED_POLL`` = block (wave 0 polls every producer of the block,
+    then a barrier) or cell (each ring thread polls its own cell's producer
+    and loads at once); epoch hand-off on one rank only."""
+    m = os.environ.get("STSP_FUSED_POLL", POLL_DEFAULT)
+    if m not in ("block", "cell"):
+        raise ValueError(f"STSP_FUSED_POLL must be 'block' or 'cell', got {m!r}")
+    return m
+
+
+POLL_DEFAULT = "block"
+
+
+def cell_producer_index(P: "FusedPlan", prod: np.ndarray) -> np.ndarray:
+    """[nb, W*W] int8 (window order v W + u): the index into prod[b] of the
+    block that produces window cell (u, v) of block b, -1 for the block's own
+    cells and cells it does not load."""
+    L = P.layout
+    pos = {int(t): k for k, t in enumerate(P.tiles)}
+    out = np.full(P.src.shape, -1, dtype=np.int8)
+    for b in range(P.nb):
+        m = np.nonzero(P.src[b] >= 0)[0]
+        if m.size == 0:
+            continue
+        tid, i, j = L.locate(P.gid[b][m])
+        li = np.array([pos[int(t)] for t in tid])
+        blk = (li * P.nby + j // P.B) * P.nbx + i // P.B
+        where = {int(c): k for k, c in enumerate(prod[b]) if c >= 0}
+        for idx, c in zip(m, blk):
+            if int(c) != b:
+                out[b, idx] = where[int(c)]
+    return out
 
 
 def read_relation_symmetric(P: "FusedPlan") -> bool:

@@ -68,7 +68,7 @@ class FusedDesc(ctypes.Structure):
         ("local_src", ctypes.c_int), ("links", ctypes.c_int * 6),
         ("nsteps", ctypes.c_int), ("prod", ctypes.c_void_p), ("PM", ctypes.c_int),
         ("cpush", ctypes.c_void_p), ("sched", ctypes.c_void_p), ("nrmf", ctypes.c_void_p),
-        ("hx", ctypes.c_void_p),
+        ("hx", ctypes.c_void_p), ("pidx", ctypes.c_void_p),
     ]
 
 
