@@ -393,16 +393,13 @@ def main():
             runner.prepare(a.steps)
         step = runner.run if runner is not None else eng.step
         step(a.warmup)
-        # one rank: no sync here.  The host work between warm-up and timing
-        # (phase marks, counters) overlaps the last warm-up launches, and the
-        # synchronize in front of the timed region waits for them, so the GPU
-        # idles ~10 us before the timed launch instead of ~50 (a GPU idle for
-        # tens of us starts the launch cold: ~0.5 us/step slower over 20
-        # steps, profiles/r5_fused/ramp_probe.json).  The exchange check is the
-        # post-timing one (runner.check() below).
-        if world == 1 and os.environ.get("STSP_BENCH_WARM_SYNC") != "1":   # =1: the A/B of round 6
-            return True
         sync()
+        # one rank: the exchange check is the post-timing one (runner.check() below);
+        # a device read here only lengthens the GPU's idle gap before the timed region.
+        # (Round 6 also tried skipping this sync so the host work before the timed
+        # region overlaps the last warm-up launches: the GPU idled 26 instead of 53 us
+        # before the timed launch and the 20-step bench did not change, 13.17-13.60 vs
+        # 13.11-13.36 us/step; profiles/r6_handoff/warm_gap.)
         if hasattr(runner, "check") and world > 1:
             try:
                 runner.check()
