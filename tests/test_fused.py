@@ -572,3 +572,31 @@ def test_block_read_relation_is_symmetric(N, t, B):
     P = FusedPlan(TileLayout(N, t, 1, ng=2), 0, CubedSphereGrid(N), B=B, ns=3)
     P.src[~P.need[:, 0]] = -1
     assert read_relation_symmetric(P)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("handoff,poll", [("tag", "block"), ("epoch", "cell"), ("epoch", "block")])
+@pytest.mark.parametrize("N,t", [(96, 2), (48, 1)])
+def test_fused_handoff_forms_equal_single_steps(monkeypatch, handoff, poll, N, t):
+    """Every in-launch hand-off form (tagged granules, per-cell producer polls,
+    the default block poll), forced on for both block sizes (B = 16 and 8):
+    back-to-back multi-step launches, with single steps in between (the epoch
+    count pauses), bitwise equal to one launch per step."""
+    from stsphere.ops.fused import FusedKernel
+    monkeypatch.setenv("STSP_FUSED_HANDOFF", handoff)
+    monkeypatch.setenv("STSP_FUSED_POLL", poll)
+    _, a = _gpu_pair(N, t)
+    _, b = _gpu_pair(N, t)
+    b.dt = a.dt
+    FusedKernel(a).step(23)
+    fk = FusedKernel(b)
+    assert fk.handoff == handoff and fk.poll == (poll if handoff == "epoch" else "block")
+    fk.launch(0, nsteps=8)
+    fk.step(1)
+    fk.step(1)
+    fk.launch(0, nsteps=6)
+    fk.step(1)
+    fk.launch(0, nsteps=6)
+    torch.cuda.synchronize()
+    fk.check()
+    assert torch.equal(a.pool[0], b.pool[0])
