@@ -373,7 +373,8 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   int xe = 0;                                            // steps this block has completed
   const int nsteps = MULTI ? a.nsteps : 1;
   const bool epoch_on = XG || MULTI;
-  const bool tagh = STSP_FUSED_TAGH && MULTI && !XG && a.hx != nullptr;     // block-uniform
+  // (several ranks: the in-rank cells by tags, another rank's from the xGMI ring)
+  const bool tagh = STSP_FUSED_TAGH && MULTI && a.hx != nullptr;            // block-uniform
   const bool pcell = MULTI && !XG && !tagh && a.pidx != nullptr;            // block-uniform
   if (epoch_on) xe = a.epoch[bid];
   const int n = a.n;
@@ -662,10 +663,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     for (int k = 0; k < TPT; ++k) {
       if (tl_wi[k] >= 0) {
         if (tl_src[k] >= 0) load_tagged(tl_src[k], tq[k], xe_);
-        else {
-#pragma unroll
-          for (int f = 0; f < 4; ++f) tq[k][f] = T(0);
-        }
+        else load_state_of(tl_src[k], tq[k], nullptr, xe_);   // another rank's cell (ring) or none
       }
     }
   };
@@ -857,10 +855,7 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
       tail_load_tagged(xe, tq);
       if (tid >= B * B) {
         if (src >= 0) load_tagged(src, Q, xe);
-        else {
-#pragma unroll
-          for (int f = 0; f < 4; ++f) Q[f] = T(0);
-        }
+        else load_state_of(src, Q, nullptr, xe);             // another rank's cell (ring) or none
         enter_cell();
       }
     } else {

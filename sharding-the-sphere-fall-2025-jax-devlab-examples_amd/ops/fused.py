@@ -1238,7 +1238,7 @@ class FusedKernel:
         # tagged in-launch hand-off (one rank): [2 slots][4 G words][S] u64,
         # zero tags; lives with the epoch array, whose counts only grow, so a
         # tag a reader waits for was written in the same launch
-        self.handoff = handoff_mode(B) if X is None else "epoch"
+        self.handoff = handoff_mode(B)
         if self.handoff == "tag" and not read_relation_symmetric(P):
             if os.environ.get("STSP_FUSED_HANDOFF") == "tag":
                 raise RuntimeError("tagged hand-off needs a symmetric block read relation")

@@ -539,12 +539,15 @@ def test_fused_loopback_plan_equals_one_rank_cpu(N, t, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("handoff", ["auto", "tag", "epoch"])
 @pytest.mark.parametrize("N,t", [(32, 2), (96, 2), (36, 1)])
-def test_fused_loopback_kernel_equals_one_rank(N, t):
+def test_fused_loopback_kernel_equals_one_rank(monkeypatch, N, t, handoff):
     """The gfx950 fused kernel on a loopback layout (the xGMI ring protocol
     through the rank's own ring, tagged granules every step, one and several
-    steps per launch) equals the plain one-rank fused step bit for bit."""
+    steps per launch; the in-rank cells by either in-launch hand-off) equals
+    the plain one-rank fused step bit for bit."""
     from stsphere.ops.fused import FusedKernel
+    monkeypatch.setenv("STSP_FUSED_HANDOFF", handoff)
     grid = CubedSphereGrid(N)
     _, a = _gpu_pair(N, t)
     Llb = TileLayout(N, t, 1, ng=2, loopback=True)
