@@ -1238,7 +1238,7 @@ class FusedKernel:
         # tagged in-launch hand-off (one rank): [2 slots][4 G words][S] u64,
         # zero tags; lives with the epoch array, whose counts only grow, so a
         # tag a reader waits for was written in the same launch
-        self.handoff = handoff_mode(B)
+        self.handoff = handoff_mode(B, multi_rank=X is not None)
         if self.handoff == "tag" and not read_relation_symmetric(P):
             if os.environ.get("STSP_FUSED_HANDOFF") == "tag":
                 raise RuntimeError("tagged hand-off needs a symmetric block read relation")
@@ -1646,19 +1646,20 @@ def ctypes_limits(L) -> Tuple[int, int]:
 # Several ranks: remote window cells through the direct xGMI ring
 # ---------------------------------------------------------------------------
 
-def handoff_mode(B: int) -> str:
-    """In-launch hand-off of a one-rank multi-step fused launch with B x B
-    blocks: "tag" (tagged granules, the data is the flag) or "epoch"
-    (write-through state, drained per-block step counter, producer poll).
-    ``STSP_FUSED_HANDOFF`` = tag / epoch / auto (default): auto takes the
-    tagged form for B <= 8, where it measured 2-3 % faster (C36 B = 6), and
-    the epoch form above, where the tagged form's doubled hand-off bytes cost
-    2-5 % (C96 B = 16; profiles/r6_handoff)."""
+def handoff_mode(B: int, multi_rank: bool = False) -> str:
+    """In-launch hand-off of the in-rank cells of a multi-step fused launch
+    with B x B blocks: "tag" (tagged granules, the data is the flag) or
+    "epoch" (write-through state, drained per-block step counter, producer
+    poll).  ``STSP_FUSED_HANDOFF`` = tag / epoch / auto (default).  auto:
+    with other ranks' cells through the xGMI ring, tag at every block size
+    (loopback proxies 3-11 % faster for B = 6 .. 16); on one rank, tag for
+    B <= 8 (2-3 % faster at B = 6) and epoch above, where the tagged form's
+    doubled hand-off bytes cost 2-5 % (C96 B = 16; profiles/r6_handoff)."""
     m = os.environ.get("STSP_FUSED_HANDOFF", "auto")
     if m not in ("tag", "epoch", "auto"):
         raise ValueError(f"STSP_FUSED_HANDOFF must be 'tag', 'epoch' or 'auto', got {m!r}")
     if m == "auto":
-        return "tag" if B <= HANDOFF_TAG_MAX_B else "epoch"
+        return "tag" if (multi_rank or B <= HANDOFF_TAG_MAX_B) else "epoch"
     return m
 
 
