@@ -194,10 +194,10 @@ struct FArgs {
   const unsigned* sched;  // [nb][3 stages][17]: per wave (16) bit p = the wave runs face pass p (faces 64 p ..
                           // 64 p + 63); word 16 bit p = pass p holds a face next to a panel-edge line
   const T* nrmf;          // [nb][3][NFL] per-face normals of panel-edge blocks (PFN builds)
-  // tagged in-launch hand-off (one rank, several steps per launch; null = the
-  // epoch hand-off): [2 slots][4 G words][S] u64, word-major.  At the end of
-  // step e every block stores its cells as 4 G tagged granules {tag = e + 2,
-  // 32-bit payload} into slot (e + 1) & 1; a reader of step e + 1 re-reads its
+  // tagged in-launch hand-off (several steps per launch; null = the epoch
+  // hand-off): [2 slots][HX<T>::W words][S] u64, word-major.  At the end of
+  // step e every block stores each of its cells as HX<T>::W tagged granules
+  // (tag e + 2) into slot (e + 1) & 1; a reader of step e + 1 re-reads its
   // window cell's granules until every tag matches.  The data is the flag: no
   // drain, no barrier, no epoch store and no separate poll round trip.
   unsigned long long* hx;
@@ -277,6 +277,53 @@ __device__ __forceinline__ void to_global(int fr, T xi, T xj, T xn, T& o0, T& o1
   o1 = ai == 1 ? xi : (aj == 1 ? xj : xn);
   o2 = ai == 2 ? xi : (aj == 2 ? xj : xn);
 }
+
+// A cell of the tagged in-launch hand-off (FArgs::hx): its 4 field values in
+// HX<T>::W 64-bit granules, each {tag, payload} and single-copy atomic.  fp64:
+// 5 granules of a 12-bit tag and 52 payload bits (the 256 value bits in 5 x 52
+// = 260), against 8 granules of a 32-bit tag and 32 payload bits; fp32: 4
+// granules of a 32-bit tag and one value.  12 tag bits suffice: a slot holds
+// this step's value (tag want) or the value two steps older (want - 2 mod
+// 4096), never anything else (profiles/r6_handoff).
+template <typename T> struct HX;
+template <> struct HX<double> {
+  static constexpr int W = 5;
+  static constexpr unsigned long long M52 = (1ull << 52) - 1;
+  __device__ static void pack(const double (&q)[4], unsigned tag, unsigned long long (&g)[5]) {
+    const unsigned long long u0 = __builtin_bit_cast(unsigned long long, q[0]);
+    const unsigned long long u1 = __builtin_bit_cast(unsigned long long, q[1]);
+    const unsigned long long u2 = __builtin_bit_cast(unsigned long long, q[2]);
+    const unsigned long long u3 = __builtin_bit_cast(unsigned long long, q[3]);
+    const unsigned long long t = (unsigned long long)(tag & 0xFFFu) << 52;
+    g[0] = t | (u0 & M52);
+    g[1] = t | (u0 >> 52) | ((u1 << 12) & M52);
+    g[2] = t | (u1 >> 40) | ((u2 << 24) & M52);
+    g[3] = t | (u2 >> 28) | ((u3 << 36) & M52);
+    g[4] = t | (u3 >> 16);
+  }
+  __device__ static bool tag_ok(unsigned long long g, unsigned want) { return (unsigned)(g >> 52) == (want & 0xFFFu); }
+  __device__ static unsigned tag_of(unsigned long long g) { return (unsigned)(g >> 52); }
+  __device__ static void unpack(const unsigned long long (&g)[5], double (&q)[4]) {
+    const unsigned long long c0 = g[0] & M52, c1 = g[1] & M52, c2 = g[2] & M52, c3 = g[3] & M52, c4 = g[4] & M52;
+    q[0] = __builtin_bit_cast(double, c0 | (c1 << 52));
+    q[1] = __builtin_bit_cast(double, (c1 >> 12) | (c2 << 40));
+    q[2] = __builtin_bit_cast(double, (c2 >> 24) | (c3 << 28));
+    q[3] = __builtin_bit_cast(double, (c3 >> 36) | (c4 << 16));
+  }
+};
+template <> struct HX<float> {
+  static constexpr int W = 4;
+  __device__ static void pack(const float (&q)[4], unsigned tag, unsigned long long (&g)[4]) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) g[f] = ((unsigned long long)tag << 32) | __builtin_bit_cast(unsigned, q[f]);
+  }
+  __device__ static bool tag_ok(unsigned long long g, unsigned want) { return (unsigned)(g >> 32) == want; }
+  __device__ static unsigned tag_of(unsigned long long g) { return (unsigned)(g >> 32); }
+  __device__ static void unpack(const unsigned long long (&g)[4], float (&q)[4]) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) q[f] = __builtin_bit_cast(float, (unsigned)g[f]);
+  }
+};
 
 // swap a value between the lanes of a pair (2 j, 2 j + 1): DPP quad_perm
 // [1, 0, 3, 2], one v_mov_dpp per 32 bits, every lane of the wave active
@@ -528,33 +575,27 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   };
   // a window cell of another block at step xe_ > launch start, tagged hand-off
   auto load_tagged = [&](int src_, T (&q)[4], int xe_) {
-    constexpr int G = sizeof(T) / 4;
+    constexpr int HW = HX<T>::W;
     const unsigned S = (unsigned)a.S;
-    const gu64* hp = (const gu64*)a.hx + (size_t)(xe_ & 1) * (4 * G) * S + (unsigned)src_;
+    const gu64* hp = (const gu64*)a.hx + (size_t)(xe_ & 1) * HW * S + (unsigned)src_;
     const unsigned want = (unsigned)xe_ + 1u;
-    unsigned long long gr[4 * G];
+    unsigned long long gr[HW];
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
       bool ok = true;
 #pragma unroll
-      for (int k = 0; k < 4 * G; ++k) gr[k] = __hip_atomic_load(hp + (size_t)k * S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < HW; ++k) gr[k] = __hip_atomic_load(hp + (size_t)k * S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-      for (int k = 0; k < 4 * G; ++k) ok &= (unsigned)(gr[k] >> 32) == want;
+      for (int k = 0; k < HW; ++k) ok &= HX<T>::tag_ok(gr[k], want);
       if (ok) break;
       if (__hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
       if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
-        fused_fail(a.err, 2u, bid, xe_, src_, (int)(gr[0] >> 32));
+        fused_fail(a.err, 2u, bid, xe_, src_, (int)HX<T>::tag_of(gr[0]));
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      if constexpr (G == 2)
-        q[f] = __builtin_bit_cast(T, (gr[2 * f + 1] << 32) | (gr[2 * f] & 0xFFFFFFFFull));
-      else
-        q[f] = __builtin_bit_cast(T, (unsigned)gr[f]);
-    }
+    HX<T>::unpack(gr, q);
   };
   auto load_state = [&](const T* Qin, int xe_) { load_state_of(src, Q, Qin, xe_); };
   T* const buf[2] = {const_cast<T*>(a.Q), a.out};
@@ -1066,22 +1107,13 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
     unsigned so = (unsigned)src;
     asm volatile("" : "+v"(so));
     if (tagh && !last) {     // tagged granules for the next step's readers (word-major)
-      constexpr int G = sizeof(T) / 4;
-      gu64* hp = (gu64*)a.hx + (size_t)((xe + 1) & 1) * (4 * G) * S + so;
-      const unsigned long long tag = (unsigned long long)((unsigned)xe + 2u) << 32;
+      constexpr int HW = HX<T>::W;
+      gu64* hp = (gu64*)a.hx + (size_t)((xe + 1) & 1) * HW * S + so;
+      unsigned long long g[HW];
+      HX<T>::pack(Q, (unsigned)xe + 2u, g);
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        if constexpr (G == 2) {
-          const unsigned long long b = __builtin_bit_cast(unsigned long long, Q[f]);
-          __hip_atomic_store(hp + (size_t)(2 * f) * S, tag | (b & 0xFFFFFFFFull), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(hp + (size_t)(2 * f + 1) * S, tag | (b >> 32), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          __hip_atomic_store(hp + (size_t)f * S, tag | __builtin_bit_cast(unsigned, Q[f]), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
+      for (int k = 0; k < HW; ++k)
+        __hip_atomic_store(hp + (size_t)k * S, g[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (MULTI) {      // write-through: the next step's readers may sit on another XCD
 #pragma unroll
       for (int f = 0; f < 4; ++f) {

@@ -165,7 +165,7 @@ typedef struct FusedDesc {
   // word 16 bit p = pass p holds a face next to a panel-edge line
   const unsigned* sched;
   const void* nrmf;     // [nb][3][2 H1 (H1+1)] per-face normals of panel-edge blocks (component-major)
-  // tagged in-launch hand-off of a one-rank multi-step launch, [2][4 G][S] u64
+  // tagged in-launch hand-off of a multi-step launch, [2][W][S] u64 (W = 5 fp64, 4 fp32)
   // zero-initialised and kept with the epoch array; null = epoch hand-off
   void* hx;
   // per-cell producer polls of a one-rank epoch hand-off: [nb][W*W] int8

@@ -1235,7 +1235,7 @@ class FusedKernel:
         self.mem = None
         # per-block step counters (xGMI tags; waits inside a multi-step launch)
         self.tens["epoch"] = torch.zeros(nb, dtype=torch.int32, device=dev)
-        # tagged in-launch hand-off (one rank): [2 slots][4 G words][S] u64,
+        # tagged in-launch hand-off: [2 slots][W words][S] u64,
         # zero tags; lives with the epoch array, whose counts only grow, so a
         # tag a reader waits for was written in the same launch
         self.handoff = handoff_mode(B, multi_rank=X is not None)
@@ -1248,7 +1248,9 @@ class FusedKernel:
                 raise RuntimeError("STSP_FUSED_HANDOFF=tag needs a library built with STSP_FUSED_TAGH=1")
             self.handoff = "epoch"
         if self.handoff == "tag":
-            words = 4 * (torch.tensor([], dtype=e.dtype).element_size() // 4)
+            # granules per cell (fused_step.hip HX<T>::W): fp64 5 (12-bit tag +
+            # 52 payload bits each), fp32 4 (32-bit tag + value)
+            words = 5 if e.dtype == torch.float64 else 4
             self.tens["hx"] = torch.zeros(2 * words * e.plan.S, dtype=torch.int64, device=dev)
         self.tens["err"] = torch.zeros(8, dtype=torch.int32, device=dev)   # code, block, step, what, seen
         prod = producer_table(P)
@@ -1650,20 +1652,18 @@ def handoff_mode(B: int, multi_rank: bool = False) -> str:
     """In-launch hand-off of the in-rank cells of a multi-step fused launch
     with B x B blocks: "tag" (tagged granules, the data is the flag) or
     "epoch" (write-through state, drained per-block step counter, producer
-    poll).  ``STSP_FUSED_HANDOFF`` = tag / epoch / auto (default).  auto:
-    with other ranks' cells through the xGMI ring, tag at every block size
-    (loopback proxies 3-11 % faster for B = 6 .. 16); on one rank, tag for
-    B <= 8 (2-3 % faster at B = 6) and epoch above, where the tagged form's
-    doubled hand-off bytes cost 2-5 % (C96 B = 16; profiles/r6_handoff)."""
+    poll).  ``STSP_FUSED_HANDOFF`` = tag / epoch / auto (default: tag).  With
+    fp64 cells packed into 5 granules of a 12-bit tag and 52 payload bits the
+    tagged form is the faster one at every block size, one rank or several
+    (C96 B = 16: 10.7-10.8 vs 11.8-12.1 us/step in-kernel; 8-granule tags
+    lost there; profiles/r6_handoff)."""
     m = os.environ.get("STSP_FUSED_HANDOFF", "auto")
     if m not in ("tag", "epoch", "auto"):
         raise ValueError(f"STSP_FUSED_HANDOFF must be 'tag', 'epoch' or 'auto', got {m!r}")
     if m == "auto":
-        return "tag" if (multi_rank or B <= HANDOFF_TAG_MAX_B) else "epoch"
+        return "tag"
     return m
 
-
-HANDOFF_TAG_MAX_B = 8
 
 
 XG_SLOT_BITS = 24
