@@ -530,38 +530,34 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
   auto load_state_of = [&](int src, T (&Q)[4], const T* Qin, int xe_) {
     const bool loaded = src >= 0 || (XG && src <= -2);
     if (XG && src <= -2) {
-      // another rank's cell: spin on its granules in ring slot xe % SLOTS until
-      // every tag carries this step (xe + 1); a timeout sets err and falls through
-      constexpr int G = sizeof(T) / 4;
+      // another rank's cell: spin on its packed granules (HX<T>) in ring slot
+      // xe % SLOTS until every tag carries this step (xe + 1; a slot holds this
+      // step's record or the one SLOTS steps older); a timeout sets err and
+      // falls through
+      constexpr int HW = HX<T>::W;
       const gu64* rp = (const gu64*)(a.recv) + (long)(xe_ % STSP_XG_SLOTS) * a.ring;
-      const int nrec = a.ring / (4 * G), rec = -2 - src;
+      const int nrec = a.ring / HW, rec = -2 - src;
       const unsigned want = (unsigned)xe_ + 1u;
-      unsigned long long gr[4 * G];
+      unsigned long long gr[HW];
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
         bool ok = true;
         if (STSP_XG_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 #pragma unroll
-        for (int k = 0; k < 4 * G; ++k)
-          gr[k] = __hip_atomic_load(rp + ring_word(nrec, 4 * G, rec, k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int k = 0; k < HW; ++k)
+          gr[k] = __hip_atomic_load(rp + ring_word(nrec, HW, rec, k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const unsigned er = __hip_atomic_load((gu32*)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-        for (int k = 0; k < 4 * G; ++k) ok &= (unsigned)(gr[k] >> 32) == want;
+        for (int k = 0; k < HW; ++k) ok &= HX<T>::tag_ok(gr[k], want);
         if (ok) break;
         if (er != 0) break;
         if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
-          fused_fail(a.err, 1u, bid, xe_, -2 - src, (int)(gr[0] >> 32));
+          fused_fail(a.err, 1u, bid, xe_, -2 - src, (int)HX<T>::tag_of(gr[0]));
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        if constexpr (G == 2)
-          Q[f] = __builtin_bit_cast(T, (gr[2 * f + 1] << 32) | (gr[2 * f] & 0xFFFFFFFFull));
-        else
-          Q[f] = __builtin_bit_cast(T, (unsigned)gr[f]);
-      }
+      HX<T>::unpack(gr, Q);
     } else if (loaded) {
       const unsigned S = (unsigned)a.S;
       unsigned so = (unsigned)src;
@@ -1151,28 +1147,19 @@ __global__ __launch_bounds__((FD<NS, B>::NT)) void fused_step_kernel(FArgs<T> a)
         }
       }
     }
-    if constexpr (XG) {   // cells other ranks read: straight into their rings, tag xe + 2
-      constexpr int G = sizeof(T) / 4;
+    if constexpr (XG) {   // cells other ranks read: straight into their rings, packed, tag xe + 2
+      constexpr int HW = HX<T>::W;
       const int* xp = a.xpush + ((long)bid * B * B + (v - R) * B + (u - R)) * a.K;
+      unsigned long long g[HW];
+      HX<T>::pack(Q, (unsigned)xe + 2u, g);
       for (int k = 0; k < a.K; ++k) {
         const int code = xp[k];
         if (code < 0) break;
         gu64* dst = ((gu64*)(a.peer_ring[code >> 24])) + (long)((xe + 1) % STSP_XG_SLOTS) * a.ring;
-        const int nrec = a.ring / (4 * G), rec = code & 0xFFFFFF;
-        const unsigned long long tag = (unsigned long long)((unsigned)xe + 2u) << 32;
+        const int nrec = a.ring / HW, rec = code & 0xFFFFFF;
 #pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          if constexpr (G == 2) {
-            const unsigned long long b = __builtin_bit_cast(unsigned long long, Q[f]);
-            __hip_atomic_store(dst + ring_word(nrec, 8, rec, 2 * f), tag | (b & 0xFFFFFFFFull), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(dst + ring_word(nrec, 8, rec, 2 * f + 1), tag | (b >> 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-          } else {
-            __hip_atomic_store(dst + ring_word(nrec, 4, rec, f), tag | __builtin_bit_cast(unsigned, Q[f]),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
-        }
+        for (int w = 0; w < HW; ++w)
+          __hip_atomic_store(dst + ring_word(nrec, HW, rec, w), g[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }
@@ -1325,6 +1312,50 @@ extern "C" int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stre
 }
 
 // Compile-time sizes of the fused kernel (host checks): ghost entries and corner faces per block.
+// Initial delivery into the fused step's xGMI rings, packed records (HX<T>):
+// entry i stores cell src[i] of the state (F = 4 fields, stride S) into ring
+// slot epoch % SLOTS of rank code[i] >> 24, record code[i] & 0xFFFFFF, tag
+// epoch + 1.  ring: granules per slot.
+template <typename T>
+__global__ __launch_bounds__(256) void fused_prime_kernel(const T* __restrict__ q, int S,
+                                                          const int* __restrict__ src, const int* __restrict__ code,
+                                                          int nent, T* const* peer_ring, int ring, int epoch) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nent) {
+    constexpr int HW = HX<T>::W;
+    const int c = code[i];
+    T v[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) v[f] = q[(long)f * S + src[i]];
+    unsigned long long g[HW];
+    HX<T>::pack(v, (unsigned)epoch + 1u, g);
+    gu64* dst = ((gu64*)(peer_ring[c >> 24])) + (long)(epoch % STSP_XG_SLOTS) * ring;
+    const int nrec = ring / HW;
+#pragma unroll
+    for (int w = 0; w < HW; ++w)
+      __hip_atomic_store(dst + ring_word(nrec, HW, c & 0xFFFFFF, w), g[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __threadfence_system();
+}
+
+// granules per cell record of the fused step's ring and tagged hand-off
+extern "C" int stsp_fused_record_words(int dtype) { return dtype == 1 ? HX<double>::W : HX<float>::W; }
+
+extern "C" int stsp_fused_prime_launch(int dtype, const void* q, int S, const int* src, const int* code, int nent,
+                                       void* const* peer_ring, int ring, int epoch, hipStream_t stream) {
+  if (nent <= 0) return 0;
+  const dim3 grid((nent + 255) / 256), block(256);
+  if (dtype == 1)
+    hipLaunchKernelGGL(fused_prime_kernel<double>, grid, block, 0, stream, (const double*)q, S, src, code, nent,
+                       (double* const*)peer_ring, ring, epoch);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(fused_prime_kernel<float>, grid, block, 0, stream, (const float*)q, S, src, code, nent,
+                       (float* const*)peer_ring, ring, epoch);
+  else
+    return -4;
+  return (int)hipGetLastError();
+}
+
 // 1 if this library carries the tagged in-launch hand-off
 extern "C" int stsp_fused_tagh(void) { return STSP_FUSED_TAGH; }
 

@@ -176,6 +176,11 @@ typedef struct FusedDesc {
 int stsp_fused_launch(int dtype, const FusedDesc* d, hipStream_t stream);
 int stsp_fused_limits(int* gmax, int* cmax);
 int stsp_fused_tagh(void);
+// the fused step's packed cell records (granules per cell) and their initial
+// delivery into the peers' xGMI rings
+int stsp_fused_record_words(int dtype);
+int stsp_fused_prime_launch(int dtype, const void* q, int S, const int* src, const int* code, int nent,
+                            void* const* peer_ring, int ring, int epoch, hipStream_t stream);
 // Direct xGMI halo build constants: protocol (0 counters, 1 tagged granules), ring slots.
 int stsp_xg_protocol(void);
 int stsp_xg_slots(void);

@@ -1289,9 +1289,8 @@ class FusedKernel:
             raise RuntimeError("fused multi-rank step needs the tagged-granule protocol (STSP_XG_TAG=1)")
         self._xlib = L
         self.slots = int(L.stsp_xg_slots())
-        esize = torch.tensor([], dtype=e.dtype).element_size()
-        F = e.physics.F
-        self.ring = X.ring_slots * F * (esize // 4)
+        # packed cell records (fused_step.hip HX<T>): 5 granules per fp64 cell
+        self.ring = X.ring_slots * int(self.lib.stsp_fused_record_words(self.dcode))
         xpush, psrc, pcode = X.producer(e.rank)
         assert psrc.size == 0 or int(psrc.max()) < e.plan.S
         peers = sorted(set(int(c) >> XG_SLOT_BITS for c in pcode.tolist())
@@ -1391,10 +1390,10 @@ class FusedKernel:
         if dist_on:
             dist.barrier(group=self.group)      # nobody still reads the slot we are about to fill
         tn = self.tens
-        rc = self._xlib.stsp_xg_prime_launch(self.dcode, native.ptr(e.pool[0]), e.plan.S, e.physics.F,
-                                             native.ptr(tn["prime_src"]), native.ptr(tn["prime_code"]),
-                                             int(tn["prime_src"].numel()), native.ptr(tn["peer_ring"]), self.ring,
-                                             e0, native.current_stream_handle())
+        rc = self.lib.stsp_fused_prime_launch(self.dcode, native.ptr(e.pool[0]), e.plan.S,
+                                              native.ptr(tn["prime_src"]), native.ptr(tn["prime_code"]),
+                                              int(tn["prime_src"].numel()), native.ptr(tn["peer_ring"]), self.ring,
+                                              e0, native.current_stream_handle())
         torch.cuda.synchronize(e.device)
         if not agree(rc == 0, dist_on, e.device, self.group):
             raise RuntimeError(f"fused xGMI prime failed ({rc})")

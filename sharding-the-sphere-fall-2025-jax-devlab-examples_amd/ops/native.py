@@ -117,6 +117,10 @@ def load(build_if_missing: bool = True):
         L.stsp_fused_limits.restype = ci
         L.stsp_fused_tagh.argtypes = []
         L.stsp_fused_tagh.restype = ci
+        L.stsp_fused_record_words.argtypes = [ci]
+        L.stsp_fused_record_words.restype = ci
+        L.stsp_fused_prime_launch.argtypes = [ci, vp, ci, vp, vp, ci, vp, ci, ci, vp]
+        L.stsp_fused_prime_launch.restype = ci
         _declare_runtime(L)
         _declare_tt(L)
         L.stsp_schedule_spin.argtypes = [ci]

@@ -21,39 +21,44 @@ from stsphere.models.geometry import CubedSphereGrid  # noqa: E402
 from stsphere.parallel.layout import TileLayout  # noqa: E402
 
 SLOT_BITS = 24
-NW = 8          # fp64 tagged: 4 fields x 2 granules of 8 bytes
+NW = 8          # fp64 tagged, stage / march kernels: 4 fields x 2 granules of 8 bytes
+NW_FUSED = 5    # fp64 fused step (round 6): 5 granules of a 12-bit tag and 52 payload bits
 SEG = 64        # bytes per memory transaction counted
 
 
-def _segments(recs, peers, nrec, j, layout):
+def _segments(recs, peers, nrec, j, layout, nw=NW):
     if layout == "aos":
-        addr = (recs * NW + j) * 8
+        addr = (recs * NW + j) * 8          # round 5: record-major, 8 granules
     else:
-        addr = (j * nrec + recs) * 8
+        addr = (j * nrec + recs) * 8        # word-major, nw granules
     return len(set(zip(peers.tolist(), (addr // SEG).tolist())))
 
 
-def _count(waves, nrec):
+def _count(waves, nrec, nw=NW):
     """waves: list of (recs, peers) per store round (active lanes of one wave
     for one push index k).  Returns instruction and transaction counts, in
-    total and for the busiest peer (one xGMI link carries one peer pair)."""
-    out = {"records": 0, "store_instr": 0, "tx_aos": 0, "tx_soa": 0}
+    total and for the busiest peer (one xGMI link carries one peer pair):
+    tx_aos for round 5's record-major 8-granule records, tx_soa for the
+    word-major records of nw granules."""
+    out = {"records": 0, "store_instr": 0, "tx_aos": 0, "tx_soa": 0, "nw": nw}
     peer = {}
     for recs, peers in waves:
         if recs.size == 0:
             continue
         out["records"] += int(recs.size)
-        out["store_instr"] += NW
+        out["store_instr"] += nw
         for p in np.unique(peers):
             m = peers == p
             d = peer.setdefault(int(p), {"records": 0, "tx_aos": 0, "tx_soa": 0})
             d["records"] += int(m.sum())
             for j in range(NW):
                 d["tx_aos"] += _segments(recs[m], peers[m], nrec, j, "aos")
-                d["tx_soa"] += _segments(recs[m], peers[m], nrec, j, "soa")
+            for j in range(nw):
+                d["tx_soa"] += _segments(recs[m], peers[m], nrec, j, "soa", nw)
         for j in range(NW):
             out["tx_aos"] += _segments(recs, peers, nrec, j, "aos")
-            out["tx_soa"] += _segments(recs, peers, nrec, j, "soa")
+        for j in range(nw):
+            out["tx_soa"] += _segments(recs, peers, nrec, j, "soa", nw)
     out["peers"] = len(peer)
     out["busiest_peer"] = max(peer.values(), key=lambda d: d["records"]) if peer else None
     return out
@@ -76,7 +81,7 @@ def fused_row(N, t, ranks, B):
                     c = lanes[:, k]
                     c = c[c >= 0].astype(np.int64)
                     waves.append((c & ((1 << SLOT_BITS) - 1), c >> SLOT_BITS))
-        per.append(_count(waves, nrec))
+        per.append(_count(waves, nrec, NW_FUSED))
     return {"path": "fused", "N": N, "t": t, "ranks": ranks, "B": B, "ring_records_per_slot": nrec}, per
 
 
@@ -117,7 +122,7 @@ def main():
         else:
             head, per = march_row(*(int(x) for x in f[1:4]))
         mx = max(per, key=lambda d: d["records"])
-        row = dict(head, max_rank={**mx, "ring_bytes": mx["records"] * NW * 8, "payload_bytes": mx["records"] * 32,
+        row = dict(head, max_rank={**mx, "ring_bytes": mx["records"] * mx["nw"] * 8, "payload_bytes": mx["records"] * 32,
                                    "tx_per_instr_aos": mx["tx_aos"] / max(1, mx["store_instr"]),
                                    "tx_per_instr_soa": mx["tx_soa"] / max(1, mx["store_instr"])},
                    total_records=sum(d["records"] for d in per))
